@@ -1,0 +1,105 @@
+// Device building blocks shared by the SpMM-family kernels (spmm.hip, dense_epi.hip):
+// the sequential-order CSR row gather and the GAS row transform.
+//
+// Mapping (d = 4*GROUP): a destination row is owned by GROUP consecutive lanes of a 64-wide
+// wavefront, each lane owning 4 consecutive features (one float4). A wave therefore carries
+// 64/GROUP rows (d=64: 16 lanes/row, 4 rows/wave) and every neighbour gather is one coalesced
+// 4*d-byte row read issued as global_load_dwordx4 by the row's lanes. Neighbour (col,val)
+// pairs are fetched cooperatively, kChunk per step, and broadcast inside the group with
+// __shfl; the kChunk row gathers of a step are all issued before the first FMA, so kChunk
+// independent 16-B loads per lane are in flight. FMAs are applied in k order per lane, so
+// splitting the loads never changes the arithmetic (bit-exact with the reference).
+#pragma once
+
+#include "common.h"
+
+namespace gnnrec {
+
+constexpr int kBlock = 256;  // 4 waves per workgroup
+constexpr int kChunk = 16;   // neighbours per gather step
+
+__device__ __forceinline__ float4 fma4(float v, const float4& x, const float4& a) {
+  return make_float4(__builtin_fmaf(v, x.x, a.x), __builtin_fmaf(v, x.y, a.y),
+                     __builtin_fmaf(v, x.z, a.z), __builtin_fmaf(v, x.w, a.w));
+}
+
+__device__ __forceinline__ float4 ld4(const float* p) {
+  return *reinterpret_cast<const float4*>(p);
+}
+__device__ __forceinline__ void st4(float* p, const float4& v) {
+  *reinterpret_cast<float4*>(p) = v;
+}
+
+// One gather step of CH neighbours [k0, k0+CH) of a row ending at `end`. TAIL selects the
+// FMA of out-of-row slots away (their loads are clamped to the row's last element).
+template <int GROUP, bool TAIL>
+__device__ __forceinline__ void gather_step(const int32_t* __restrict__ col,
+                                            const float* __restrict__ val, int64_t k0,
+                                            int64_t end, const float* __restrict__ x,
+                                            int64_t ldx, int gl, float4& a) {
+  constexpr int PER = (GROUP >= kChunk) ? 1 : kChunk / GROUP;  // pairs loaded per lane
+  int cm[PER];
+  float vm[PER];
+#pragma unroll
+  for (int m = 0; m < PER; ++m) {
+    int64_t k = k0 + gl + (int64_t)m * GROUP;
+    if (TAIL) k = k < end ? k : end - 1;
+    if (GROUP >= kChunk && gl >= kChunk) k = k0;  // idle lanes: any in-row address
+    cm[m] = __builtin_nontemporal_load(col + k);
+    vm[m] = __builtin_nontemporal_load(val + k);
+  }
+  float4 xv[kChunk];
+#pragma unroll
+  for (int t = 0; t < kChunk; ++t) {
+    const int c = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
+    xv[t] = ld4(x + (int64_t)c * ldx + 4 * gl);
+  }
+#pragma unroll
+  for (int t = 0; t < kChunk; ++t) {
+    const float v = __shfl(vm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
+    const float4 n = fma4(v, xv[t], a);
+    if (TAIL) {
+      const bool ok = (k0 + t) < end;
+      a.x = ok ? n.x : a.x;
+      a.y = ok ? n.y : a.y;
+      a.z = ok ? n.z : a.z;
+      a.w = ok ? n.w : a.w;
+    } else {
+      a = n;
+    }
+  }
+}
+
+// Sequential-order row reduction: returns the lane's float4 slice of (A x)[r].
+template <int GROUP>
+__device__ __forceinline__ float4 gather_row(const int32_t* __restrict__ col,
+                                             const float* __restrict__ val, int64_t beg,
+                                             int64_t end, const float* __restrict__ x,
+                                             int64_t ldx, int gl) {
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  int64_t k0 = beg;
+  for (; k0 + kChunk <= end; k0 += kChunk) gather_step<GROUP, false>(col, val, k0, end, x, ldx, gl, a);
+  if (k0 < end) gather_step<GROUP, true>(col, val, k0, end, x, ldx, gl, a);
+  return a;
+}
+
+// ---- GAS (block-diagonal orthogonal transform + column shuffle) -----------------------
+// y[r, j] = sum_{c<bs} z[r, bs*b + c] * W_b[c, e],  perm[j] = bs*b + e  (sequential fmaf in c).
+// The row z is parked in LDS so every lane can read the bs inputs of its 4 outputs.
+template <int D>
+__device__ __forceinline__ float4 gas_row(const float* zrow_lds, const float* w_lds, int bs,
+                                          const int (&pj)[4]) {
+  float o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int b = pj[q] / bs, e = pj[q] - b * bs;
+    const float* z = zrow_lds + b * bs;
+    const float* w = w_lds + (b * bs) * bs + e;
+    float s = 0.f;
+    for (int c = 0; c < bs; ++c) s = __builtin_fmaf(z[c], w[c * bs], s);
+    o[q] = s;
+  }
+  return make_float4(o[0], o[1], o[2], o[3]);
+}
+
+}  // namespace gnnrec

@@ -1,0 +1,243 @@
+// Normalised-adjacency SpMM over a CSR destination-row operand, gfx950 (MI355X).
+//
+// Replaces torch.sparse.mm(adj, x) of the reference (baselines/lightgcn.py:88,178,
+// baselines/ngcf.py:70, orthogonal_bundle/model.py:172,184,333,344). The reference CPU kernel
+// (ATen sparse addmm on the row-sorted COO) computes, per destination row r and feature f,
+//     y[r,f] = fmaf(val_k, x[col_k, f], y[r,f])  for k over the row in ascending column order,
+// starting from +0.0f. That order is reproduced exactly here, so results are bit-identical.
+//
+// Row mapping and load pipelining: see gather.h.
+#include "gather.h"
+
+namespace gnnrec {
+
+// LightGCN layer-mean epilogue (see GNNREC_EPI_* in gnnrec.h).
+__device__ __forceinline__ void acc_epilogue(int epi, const float4& y, const float* self_row,
+                                             float* acc_row, float acc_div) {
+  if (!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD))) return;
+  float4 b = (epi & GNNREC_EPI_ACC_INIT) ? ld4(self_row) : ld4(acc_row);
+  b.x = b.x + y.x;
+  b.y = b.y + y.y;
+  b.z = b.z + y.z;
+  b.w = b.w + y.w;
+  if (epi & GNNREC_EPI_ACC_DIV) {
+    b.x = b.x / acc_div;
+    b.y = b.y / acc_div;
+    b.z = b.z / acc_div;
+    b.w = b.w / acc_div;
+  }
+  st4(acc_row, b);
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void spmm_vec4_kernel(
+    Csr A, const float* __restrict__ x, int64_t ldx, float* __restrict__ y, int64_t ldy,
+    int epi, const float* __restrict__ self, int64_t ld_self, float* __restrict__ acc,
+    int64_t ld_acc, float acc_div) {
+  constexpr int GROUP = D / 4;
+  constexpr int RPW = 64 / GROUP;
+  const int lane = threadIdx.x & 63;
+  const int gl = lane % GROUP;
+  const int64_t r =
+      ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
+  if (r >= A.n_rows) return;  // the whole group leaves together
+  const int64_t beg = A.row_ptr[r], end = A.row_ptr[r + 1];
+  const float4 a = gather_row<GROUP>(A.col, A.val, beg, end, x, ldx, gl);
+  if (!(epi & GNNREC_EPI_NO_Y)) st4(y + r * ldy + 4 * gl, a);
+  acc_epilogue(epi, a, self + r * ld_self + 4 * gl, acc + r * ld_acc + 4 * gl, acc_div);
+}
+
+// Any-d fallback: one wave per row, lanes stride the features (same k order per feature).
+__global__ __launch_bounds__(kBlock) void spmm_generic_kernel(
+    Csr A, const float* __restrict__ x, int64_t ldx, float* __restrict__ y, int64_t ldy,
+    int d, int epi, const float* __restrict__ self, int64_t ld_self, float* __restrict__ acc,
+    int64_t ld_acc, float acc_div) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (r >= A.n_rows) return;
+  const int64_t beg = A.row_ptr[r], end = A.row_ptr[r + 1];
+  for (int f = lane; f < d; f += 64) {
+    float a = 0.f;
+    for (int64_t k = beg; k < end; ++k) a = __builtin_fmaf(A.val[k], x[(int64_t)A.col[k] * ldx + f], a);
+    if (!(epi & GNNREC_EPI_NO_Y)) y[r * ldy + f] = a;
+    if (epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) {
+      float b = (epi & GNNREC_EPI_ACC_INIT) ? self[r * ld_self + f] : acc[r * ld_acc + f];
+      b = b + a;
+      if (epi & GNNREC_EPI_ACC_DIV) b = b / acc_div;
+      acc[r * ld_acc + f] = b;
+    }
+  }
+}
+
+// MODE 0: standalone GAS of x rows. MODE 1: GAS(A x) (fused hop epilogue).
+template <int D, int MODE>
+__global__ __launch_bounds__(kBlock) void gas_kernel(Csr A, const float* __restrict__ x,
+                                                     int64_t ldx, float* __restrict__ y,
+                                                     int64_t ldy, int bs,
+                                                     const float* __restrict__ blocks,
+                                                     const int32_t* __restrict__ perm) {
+  constexpr int GROUP = D / 4;
+  constexpr int RPW = 64 / GROUP;
+  constexpr int ROWS = RPW * (kBlock / 64);
+  __shared__ float w_lds[D * 32];         // d/bs blocks of bs*bs (bs <= 32)
+  __shared__ float z_lds[ROWS][D + 4];
+  const int lane = threadIdx.x & 63;
+  const int gl = lane % GROUP;
+  const int slot = (threadIdx.x >> 6) * RPW + lane / GROUP;
+  for (int i = threadIdx.x; i < D * bs; i += kBlock) w_lds[i] = blocks[i];
+  int pj[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) pj[q] = perm[4 * gl + q];
+  const int64_t r = (int64_t)blockIdx.x * ROWS + slot;
+  const bool valid = r < A.n_rows;
+  float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (valid) {
+    if (MODE == 0) {
+      z = ld4(x + r * ldx + 4 * gl);
+    } else {
+      z = gather_row<GROUP>(A.col, A.val, A.row_ptr[r], A.row_ptr[r + 1], x, ldx, gl);
+    }
+  }
+  st4(&z_lds[slot][4 * gl], z);
+  __syncthreads();
+  if (valid) st4(y + r * ldy + 4 * gl, gas_row<D>(&z_lds[slot][0], w_lds, bs, pj));
+}
+
+}  // namespace gnnrec
+
+using namespace gnnrec;
+
+namespace {
+
+template <int D>
+void launch_spmm_vec4(const Csr& A, const float* x, int64_t ldx, float* y, int64_t ldy, int epi,
+                      const float* self, int64_t ld_self, float* acc, int64_t ld_acc,
+                      float acc_div, hipStream_t s) {
+  constexpr int RPB = (64 / (D / 4)) * (kBlock / 64);
+  const int64_t grid = ceil_div(A.n_rows, RPB);
+  hipLaunchKernelGGL(spmm_vec4_kernel<D>, dim3((unsigned)grid), dim3(kBlock), 0, s, A, x, ldx,
+                     y, ldy, epi, self, ld_self, acc, ld_acc, acc_div);
+}
+
+bool vec4_ok(int d, const float* x, int64_t ldx, const float* y, int64_t ldy, int epi,
+             const float* self, int64_t ld_self, const float* acc, int64_t ld_acc) {
+  if (!(d == 8 || d == 16 || d == 32 || d == 64 || d == 128 || d == 256)) return false;
+  if (!aligned16(x) || (ldx & 3)) return false;
+  if (!(epi & GNNREC_EPI_NO_Y) && (!aligned16(y) || (ldy & 3))) return false;
+  if ((epi & GNNREC_EPI_ACC_INIT) && (!aligned16(self) || (ld_self & 3))) return false;
+  if ((epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) && (!aligned16(acc) || (ld_acc & 3)))
+    return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" int gnnrec_spmm_csr_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
+                                   int64_t n_rows, const float* x, int64_t ldx, float* y,
+                                   int64_t ldy, int32_t d, int32_t epi, const float* self,
+                                   int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
+                                   gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(n_rows >= 0 && d >= 1, "spmm: bad sizes n_rows=%lld d=%d", (long long)n_rows, d);
+  if (n_rows == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(row_ptr && x, "spmm: null row_ptr/x");
+  GNNREC_REQUIRE(ldx >= d, "spmm: ldx < d");
+  GNNREC_REQUIRE((epi & GNNREC_EPI_NO_Y) || (y && ldy >= d), "spmm: null y or ldy < d");
+  GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_INIT) || (self && ld_self >= d), "spmm: ACC_INIT needs self");
+  GNNREC_REQUIRE(!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) || (acc && ld_acc >= d),
+                 "spmm: ACC needs acc");
+  GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_DIV) || (epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)),
+                 "spmm: ACC_DIV without ACC_INIT/ACC_ADD");
+  const Csr A{row_ptr, col, val, n_rows};
+  hipStream_t s = as_hip(stream);
+  if (vec4_ok(d, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc)) {
+    switch (d) {
+      case 8: launch_spmm_vec4<8>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, s); break;
+      case 16: launch_spmm_vec4<16>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, s); break;
+      case 32: launch_spmm_vec4<32>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, s); break;
+      case 64: launch_spmm_vec4<64>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, s); break;
+      case 128: launch_spmm_vec4<128>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, s); break;
+      default: launch_spmm_vec4<256>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, s); break;
+    }
+  } else {
+    const int64_t grid = ceil_div(n_rows, kBlock / 64);
+    hipLaunchKernelGGL(spmm_generic_kernel, dim3((unsigned)grid), dim3(kBlock), 0, s, A, x, ldx,
+                       y, ldy, d, epi, self, ld_self, acc, ld_acc, acc_div);
+  }
+  return check_launch("spmm");
+}
+
+extern "C" int gnnrec_lightgcn_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
+                                   int64_t n_rows, const float* x0, int32_t d, int32_t n_layers,
+                                   float* work0, float* work1, float* layers, float* out,
+                                   int64_t ld_out, gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(n_layers >= 0 && d >= 1 && n_rows >= 0, "lightgcn: bad sizes");
+  GNNREC_REQUIRE(x0 && out && ld_out >= d, "lightgcn: null x0/out");
+  GNNREC_REQUIRE(layers || n_layers <= 1 || (work0 && work1), "lightgcn: need work0/work1 or layers");
+  if (n_rows == 0) return GNNREC_OK;
+  hipStream_t s = as_hip(stream);
+  if (n_layers == 0) {  // mean of a single layer is the layer itself
+    if (hipMemcpy2DAsync(out, ld_out * sizeof(float), x0, d * sizeof(float), d * sizeof(float),
+                         n_rows, hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return check_launch("lightgcn copy");
+    return GNNREC_OK;
+  }
+  const float* in = x0;
+  for (int k = 1; k <= n_layers; ++k) {
+    float* yk = layers ? layers + (int64_t)(k - 1) * n_rows * d : ((k & 1) ? work0 : work1);
+    int epi = (k == 1) ? GNNREC_EPI_ACC_INIT : GNNREC_EPI_ACC_ADD;
+    if (k == n_layers) {
+      epi |= GNNREC_EPI_ACC_DIV;
+      if (!layers) epi |= GNNREC_EPI_NO_Y;
+    }
+    const int rc = gnnrec_spmm_csr_f32(row_ptr, col, val, n_rows, in, d, yk, d, d, epi, x0, d, out,
+                                       ld_out, (float)(n_layers + 1), stream);
+    if (rc != GNNREC_OK) return rc;
+    in = yk;
+  }
+  return GNNREC_OK;
+}
+
+namespace {
+template <int D, int MODE>
+void launch_gas(const Csr& A, const float* x, int64_t ldx, float* y, int64_t ldy, int bs,
+                const float* blocks, const int32_t* perm, hipStream_t s) {
+  constexpr int ROWS = (64 / (D / 4)) * (kBlock / 64);
+  hipLaunchKernelGGL((gas_kernel<D, MODE>), dim3((unsigned)ceil_div(A.n_rows, ROWS)), dim3(kBlock),
+                     0, s, A, x, ldx, y, ldy, bs, blocks, perm);
+}
+
+template <int MODE>
+int gas_dispatch(const Csr& A, const float* x, int64_t ldx, float* y, int64_t ldy, int d, int bs,
+                 const float* blocks, const int32_t* perm, hipStream_t s) {
+  GNNREC_REQUIRE(bs >= 1 && bs <= 32 && d % bs == 0, "gas: block size %d must divide d=%d and be <= 32", bs, d);
+  GNNREC_REQUIRE(aligned16(x) && aligned16(y) && !(ldx & 3) && !(ldy & 3), "gas: x/y must be 16-B aligned with ld %% 4 == 0");
+  GNNREC_REQUIRE(blocks && perm, "gas: null blocks/perm");
+  switch (d) {
+    case 16: launch_gas<16, MODE>(A, x, ldx, y, ldy, bs, blocks, perm, s); break;
+    case 32: launch_gas<32, MODE>(A, x, ldx, y, ldy, bs, blocks, perm, s); break;
+    case 64: launch_gas<64, MODE>(A, x, ldx, y, ldy, bs, blocks, perm, s); break;
+    case 128: launch_gas<128, MODE>(A, x, ldx, y, ldy, bs, blocks, perm, s); break;
+    default: set_error("gas: d=%d unsupported (16, 32, 64, 128)", d); return GNNREC_EUNSUPPORTED;
+  }
+  return check_launch("gas");
+}
+}  // namespace
+
+extern "C" int gnnrec_gas_f32(const float* x, int64_t ldx, int64_t n_rows, int32_t d, int32_t bs,
+                              const float* blocks, const int32_t* perm, float* y, int64_t ldy,
+                              gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(n_rows >= 0 && x && y && ldx >= d && ldy >= d, "gas: bad args");
+  if (n_rows == 0) return GNNREC_OK;
+  const Csr A{nullptr, nullptr, nullptr, n_rows};
+  return gas_dispatch<0>(A, x, ldx, y, ldy, d, bs, blocks, perm, as_hip(stream));
+}
+
+extern "C" int gnnrec_spmm_gas_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
+                                   int64_t n_rows, const float* x, int64_t ldx, float* y,
+                                   int64_t ldy, int32_t d, int32_t bs, const float* blocks,
+                                   const int32_t* perm, gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(n_rows >= 0 && row_ptr && x && y && ldx >= d && ldy >= d, "spmm_gas: bad args");
+  if (n_rows == 0) return GNNREC_OK;
+  const Csr A{row_ptr, col, val, n_rows};
+  return gas_dispatch<1>(A, x, ldx, y, ldy, d, bs, blocks, perm, as_hip(stream));
+}

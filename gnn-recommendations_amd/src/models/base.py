@@ -1,0 +1,52 @@
+"""BaseRecommender: the model API the drop-in keeps (reference: src/models/base.py:15-122).
+
+Subclasses implement ``forward(adj_matrix) -> (user_emb, item_emb)``, ``predict`` and
+``get_all_embeddings``; the defaults below raise like the reference does.
+"""
+from typing import Tuple
+
+import torch
+import torch.nn as nn
+
+
+class BaseRecommender(nn.Module):
+    """Common base of every recommender (n_users, n_items, embedding_dim bookkeeping)."""
+
+    def __init__(self, n_users: int, n_items: int, embedding_dim: int):
+        super().__init__()
+        self.n_users = n_users
+        self.n_items = n_items
+        self.embedding_dim = embedding_dim
+
+    def _unimplemented(self, what: str):
+        raise NotImplementedError(f"{what}() must be implemented by {type(self).__name__}")
+
+    def forward(self, *args, **kwargs):
+        self._unimplemented("forward")
+
+    def predict(self, users: torch.Tensor, items: torch.Tensor) -> torch.Tensor:
+        self._unimplemented("predict")
+
+    def get_all_embeddings(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        self._unimplemented("get_all_embeddings")
+
+    def get_parameters_count(self) -> int:
+        return sum(p.numel() for p in self.parameters() if p.requires_grad)
+
+    def reset_parameters(self):
+        """Default init (base.py:108-122): N(0, 0.01) embeddings, xavier Linear, zero bias."""
+        for m in self.modules():
+            if isinstance(m, nn.Embedding):
+                nn.init.normal_(m.weight, mean=0.0, std=0.01)
+            elif isinstance(m, nn.Linear):
+                nn.init.xavier_uniform_(m.weight)
+                if m.bias is not None:
+                    nn.init.zeros_(m.bias)
+
+    # helpers shared by the graph models --------------------------------------------------
+    def _initial_table(self) -> torch.Tensor:
+        """x0 = cat(user_embedding, item_embedding) -> [N, d]."""
+        return torch.cat([self.user_embedding.weight, self.item_embedding.weight], dim=0)
+
+    def _score_pairs(self, user_emb, item_emb, users, items) -> torch.Tensor:
+        return (user_emb[users] * item_emb[items]).sum(dim=1)

@@ -1,0 +1,112 @@
+"""ctypes binding of libgnnrec.so (the C ABI declared in include/gnnrec.h).
+
+The library is the ONLY compute path for tensors on a ROCm device: there is no eager or
+CPU fallback behind these functions. If the shared object is missing or does not export
+the expected ABI version, :func:`lib` raises :class:`NativeLibraryError`.
+
+torch must be imported before the library is loaded so that libgnnrec resolves
+``libamdhip64.so.7`` to the HIP runtime torch already mapped (one runtime, shared streams).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (load order: torch's HIP runtime first)
+
+_PKG_ROOT = Path(__file__).resolve().parents[2]
+LIB_PATH = Path(os.environ.get("GNNREC_LIB", _PKG_ROOT / "lib" / "libgnnrec.so"))
+ABI_VERSION = 1
+
+# gnnrec.h epilogue flags
+EPI_ACC_INIT = 1
+EPI_ACC_ADD = 2
+EPI_ACC_DIV = 4
+EPI_NO_Y = 8
+
+_p = C.c_void_p
+_i64 = C.c_int64
+_i32 = C.c_int32
+_f32 = C.c_float
+
+# name -> argtypes (all return int status unless listed in _RESTYPES)
+_SIGNATURES = {
+    "gnnrec_version": [],
+    "gnnrec_abi_version": [],
+    "gnnrec_last_error": [],
+    "gnnrec_spmm_csr_f32": [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i32, _i32, _p, _i64, _p,
+                            _i64, _f32, _p],
+    "gnnrec_lightgcn_f32": [_p, _p, _p, _i64, _p, _i32, _i32, _p, _p, _p, _p, _i64, _p],
+    "gnnrec_gas_f32": [_p, _i64, _i64, _i32, _i32, _p, _p, _p, _i64, _p],
+    "gnnrec_spmm_gas_f32": [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i32, _i32, _p, _p, _p],
+    "gnnrec_spmm_ngcf_f32": [_p, _p, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _i32, _p, _p, _p,
+                             _p, _f32, _p, _p, _i32, _p],
+    "gnnrec_spmm_dense_f32": [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i32, _p, _f32, _p, _i64,
+                              _f32, _p, _i64, _i32, _f32, _f32, _p],
+    "gnnrec_gat_aggregate_f32": [_p, _p, _i64, _p, _i64, _p, _p, _i32, _i32, _f32, _i32, _p,
+                                 _i64, _p],
+    "gnnrec_score_topk_f32": [_p, _i64, _i64, _p, _i64, _i64, _i32, _p, _p, _i32, _p, _p, _p],
+    "gnnrec_build_bipartite_csr": [_p, _p, _i64, _i64, _i64, _i32, _p, _p, _p, _p, _p, _i32],
+    "gnnrec_normalize_values": [_p, _p, _p, _i64, _p, _i32, _p, _i32],
+}
+_RESTYPES = {"gnnrec_version": C.c_char_p, "gnnrec_last_error": C.c_char_p,
+             "gnnrec_abi_version": C.c_int}
+
+EXPORTED = tuple(_SIGNATURES)
+
+
+class NativeLibraryError(RuntimeError):
+    """libgnnrec.so is missing, stale, or a call into it failed."""
+
+
+_LIB = None
+
+
+def lib() -> C.CDLL:
+    """Load (once) and return the bound library; raises NativeLibraryError if unusable."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not LIB_PATH.exists():
+        raise NativeLibraryError(
+            f"{LIB_PATH} not found: build it with `python gnn-recommendations_amd/build_native.py` "
+            "(or __graft_entry__.build()). There is no fallback path.")
+    try:
+        handle = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
+    except OSError as e:
+        raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+    for name, argtypes in _SIGNATURES.items():
+        try:
+            fn = getattr(handle, name)
+        except AttributeError as e:
+            raise NativeLibraryError(f"{LIB_PATH} does not export {name}") from e
+        fn.argtypes = argtypes
+        fn.restype = _RESTYPES.get(name, C.c_int)
+    abi = handle.gnnrec_abi_version()
+    if abi != ABI_VERSION:
+        raise NativeLibraryError(f"{LIB_PATH} has ABI {abi}, expected {ABI_VERSION}: rebuild it")
+    _LIB = handle
+    return handle
+
+
+def check(rc: int, what: str) -> None:
+    """Raise with the library's thread-local message when a call returned non-zero."""
+    if rc != 0:
+        msg = lib().gnnrec_last_error().decode(errors="replace")
+        kind = {-1: ValueError, -3: NotImplementedError}.get(rc, NativeLibraryError)
+        raise kind(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t) -> int:
+    """Device/host address of a tensor (0 for None)."""
+    return 0 if t is None else t.data_ptr()
+
+
+def stream_of(device: torch.device) -> int:
+    """The current torch stream on `device` as a raw hipStream_t (int)."""
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def version() -> str:
+    return lib().gnnrec_version().decode()

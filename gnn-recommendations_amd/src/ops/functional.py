@@ -1,0 +1,215 @@
+"""Torch-facing ops over libgnnrec (device tensors only; no fallback path).
+
+Every function here takes a :class:`CsrGraph` on a ROCm device and fp32 row-major tables on
+the same device, launches on torch's current stream, and raises if the native library is
+unavailable. Autograd: the SpMM and the fused LightGCN propagation are differentiable
+(backward = the same kernel over A^T, which is A itself for the symmetric normalisation,
+SURVEY §2.1); the fused NGCF / GAS / OrthogonalBundle kernels are inference kernels and the
+models use them only when no gradient is required.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT, EPI_NO_Y, check, ptr
+from .graph import CsrGraph
+
+
+def _require_device(adj: CsrGraph, *tensors: torch.Tensor) -> None:
+    if adj.device.type != "cuda":
+        raise ValueError(f"libgnnrec ops need the operand on a ROCm device, got {adj.device}")
+    for t in tensors:
+        if t is None:
+            continue
+        if t.device != adj.device:
+            raise ValueError(f"tensor on {t.device}, operand on {adj.device}")
+        if t.dtype != torch.float32:
+            raise TypeError(f"expected float32, got {t.dtype}")
+        if t.dim() != 2 or t.stride(1) != 1:
+            raise ValueError("expected a 2-D row-major table (stride(1) == 1)")
+
+
+def _rowmajor(t: torch.Tensor) -> torch.Tensor:
+    return t if (t.dim() == 2 and t.stride(1) == 1 and t.stride(0) % 4 == 0) else t.contiguous()
+
+
+def _csr_args(adj: CsrGraph):
+    return ptr(adj.row_ptr), ptr(adj.col), ptr(adj.val), adj.n_rows
+
+
+# ---- raw launches (no autograd) ---------------------------------------------------------
+def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi: int = 0,
+              self_rows: Optional[torch.Tensor] = None, acc: Optional[torch.Tensor] = None,
+              acc_div: float = 1.0) -> None:
+    """y = A x with an optional fused layer-mean epilogue (gnnrec_spmm_csr_f32)."""
+    _require_device(adj, x, y, self_rows, acc)
+    d = x.shape[1]
+    if x.shape[0] < adj.shape[1]:
+        raise ValueError(f"x has {x.shape[0]} rows, operand has {adj.shape[1]} columns")
+    L = _lib.lib()
+    check(L.gnnrec_spmm_csr_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(y),
+                                y.stride(0) if y is not None else d, d, epi, ptr(self_rows),
+                                self_rows.stride(0) if self_rows is not None else d, ptr(acc),
+                                acc.stride(0) if acc is not None else d, float(acc_div),
+                                _lib.stream_of(adj.device)), "gnnrec_spmm_csr_f32")
+
+
+def spmm_forward(adj: CsrGraph, x: torch.Tensor) -> torch.Tensor:
+    x = _rowmajor(x)
+    y = torch.empty((adj.n_rows, x.shape[1]), dtype=torch.float32, device=x.device)
+    spmm_into(adj, x, y)
+    return y
+
+
+def lightgcn_forward(adj: CsrGraph, x0: torch.Tensor, n_layers: int,
+                     return_layers: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """out = mean(x0, A x0, ..., A^K x0); optionally the K hop outputs [K, N, d]."""
+    x0 = x0.contiguous()
+    _require_device(adj, x0)
+    n, d = x0.shape
+    if adj.n_rows != n or adj.shape[1] != n:
+        raise ValueError("LightGCN propagation needs a square operand matching x0")
+    out = torch.empty_like(x0)
+    layers = work0 = work1 = None
+    if return_layers:
+        layers = torch.empty((n_layers, n, d), dtype=torch.float32, device=x0.device)
+    elif n_layers > 1:
+        work0 = torch.empty_like(x0)
+        work1 = torch.empty_like(x0)
+    elif n_layers == 1:
+        work0 = work1 = torch.empty_like(x0)
+    L = _lib.lib()
+    check(L.gnnrec_lightgcn_f32(*_csr_args(adj), ptr(x0), d, int(n_layers), ptr(work0),
+                                ptr(work1), ptr(layers), ptr(out), d, _lib.stream_of(adj.device)),
+          "gnnrec_lightgcn_f32")
+    return out, layers
+
+
+# ---- autograd ------------------------------------------------------------------------------
+class _SpMM(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, adj: CsrGraph, x: torch.Tensor):
+        ctx.adj = adj
+        return spmm_forward(adj, x)
+
+    @staticmethod
+    def backward(ctx, g):
+        adj: CsrGraph = ctx.adj
+        if adj.shard_info is not None:
+            raise NotImplementedError("backward through a row shard: use ops.distributed")
+        return None, spmm_forward(adj.t(), g.contiguous())
+
+
+def spmm(adj: CsrGraph, x: torch.Tensor) -> torch.Tensor:
+    """Drop-in for torch.sparse.mm(adj_matrix, x) with a CsrGraph operand (bit-exact)."""
+    return _SpMM.apply(adj, x)
+
+
+class _LightGCN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, adj: CsrGraph, x0: torch.Tensor, n_layers: int):
+        ctx.adj, ctx.n_layers = adj, n_layers
+        out, _ = lightgcn_forward(adj, x0, n_layers)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        # d/dx0 of mean_k A^k x0 is mean_k (A^T)^k g: the same propagation over A^T.
+        gx, _ = lightgcn_forward(ctx.adj.t(), g.contiguous(), ctx.n_layers)
+        return None, gx, None
+
+
+def lightgcn_propagate(adj: CsrGraph, x0: torch.Tensor, n_layers: int) -> torch.Tensor:
+    """Fused K-hop LightGCN propagation + layer mean (lightgcn.py:76-95), differentiable."""
+    return _LightGCN.apply(adj, x0, int(n_layers))
+
+
+# ---- fused inference kernels ----------------------------------------------------------
+def gas(x: torch.Tensor, blocks: torch.Tensor, perm: torch.Tensor) -> torch.Tensor:
+    """GroupShuffleLayer forward: (x @ blockdiag(blocks))[:, perm] (gnnrec_gas_f32)."""
+    x = _rowmajor(x)
+    nb, bs, _ = blocks.shape
+    d = x.shape[1]
+    if nb * bs != d:
+        raise ValueError("blocks do not tile the feature dimension")
+    if x.device.type != "cuda":
+        raise ValueError("gas needs a ROCm device tensor")
+    y = torch.empty_like(x, memory_format=torch.contiguous_format)
+    b = blocks.detach().to(x.device, torch.float32).contiguous()
+    p = perm.to(x.device, torch.int32).contiguous()
+    check(_lib.lib().gnnrec_gas_f32(ptr(x), x.stride(0), x.shape[0], d, bs, ptr(b), ptr(p),
+                                    ptr(y), d, _lib.stream_of(x.device)), "gnnrec_gas_f32")
+    return y
+
+
+def spmm_gas(adj: CsrGraph, x: torch.Tensor, blocks: torch.Tensor,
+             perm: torch.Tensor) -> torch.Tensor:
+    """GAS(A x) in one kernel."""
+    x = _rowmajor(x)
+    _require_device(adj, x)
+    nb, bs, _ = blocks.shape
+    d = x.shape[1]
+    y = torch.empty((adj.n_rows, d), dtype=torch.float32, device=x.device)
+    b = blocks.detach().to(x.device, torch.float32).contiguous()
+    p = perm.to(x.device, torch.int32).contiguous()
+    check(_lib.lib().gnnrec_spmm_gas_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(y), d, d, bs,
+                                         ptr(b), ptr(p), _lib.stream_of(adj.device)),
+          "gnnrec_spmm_gas_f32")
+    return y
+
+
+def ngcf_layer(adj: CsrGraph, x: torch.Tensor, W1: torch.Tensor, b1: torch.Tensor,
+               W2: torch.Tensor, b2: torch.Tensor, slope: float = 0.2,
+               x_self: Optional[torch.Tensor] = None,
+               gas_blocks: Optional[torch.Tensor] = None,
+               gas_perm: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """NGCFLayer.forward in eval mode (ngcf.py:69-84), optionally followed by GAS."""
+    x = _rowmajor(x)
+    if x_self is None:
+        x_self = x
+    _require_device(adj, x, x_self)
+    d = x.shape[1]
+    if W1.shape != (d, d) or W2.shape != (d, d):
+        raise NotImplementedError("fused NGCF kernel needs square d x d Linear layers")
+    y = torch.empty((adj.n_rows, d), dtype=torch.float32, device=x.device)
+    dev = x.device
+    w1 = W1.detach().to(dev, torch.float32).contiguous()
+    w2 = W2.detach().to(dev, torch.float32).contiguous()
+    bb1 = b1.detach().to(dev, torch.float32).contiguous()
+    bb2 = b2.detach().to(dev, torch.float32).contiguous()
+    gb = gp = None
+    bs = 0
+    if gas_blocks is not None:
+        gb = gas_blocks.detach().to(dev, torch.float32).contiguous()
+        gp = gas_perm.to(dev, torch.int32).contiguous()
+        bs = gb.shape[1]
+    check(_lib.lib().gnnrec_spmm_ngcf_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(x_self),
+                                          x_self.stride(0), ptr(y), d, d, ptr(w1), ptr(bb1),
+                                          ptr(w2), ptr(bb2), float(slope), ptr(gb), ptr(gp), bs,
+                                          _lib.stream_of(adj.device)), "gnnrec_spmm_ngcf_f32")
+    return y
+
+
+def dense_layer(adj: CsrGraph, x: torch.Tensor, M: torch.Tensor, c_out: float,
+                resid: torch.Tensor, c_res: float, *, y: Optional[torch.Tensor] = None,
+                acc: Optional[torch.Tensor] = None, acc_mode: int = 0, w_out: float = 0.0,
+                w_res: float = 0.0, store_y: bool = True) -> Optional[torch.Tensor]:
+    """c_out * ((A x) @ M) + c_res * resid, with the optional fused layer sum into `acc`."""
+    x = _rowmajor(x)
+    resid = _rowmajor(resid)
+    _require_device(adj, x, resid, acc)
+    d = x.shape[1]
+    if store_y and y is None:
+        y = torch.empty((adj.n_rows, d), dtype=torch.float32, device=x.device)
+    m = M.detach().to(x.device, torch.float32).contiguous()
+    check(_lib.lib().gnnrec_spmm_dense_f32(*_csr_args(adj), ptr(x), x.stride(0),
+                                           ptr(y if store_y else None), d, d, ptr(m),
+                                           float(c_out), ptr(resid), resid.stride(0),
+                                           float(c_res), ptr(acc),
+                                           acc.stride(0) if acc is not None else d,
+                                           int(acc_mode), float(w_out), float(w_res),
+                                           _lib.stream_of(adj.device)), "gnnrec_spmm_dense_f32")
+    return y if store_y else None

@@ -1,0 +1,275 @@
+"""CsrGraph: the device-resident graph operand of the propagation kernels.
+
+The reference keeps the normalised adjacency as a scipy COO matrix, re-wraps it into an
+uncoalesced int64 ``torch.sparse_coo_tensor`` on every ``get_torch_adjacency()`` call
+(data/dataset.py:472-491, data/graph_builder.py:147-174) and copies it host->device every
+epoch (training/trainer.py:233-234). Here the operand is built once, natively, as CSR over
+destination rows and stays resident in HBM:
+
+    row_ptr  int64 [n_rows + 1]  absolute offsets
+    col      int32 [nnz]         ascending inside each row (what makes SpMM bit-exact)
+    val      fp32  [nnz]         fl32(fl32(dis[r] * a_rc) * dis[c]), as scipy computes it
+
+That is 8 B per nonzero instead of the reference's 20 B (two int64 indices + fp32 value).
+A CsrGraph quacks like the reference's adjacency where the models look at it
+(``.is_sparse``, ``.shape``, ``.size()``, ``.device``, ``.to()``), so it can be passed
+wherever ``adj_matrix`` is expected.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+def _np(t: torch.Tensor) -> np.ndarray:
+    return t.detach().cpu().numpy()
+
+
+def inv_sqrt_degrees(deg: np.ndarray, normalization: str = "symmetric") -> np.ndarray:
+    """Degree scaling exactly as graph_builder.py:111-131 (numpy float32 power)."""
+    deg = np.maximum(np.asarray(deg, dtype=np.float32), np.float32(1.0))
+    if normalization == "symmetric":
+        d = np.power(deg, np.float32(-0.5))
+    elif normalization == "row":
+        d = np.power(deg, np.float32(-1.0))
+    else:
+        raise ValueError(f"unknown normalization: {normalization}")
+    d[np.isinf(d)] = 0.0
+    return d.astype(np.float32, copy=False)
+
+
+@dataclass
+class ShardInfo:
+    """Destination-row shard of a partitioned graph (multi-GPU)."""
+    rank: int
+    world: int
+    row_begin: int          # first global row owned by this shard
+    row_end: int            # one past the last
+    rows_pad: int           # rows per rank in the padded all-gather layout
+    bounds: Tuple[int, ...]  # row boundaries of every rank (len world+1)
+
+
+@dataclass
+class CsrGraph:
+    row_ptr: torch.Tensor
+    col: torch.Tensor
+    val: torch.Tensor
+    shape: Tuple[int, int]
+    n_users: Optional[int] = None
+    n_items: Optional[int] = None
+    symmetric: bool = False
+    shard_info: Optional[ShardInfo] = None
+    _transpose: Optional["CsrGraph"] = field(default=None, repr=False)
+
+    # ---- reference-adjacency look-alike -------------------------------------------
+    is_sparse = True
+
+    @property
+    def device(self) -> torch.device:
+        return self.val.device
+
+    @property
+    def nnz(self) -> int:
+        return int(self.col.numel())
+
+    @property
+    def n_rows(self) -> int:
+        return int(self.row_ptr.numel() - 1)
+
+    def size(self, dim: Optional[int] = None):
+        s = torch.Size(self.shape)
+        return s if dim is None else s[dim]
+
+    def _nonzero_count(self) -> int:
+        return self.nnz
+
+    def to(self, device, non_blocking: bool = False) -> "CsrGraph":
+        device = torch.device(device)
+        if device == self.device:
+            return self
+        g = CsrGraph(self.row_ptr.to(device, non_blocking=non_blocking),
+                     self.col.to(device, non_blocking=non_blocking),
+                     self.val.to(device, non_blocking=non_blocking), self.shape, self.n_users,
+                     self.n_items, self.symmetric, self.shard_info)
+        return g
+
+    def cuda(self, device=None) -> "CsrGraph":
+        return self.to(torch.device("cuda") if device is None else torch.device("cuda", device)
+                       if isinstance(device, int) else device)
+
+    def cpu(self) -> "CsrGraph":
+        return self.to("cpu")
+
+    def validate(self) -> None:
+        """Host-side structural checks (the kernels trust the operand)."""
+        rp = _np(self.row_ptr)
+        col = _np(self.col)
+        if rp.shape[0] != self.shape[0] + 1 and self.shard_info is None:
+            raise ValueError("row_ptr length must be n_rows + 1")
+        if np.any(np.diff(rp) < 0):
+            raise ValueError("row_ptr must be non-decreasing")
+        if rp[-1] - rp[0] != col.shape[0] or self.val.numel() != col.shape[0]:
+            raise ValueError("row_ptr span, col and val sizes disagree")
+        if col.size and (col.min() < 0 or col.max() >= self.shape[1]):
+            raise ValueError("column index out of range")
+        rows = np.repeat(np.arange(rp.shape[0] - 1), np.diff(rp))
+        bad = (np.diff(col.astype(np.int64)) <= 0) & (rows[1:] == rows[:-1])
+        if np.any(bad):
+            raise ValueError("columns must be strictly ascending within each row")
+
+    # ---- construction ---------------------------------------------------------------
+    @classmethod
+    def from_interactions(cls, users, items, n_users: int, n_items: int,
+                          normalization: str = "symmetric", self_loop: bool = False,
+                          n_threads: int = 0, device="cpu", binary: bool = False) -> "CsrGraph":
+        """Native equivalent of build_bipartite_graph + normalize_adjacency_matrix
+        (graph_builder.py:16-144) for interaction lists; identical values and order.
+        Duplicate pairs are summed like the reference (weight 2) unless `binary`."""
+        u = np.ascontiguousarray(np.asarray(users, dtype=np.int64))
+        i = np.ascontiguousarray(np.asarray(items, dtype=np.int64))
+        if u.shape != i.shape:
+            raise ValueError("users and items must have the same length")
+        N = int(n_users) + int(n_items)
+        cap = 2 * u.shape[0] + (N if self_loop else 0)
+        row_ptr = np.empty(N + 1, np.int64)
+        col = np.empty(max(cap, 1), np.int32)
+        cnt = np.empty(max(cap, 1), np.float32)
+        deg = np.empty(max(N, 1), np.float32)
+        nnz = np.zeros(1, np.int64)
+        L = _lib.lib()
+        _lib.check(L.gnnrec_build_bipartite_csr(
+            u.ctypes.data, i.ctypes.data, u.shape[0], int(n_users), int(n_items),
+            (1 if self_loop else 0) | (2 if binary else 0),
+            row_ptr.ctypes.data, col.ctypes.data, cnt.ctypes.data, deg.ctypes.data,
+            nnz.ctypes.data, int(n_threads)), "build_bipartite_csr")
+        nnz = int(nnz[0])
+        col, cnt, deg = col[:nnz], cnt[:nnz], deg[:N]
+        if normalization == "none":
+            val = cnt
+        else:
+            dis = inv_sqrt_degrees(deg, normalization)
+            val = np.empty(max(nnz, 1), np.float32)[:nnz]
+            _lib.check(L.gnnrec_normalize_values(
+                row_ptr.ctypes.data, col.ctypes.data, cnt.ctypes.data, N, dis.ctypes.data,
+                0 if normalization == "symmetric" else 1, val.ctypes.data, int(n_threads)),
+                "normalize_values")
+        g = cls(torch.from_numpy(row_ptr), torch.from_numpy(col), torch.from_numpy(val), (N, N),
+                int(n_users), int(n_items), symmetric=normalization in ("symmetric", "none"))
+        return g.to(device)
+
+    @classmethod
+    def from_scipy(cls, adj, n_users: Optional[int] = None, n_items: Optional[int] = None,
+                   symmetric: Optional[bool] = None, device="cpu") -> "CsrGraph":
+        """From any scipy sparse matrix (e.g. the reference's norm_adj_matrix)."""
+        import scipy.sparse as sp
+        csr = sp.csr_matrix(adj, dtype=np.float32, copy=True)
+        csr.sum_duplicates()
+        csr.sort_indices()
+        if csr.shape[1] >= 2 ** 31:
+            raise ValueError("more than 2^31 columns")
+        if symmetric is None:
+            symmetric = csr.shape[0] == csr.shape[1] and (abs(csr - csr.T) > 0).nnz == 0
+        g = cls(torch.from_numpy(csr.indptr.astype(np.int64)),
+                torch.from_numpy(csr.indices.astype(np.int32)),
+                torch.from_numpy(csr.data.astype(np.float32)), tuple(csr.shape), n_users,
+                n_items, bool(symmetric))
+        return g.to(device)
+
+    @classmethod
+    def from_torch_sparse(cls, adj: torch.Tensor, symmetric: Optional[bool] = None,
+                          n_users: Optional[int] = None,
+                          n_items: Optional[int] = None) -> "CsrGraph":
+        """From a torch COO/CSR tensor, on its own device (coalesced: duplicates summed)."""
+        if adj.layout == torch.sparse_csr:
+            crow, colv, val = adj.crow_indices(), adj.col_indices(), adj.values()
+            n_rows = adj.shape[0]
+        else:
+            a = adj.coalesce()
+            idx, val = a.indices(), a.values()
+            n_rows = a.shape[0]
+            crow = torch.zeros(n_rows + 1, dtype=torch.int64, device=idx.device)
+            crow[1:] = torch.cumsum(torch.bincount(idx[0], minlength=n_rows), 0)
+            colv = idx[1]
+        g = cls(crow.to(torch.int64).contiguous(), colv.to(torch.int32).contiguous(),
+                val.to(torch.float32).contiguous(), tuple(adj.shape), n_users, n_items,
+                bool(symmetric) if symmetric is not None else False)
+        if symmetric is None:
+            g.symmetric = g.is_symmetric()
+        return g
+
+    # ---- conversion -------------------------------------------------------------------
+    def to_scipy(self):
+        import scipy.sparse as sp
+        rp = _np(self.row_ptr)
+        return sp.csr_matrix((_np(self.val), _np(self.col).astype(np.int64), rp - rp[0]),
+                             shape=(rp.shape[0] - 1, self.shape[1]))
+
+    def to_torch_sparse_coo(self) -> torch.Tensor:
+        """The reference's operand layout (graph_builder.py:163-172), uncoalesced flag."""
+        rp = self.row_ptr
+        counts = (rp[1:] - rp[:-1])
+        rows = torch.repeat_interleave(torch.arange(counts.numel(), device=rp.device), counts)
+        idx = torch.stack([rows, self.col.to(torch.int64)])
+        return torch.sparse_coo_tensor(idx, self.val, (counts.numel(), self.shape[1]))
+
+    def is_symmetric(self) -> bool:
+        if self.shape[0] != self.shape[1] or self.shard_info is not None:
+            return False
+        s = self.to_scipy()
+        return (abs(s - s.T) > 0).nnz == 0
+
+    def t(self) -> "CsrGraph":
+        """A^T as a CsrGraph (cached); A itself when the operand is symmetric."""
+        if self.symmetric:
+            return self
+        if self._transpose is None:
+            st = self.to_scipy().T.tocsr()
+            st.sort_indices()
+            self._transpose = CsrGraph.from_scipy(st, self.n_items, self.n_users, False,
+                                                  device=self.device)
+            self._transpose._transpose = self
+        return self._transpose
+
+    # ---- multi-GPU partition -----------------------------------------------
+    @staticmethod
+    def partition_bounds(row_ptr: np.ndarray, world: int, balance: str = "nnz") -> Tuple[int, ...]:
+        """Contiguous destination-row ranges, balanced by nnz (default) or by rows."""
+        n = row_ptr.shape[0] - 1
+        if balance == "rows":
+            b = [min(n, (n * p + world - 1) // world) for p in range(world + 1)]
+        else:
+            total = row_ptr[-1] - row_ptr[0]
+            targets = row_ptr[0] + (total * np.arange(world + 1)) // max(world, 1)
+            b = list(np.searchsorted(row_ptr, targets, side="left").clip(0, n))
+            b[0], b[-1] = 0, n
+            for p in range(1, world + 1):
+                b[p] = max(b[p], b[p - 1])
+        return tuple(int(v) for v in b)
+
+    def shard(self, rank: int, world: int, balance: str = "nnz") -> "CsrGraph":
+        """Rows [b_rank, b_rank+1) with columns remapped into the padded all-gather layout
+        (global row r of rank p lives at p*rows_pad + (r - b_p))."""
+        rp = _np(self.row_ptr)
+        bounds = self.partition_bounds(rp, world, balance)
+        rows_pad = max(bounds[p + 1] - bounds[p] for p in range(world))
+        rows_pad = max(1, (rows_pad + 3) // 4 * 4)
+        lo, hi = bounds[rank], bounds[rank + 1]
+        k0, k1 = int(rp[lo]), int(rp[hi])
+        col = _np(self.col)[k0:k1].astype(np.int64)
+        owner = np.searchsorted(np.asarray(bounds), col, side="right") - 1
+        col = owner * rows_pad + (col - np.asarray(bounds)[owner])
+        g = CsrGraph(torch.from_numpy(rp[lo:hi + 1] - k0),
+                     torch.from_numpy(col.astype(np.int32)),
+                     self.val.detach().cpu()[k0:k1].clone(), (hi - lo, rows_pad * world),
+                     self.n_users, self.n_items, False,
+                     ShardInfo(rank, world, lo, hi, rows_pad, bounds))
+        return g.to(self.device)
+
+    def __repr__(self) -> str:  # keep it short: the tensors are huge
+        return (f"CsrGraph(shape={self.shape}, nnz={self.nnz}, device={self.device}, "
+                f"symmetric={self.symmetric}, shard={self.shard_info})")

@@ -1,0 +1,186 @@
+/*
+ * gnnrec.h — C ABI of the MI355X-native propagation hot path (libgnnrec.so).
+ *
+ * The reference (timur1arkhipov/gnn-recommendations) is pure Python and has no FFI:
+ * its hot path is the PyTorch call `torch.sparse.mm(adj_matrix, x)` inside the model
+ * classes. Each entry point below replaces one such op call site (or a fused chain of
+ * them); the citations name the reference lines (paths relative to
+ * gnn-recommendations/). The Python host layer (gnn-recommendations_amd/src/ops/_lib.py)
+ * binds these with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions (all entry points):
+ *   - Device pointers are owned by the caller (PyTorch caching allocator); nothing is
+ *     allocated, freed or synchronised inside a compute call, so every call is legal
+ *     inside hipGraph capture. Work is queued on `stream` (NULL = legacy default stream).
+ *   - Return 0 (GNNREC_OK) on success or a negative gnnrec_status; the message of the
+ *     last failure on the calling thread is returned by gnnrec_last_error().
+ *   - No C++ exception crosses the ABI. All functions are reentrant.
+ *   - Graph operand = CSR over destination rows: `row_ptr[n_rows+1]` (int64, absolute
+ *     offsets into col/val, row_ptr[0] need not be 0), `col[]` (int32, ascending within
+ *     each row), `val[]` (fp32). Ascending columns are what makes the SpMM bit-exact with
+ *     the reference's COO `torch.sparse.mm` (per-row sequential fmaf, col order).
+ *   - Dense tables are fp32 row-major with an explicit leading dimension in ELEMENTS.
+ */
+#ifndef GNNREC_H_
+#define GNNREC_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GNNREC_ABI_VERSION 1
+
+typedef struct ihipStream_t* gnnrec_stream_t;
+
+enum gnnrec_status {
+  GNNREC_OK = 0,
+  GNNREC_EINVAL = -1,       /* bad argument (null pointer, bad size, unsupported d) */
+  GNNREC_EHIP = -2,         /* a HIP runtime call failed (launch error) */
+  GNNREC_EUNSUPPORTED = -3  /* combination not implemented */
+};
+
+/* Epilogue flags of gnnrec_spmm_csr_f32 (bit set). They fuse the LightGCN layer mean
+ * `torch.stack(all_embeddings).mean(0)` (baselines/lightgcn.py:94-95) into the hop:
+ *   ACC_INIT: acc[r] = self[r] + y[r]          (first hop: x0 + x1)
+ *   ACC_ADD : acc[r] = acc[r] + y[r]           (later hops, sequential like torch.mean)
+ *   ACC_DIV : then acc[r] = acc[r] / acc_div   (last hop: / (K+1))
+ *   NO_Y    : do not store y (last hop when the layer output itself is not needed) */
+#define GNNREC_EPI_ACC_INIT 1
+#define GNNREC_EPI_ACC_ADD 2
+#define GNNREC_EPI_ACC_DIV 4
+#define GNNREC_EPI_NO_Y 8
+
+/* ---- library identity ------------------------------------------------------------ */
+const char* gnnrec_version(void);
+int gnnrec_abi_version(void);
+const char* gnnrec_last_error(void);
+
+/* ---- a4: normalised-adjacency SpMM -------------------------------------------------
+ * Replaces torch.sparse.mm(adj_matrix, x) at baselines/lightgcn.py:88,178,
+ * baselines/ngcf.py:70, orthogonal_bundle/model.py:172,184,333,344, baselines/kgtore.py:310.
+ *   y[r, :] = sum_k val[k] * x[col[k], :]   for k in row r, ascending k, starting at +0.0f,
+ *   each term applied with fmaf (bit-exact with the reference CPU path).
+ * `self`/`acc` are only read/written when an ACC_* flag is set (see above); `self` is the
+ * input-table row of destination r (x0 for LightGCN's first hop).
+ * Any d >= 1 is accepted; d in {8,16,32,64,128,256} take the vectorised fast path. */
+int gnnrec_spmm_csr_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
+                        int64_t n_rows, const float* x, int64_t ldx, float* y, int64_t ldy,
+                        int32_t d, int32_t epi, const float* self, int64_t ld_self,
+                        float* acc, int64_t ld_acc, float acc_div, gnnrec_stream_t stream);
+
+/* ---- a5: whole LightGCN propagation (K hops + fused layer mean) ----------------------
+ * Replaces the body of LightGCN.forward (baselines/lightgcn.py:76-95) on one device:
+ *   out = (((x0 + A x0) + A^2 x0) + ... + A^K x0) / (K+1)
+ * work0/work1: two [n_rows, d] scratch tables (ping-pong hop outputs); `layers`, if not
+ * NULL, receives the K hop outputs x1..xK as K consecutive [n_rows, ld_out] tables
+ * (get_layer_embeddings, lightgcn.py:153-183) and then work0/work1 may be NULL.
+ * Requires a square operand (n_rows == rows of x0). */
+int gnnrec_lightgcn_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
+                        int64_t n_rows, const float* x0, int32_t d, int32_t n_layers,
+                        float* work0, float* work1, float* layers, float* out, int64_t ld_out,
+                        gnnrec_stream_t stream);
+
+/* ---- a7: Group-and-Shuffle transform -----------------------------------------------
+ * Replaces GroupShuffleLayer.forward (orthogonal_bundle/group_shuffle_layer.py:88-94):
+ *   y = (x @ blockdiag(W_0..W_{d/bs-1}))[:, perm]
+ *   y[r, j] = sum_{c<bs} x[r, bs*b + c] * W_b[c, e]   with perm[j] = bs*b + e.
+ * blocks: [d/bs, bs, bs] row-major (W_b[c][e] = blocks[(b*bs + c)*bs + e]); perm: [d]. */
+int gnnrec_gas_f32(const float* x, int64_t ldx, int64_t n_rows, int32_t d, int32_t bs,
+                   const float* blocks, const int32_t* perm, float* y, int64_t ldy,
+                   gnnrec_stream_t stream);
+
+/* Fused hop + GAS: y = GAS(A x) (SpMM epilogue; one HBM round trip fewer). */
+int gnnrec_spmm_gas_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
+                        int64_t n_rows, const float* x, int64_t ldx, float* y, int64_t ldy,
+                        int32_t d, int32_t bs, const float* blocks, const int32_t* perm,
+                        gnnrec_stream_t stream);
+
+/* ---- a6: NGCF layer (SpMM + two 64x64 Linear on MFMA + LeakyReLU [+ GAS]) -----------
+ * Replaces NGCFLayer.forward (baselines/ngcf.py:69-84) in eval mode (dropout = identity):
+ *   n   = A x
+ *   out = LeakyReLU_slope( (n @ W1^T + b1) + ((x_self * n) @ W2^T + b2) )
+ * W1, W2: [d, d] in nn.Linear layout (out_features x in_features); b1, b2: [d].
+ * x_self: the input-table rows of the destination rows ([n_rows, ld_self]).
+ * If gas_blocks != NULL, GAS(gas_blocks, gas_perm, gas_bs) is applied to `out` before the
+ * store (BASELINE config 3: x_{l+1} = GS_l(NGCFLayer_l(x_l))).
+ * d must be 32, 64 or 128 (MFMA f32 16x16x4 tiles). */
+int gnnrec_spmm_ngcf_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
+                         int64_t n_rows, const float* x, int64_t ldx, const float* x_self,
+                         int64_t ld_self, float* y, int64_t ldy, int32_t d, const float* W1,
+                         const float* b1, const float* W2, const float* b2, float slope,
+                         const float* gas_blocks, const int32_t* gas_perm, int32_t gas_bs,
+                         gnnrec_stream_t stream);
+
+/* ---- a9: OrthogonalBundle layer (SpMM + composed 64x64 transform + residual) ---------
+ * Replaces orthogonal_bundle/model.py:171-195 (adjacency path) plus the softmax-weighted
+ * layer sum of model.py:204-207:
+ *   out = c_out * ((A x) @ M) + c_res * resid
+ * with M = W_conn @ W_gs[:, perm] composed on the host (d x d, row-major) and
+ * c_out = 1 - alpha, c_res = alpha, resid = x_init rows of the destinations.
+ * acc_mode 0: no layer sum; 1: acc = fl(w_res*resid) + fl(w_out*out) (layer 0 + layer 1);
+ * 2: acc = acc + fl(w_out*out). `y` may be NULL when only acc is wanted.
+ * d must be 32, 64 or 128. */
+int gnnrec_spmm_dense_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
+                          int64_t n_rows, const float* x, int64_t ldx, float* y, int64_t ldy,
+                          int32_t d, const float* M, float c_out, const float* resid,
+                          int64_t ld_resid, float c_res, float* acc, int64_t ld_acc,
+                          int32_t acc_mode, float w_out, float w_res, gnnrec_stream_t stream);
+
+/* ---- a11: GAT sparse edge-softmax aggregation ---------------------------------------
+ * Replaces the dense masked softmax + mm of GATLayer.forward (baselines/gat.py:99-149):
+ * for every head h and destination row r with neighbours j (CSR pattern; val ignored):
+ *   e_j = LeakyReLU_slope(s_self[r, h] + s_neigh[j, h]);  a = softmax_j(e)
+ *   o[r, h, :] = sum_j a_j * hfeat[j, h, :]
+ * hfeat: [N, heads*o_dim] (head-major columns, = cat of the per-head W_h x);
+ * s_self/s_neigh: [N, heads]. mean_heads = 0: out[r] = cat_h o[r,h,:] ([n_rows, heads*o]);
+ * 1: out[r] = mean_h o[r,h,:] ([n_rows, o]). An empty row yields NaN (softmax over an
+ * empty set, as the reference's all-(-inf) row). o_dim <= 256. */
+int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* col, int64_t n_rows,
+                             const float* hfeat, int64_t ldh, const float* s_self,
+                             const float* s_neigh, int32_t heads, int32_t o_dim, float slope,
+                             int32_t mean_heads, float* out, int64_t ldo,
+                             gnnrec_stream_t stream);
+
+/* ---- a13: scoring + seen-item mask + top-K ------------------------------------------
+ * Replaces evaluator.py:96-105 / trainer.py:327-336 for one batch of users:
+ *   score[b, i] = sum_{f<d} u[b, f] * v[i, f]   (sequential fmaf over f, from +0.0f)
+ *   score[b, i] = -inf for items i in the seen list of user b (CSR seen_ptr/seen_col)
+ *   top-k by (score desc, item index asc) -> out_idx[b, :k] (int64), out_score[b, :k].
+ * k <= 128. */
+int gnnrec_score_topk_f32(const float* u, int64_t ldu, int64_t n_users_batch,
+                          const float* v, int64_t ldv, int64_t n_items, int32_t d,
+                          const int64_t* seen_ptr, const int32_t* seen_col, int32_t k,
+                          int64_t* out_idx, float* out_score, gnnrec_stream_t stream);
+
+/* ---- a1-a3: host-side operand construction (native, no GPU) -------------------------
+ * build_bipartite_graph + normalize_adjacency_matrix (data/graph_builder.py:16-144):
+ * CSR over N = n_users + n_items rows of A = [[0, R], [R^T, 0]] with columns ascending,
+ * duplicate (user,item) pairs summed (coo -> csr semantics, graph_builder.py:107).
+ * col/cnt must hold 2*n_pairs (+N with self_loop) entries; the number used is returned in
+ * *nnz_out. Fills row_ptr[N+1], col[nnz], cnt[nnz] (edge multiplicity as float) and deg[N]
+ * (float32 row sums, graph_builder.py:111). users/items must be in range (else EINVAL).
+ * flags: GNNREC_BUILD_SELF_LOOP adds the identity (graph_builder.py:73-74);
+ * GNNREC_BUILD_BINARY keeps duplicate pairs once with weight 1 (the deduplicated input
+ * preprocessing.py:185-218 guarantees), instead of summing them. n_threads <= 0: all cores. */
+#define GNNREC_BUILD_SELF_LOOP 1
+#define GNNREC_BUILD_BINARY 2
+int gnnrec_build_bipartite_csr(const int64_t* users, const int64_t* items, int64_t n_pairs,
+                               int64_t n_users, int64_t n_items, int32_t flags,
+                               int64_t* row_ptr, int32_t* col, float* cnt, float* deg,
+                               int64_t* nnz_out, int32_t n_threads);
+
+/* Symmetric normalisation values (graph_builder.py:116-126):
+ *   val[k] = fl32(fl32(dis[r] * cnt[k]) * dis[col[k]])  with dis = deg^-1/2 computed by the
+ * caller with numpy float32 power (graph_builder.py:119), bit-identical to scipy's
+ * D^-1/2 @ A @ D^-1/2. mode 1 = 'row' normalisation: val = fl32(dis[r] * cnt[k]). */
+int gnnrec_normalize_values(const int64_t* row_ptr, const int32_t* col, const float* cnt,
+                            int64_t n_rows, const float* dis, int32_t mode, float* val,
+                            int32_t n_threads);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GNNREC_H_ */

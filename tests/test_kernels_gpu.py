@@ -1,0 +1,207 @@
+"""HIP kernels vs the oracle and the reference goldens (through the C ABI).
+
+Bit-exact: SpMM (every d, strides, epilogues), fused LightGCN. fp32 tolerance where the
+reference's order is MKL's (GAS/NGCF/OB transforms): 1e-5 absolute on O(0.1) values.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from conftest import golden_csr, load_golden
+
+from src.ops import CsrGraph, functional as F
+from src.ops import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def graph_from_golden(name, device):
+    rp, col, val, nu, ni = golden_csr(name)
+    g = CsrGraph(torch.from_numpy(rp), torch.from_numpy(col), torch.from_numpy(val),
+                 (rp.size - 1, rp.size - 1), nu, ni, symmetric=True)
+    return g.to(device), (rp, col, val)
+
+
+def bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.uint32)
+
+
+def random_graph(n_users, n_items, n_pairs, seed, device, heavy_user=None):
+    rng = np.random.default_rng(seed)
+    u = rng.integers(0, n_users, n_pairs)
+    i = rng.integers(0, n_items, n_pairs)
+    if heavy_user is not None:  # one very long row (power-law head)
+        u = np.concatenate([u, np.full(heavy_user, 0)])
+        i = np.concatenate([i, rng.permutation(n_items)[:heavy_user]])
+    g = CsrGraph.from_interactions(u, i, n_users, n_items)
+    return g.to(device), (g.row_ptr.numpy(), g.col.numpy(), g.val.numpy())
+
+
+@pytest.mark.parametrize("d", [1, 3, 8, 16, 32, 48, 64, 128, 256])
+def test_spmm_bit_exact_all_dims(cuda, d):
+    g, (rp, col, val) = graph_from_golden("g_small", cuda)
+    x = (torch.randn(g.shape[0], d, generator=torch.Generator().manual_seed(d)) * 0.1)
+    y = F.spmm_forward(g, x.to(cuda)).cpu().numpy()
+    np.testing.assert_array_equal(bits(y), bits(oracle.spmm(rp, col, val, x.numpy())))
+
+
+def test_spmm_strided_tables(cuda):
+    g, (rp, col, val) = graph_from_golden("g_dup", cuda)
+    big = torch.randn(g.shape[0], 80, device=cuda)
+    x = big[:, 8:72]                       # ld 80, 16-B aligned view
+    y = torch.full((g.shape[0], 96), 7.0, device=cuda)
+    F.spmm_into(g, x, y[:, 16:80])
+    ref = oracle.spmm(rp, col, val, x.cpu().numpy())
+    np.testing.assert_array_equal(bits(y[:, 16:80].cpu().numpy()), bits(ref))
+    assert torch.all(y[:, :16] == 7.0) and torch.all(y[:, 80:] == 7.0)
+
+
+def test_spmm_epilogue_flags(cuda):
+    g, (rp, col, val) = graph_from_golden("g_small", cuda)
+    n = g.shape[0]
+    x = torch.randn(n, 64, device=cuda) * 0.1
+    acc = torch.empty_like(x)
+    y = torch.empty_like(x)
+    F.spmm_into(g, x, y, epi=_lib.EPI_ACC_INIT, self_rows=x, acc=acc)
+    yr = oracle.spmm(rp, col, val, x.cpu().numpy())
+    np.testing.assert_array_equal(bits(acc.cpu().numpy()), bits(x.cpu().numpy() + yr))
+    acc2 = acc.clone()
+    F.spmm_into(g, x, None, epi=_lib.EPI_ACC_ADD | _lib.EPI_ACC_DIV | _lib.EPI_NO_Y, acc=acc2,
+                acc_div=3.0)
+    np.testing.assert_array_equal(bits(acc2.cpu().numpy()),
+                                  bits((acc.cpu().numpy() + yr) / np.float32(3.0)))
+
+
+def test_spmm_empty_rows_and_empty_graph(cuda):
+    g, (rp, col, val) = graph_from_golden("g_iso", cuda)  # isolated users/items
+    assert np.any(np.diff(rp) == 0)
+    x = torch.randn(g.shape[0], 64, device=cuda)
+    y = F.spmm_forward(g, x).cpu().numpy()
+    np.testing.assert_array_equal(bits(y), bits(oracle.spmm(rp, col, val, x.cpu().numpy())))
+    assert np.all(y[np.diff(rp) == 0] == 0) and not np.signbit(y[np.diff(rp) == 0]).any()
+    e = CsrGraph.from_interactions(np.zeros(0, np.int64), np.zeros(0, np.int64), 5, 3).to(cuda)
+    assert torch.all(F.spmm_forward(e, torch.randn(8, 64, device=cuda)) == 0)
+
+
+def test_spmm_long_rows_bit_exact(cuda):
+    g, (rp, col, val) = random_graph(3000, 20000, 60000, 5, cuda, heavy_user=15000)
+    assert np.diff(rp).max() >= 15000
+    x = torch.randn(g.shape[0], 64, device=cuda)
+    y = F.spmm_forward(g, x).cpu().numpy()
+    np.testing.assert_array_equal(bits(y), bits(oracle.spmm(rp, col, val, x.cpu().numpy())))
+
+
+def test_spmm_deterministic(cuda):
+    g, _ = random_graph(5000, 7000, 100000, 9, cuda)
+    x = torch.randn(g.shape[0], 64, device=cuda)
+    a = F.spmm_forward(g, x)
+    b = F.spmm_forward(g, x)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("K,d", [(1, 32), (2, 64), (3, 64), (3, 128)])
+def test_lightgcn_fused_bit_exact_vs_reference(cuda, K, d):
+    f = load_golden(f"lightgcn_K{K}_d{d}")
+    g, _ = graph_from_golden("g_small", cuda)
+    x0 = torch.from_numpy(np.concatenate([f["user_w"], f["item_w"]])).to(cuda)
+    out, layers = F.lightgcn_forward(g, x0, K, return_layers=True)
+    nu = f["user_out"].shape[0]
+    out = out.cpu().numpy()
+    np.testing.assert_array_equal(bits(out[:nu]), bits(f["user_out"]))
+    np.testing.assert_array_equal(bits(out[nu:]), bits(f["item_out"]))
+    for k in range(K):
+        np.testing.assert_array_equal(bits(layers[k].cpu().numpy()), bits(f["layers"][k + 1]))
+    out2, none = F.lightgcn_forward(g, x0, K)  # ping-pong buffers, NO_Y last hop
+    assert none is None
+    np.testing.assert_array_equal(bits(out2.cpu().numpy()), bits(out))
+
+
+def test_lightgcn_zero_layers(cuda):
+    g, _ = graph_from_golden("g_small", cuda)
+    x0 = torch.randn(g.shape[0], 64, device=cuda)
+    out, _ = F.lightgcn_forward(g, x0, 0)
+    assert torch.equal(out, x0)
+
+
+def test_lightgcn_backward_matches_reference(cuda):
+    f = load_golden("lightgcn_grad_K3_d64")
+    g, _ = graph_from_golden("g_small", cuda)
+    x0 = torch.from_numpy(np.concatenate([f["user_w"], f["item_w"]])).to(cuda).requires_grad_()
+    out = F.lightgcn_propagate(g, x0, 3)
+    gout = torch.from_numpy(np.concatenate([f["g_u"], f["g_i"]])).to(cuda)
+    (out * gout).sum().backward()
+    ref = np.concatenate([f["grad_user"], f["grad_item"]])
+    np.testing.assert_allclose(x0.grad.cpu().numpy(), ref, rtol=0, atol=1e-6)
+
+
+def test_gas_vs_reference(cuda):
+    f = load_golden("gas_d64_bs8")
+    x = torch.from_numpy(f["x"]).to(cuda)
+    y = F.gas(x, torch.from_numpy(f["blocks"]), torch.from_numpy(f["perm"]).to(cuda))
+    np.testing.assert_allclose(y.cpu().numpy(), f["y"], rtol=0, atol=1e-6)
+    np.testing.assert_array_equal(bits(y.cpu().numpy()), bits(oracle.gas(f["x"], f["blocks"], f["perm"])))
+
+
+def test_spmm_gas_fused(cuda):
+    f = load_golden("gas_d64_bs8")
+    g, (rp, col, val) = graph_from_golden("g_small", cuda)
+    x = torch.randn(g.shape[0], 64, device=cuda) * 0.1
+    blocks = torch.from_numpy(f["blocks"]).to(cuda)
+    perm = torch.from_numpy(f["perm"]).to(cuda)
+    y = F.spmm_gas(g, x, blocks, perm).cpu().numpy()
+    ref = oracle.gas(oracle.spmm(rp, col, val, x.cpu().numpy()), f["blocks"], f["perm"])
+    np.testing.assert_array_equal(bits(y), bits(ref))
+
+
+def test_ngcf_layers_vs_reference(cuda):
+    f = load_golden("ngcf_d64")
+    g, _ = graph_from_golden("g_small", cuda)
+    x = torch.from_numpy(np.concatenate([f["user_w"], f["item_w"]])).to(cuda)
+    outs = [x]
+    for li in range(3):
+        t = lambda k: torch.from_numpy(f[f"{k}_{li}"]).to(cuda)  # noqa: E731
+        x = F.ngcf_layer(g, x, t("W1"), t("b1"), t("W2"), t("b2"), 0.2)
+        outs.append(x)
+    cat = torch.cat(outs, 1).cpu().numpy()
+    nu = f["user_out"].shape[0]
+    np.testing.assert_allclose(cat[:nu], f["user_out"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(cat[nu:], f["item_out"], rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("d", [32, 64, 128])
+def test_ngcf_gas_vs_oracle(cuda, d):
+    g, (rp, col, val) = random_graph(700, 900, 9000, d, cuda)
+    rng = np.random.default_rng(d)
+    x = rng.standard_normal((g.shape[0], d)).astype(np.float32) * 0.1
+    W1, W2 = (rng.standard_normal((2, d, d)) / np.sqrt(d)).astype(np.float32)
+    b1, b2 = (rng.standard_normal((2, d)) * 0.05).astype(np.float32)
+    q, _ = np.linalg.qr(rng.standard_normal((d // 8, 8, 8)))
+    blocks = q.astype(np.float32)
+    perm = rng.permutation(d).astype(np.int32)
+    T = lambda a: torch.from_numpy(a).to(cuda)  # noqa: E731
+    y = F.ngcf_layer(g, T(x), T(W1), T(b1), T(W2), T(b2), 0.2, gas_blocks=T(blocks),
+                     gas_perm=T(perm)).cpu().numpy()
+    ref = oracle.gas(oracle.ngcf_layer(rp, col, val, x, W1, b1, W2, b2, 0.2), blocks, perm)
+    np.testing.assert_allclose(y, ref, rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("d", [32, 64, 128])
+def test_dense_layer_vs_oracle(cuda, d):
+    g, (rp, col, val) = random_graph(500, 800, 7000, 3 * d, cuda)
+    rng = np.random.default_rng(d + 1)
+    x = rng.standard_normal((g.shape[0], d)).astype(np.float32) * 0.1
+    xi = rng.standard_normal((g.shape[0], d)).astype(np.float32) * 0.1
+    M = (rng.standard_normal((d, d)) / np.sqrt(d)).astype(np.float32)
+    T = lambda a: torch.from_numpy(a).to(cuda)  # noqa: E731
+    acc = torch.empty(g.shape[0], d, device=cuda)
+    y = F.dense_layer(g, T(x), T(M), 0.9, T(xi), 0.1, acc=acc, acc_mode=1, w_out=0.3, w_res=0.7)
+    n = oracle.spmm(rp, col, val, x).astype(np.float64)
+    ref = (np.float32(0.9) * (n @ M) + np.float32(0.1) * xi).astype(np.float32)
+    np.testing.assert_allclose(y.cpu().numpy(), ref, rtol=0, atol=1e-5)
+    np.testing.assert_allclose(acc.cpu().numpy(), np.float32(0.7) * xi + np.float32(0.3) * ref,
+                               rtol=0, atol=1e-5)
+    acc_before = acc.clone()
+    F.dense_layer(g, T(x), T(M), 0.9, T(xi), 0.1, acc=acc, acc_mode=2, w_out=0.5, store_y=False)
+    np.testing.assert_allclose(acc.cpu().numpy(), (acc_before + 0.5 * y).cpu().numpy(), rtol=0,
+                               atol=1e-6)
