@@ -163,9 +163,13 @@ __global__ __launch_bounds__(kBlock) void spmm_mfma_kernel(DenseParams p) {
         o = gas ? gas_row<D>(&o_lds[slot][0], w_gas, p.gas_bs, pj) : ld4(&o_lds[slot][4 * gl]);
       } else {
         const float4 t = ld4(&o_lds[slot][4 * gl]);
-        const float4 rs = ld4(p.resid + r * p.ld_resid + 4 * gl);
-        o = make_float4(p.c_out * t.x + p.c_res * rs.x, p.c_out * t.y + p.c_res * rs.y,
-                        p.c_out * t.z + p.c_res * rs.z, p.c_out * t.w + p.c_res * rs.w);
+        const float4 rs = p.resid ? ld4(p.resid + r * p.ld_resid + 4 * gl)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (p.resid)
+          o = make_float4(p.c_out * t.x + p.c_res * rs.x, p.c_out * t.y + p.c_res * rs.y,
+                          p.c_out * t.z + p.c_res * rs.z, p.c_out * t.w + p.c_res * rs.w);
+        else
+          o = make_float4(p.c_out * t.x, p.c_out * t.y, p.c_out * t.z, p.c_out * t.w);
         if (p.acc_mode) {
           float* ar = p.acc + r * p.ld_acc + 4 * gl;
           const float4 base =
@@ -241,8 +245,9 @@ extern "C" int gnnrec_spmm_dense_f32(const int64_t* row_ptr, const int32_t* col,
   GNNREC_REQUIRE(row_ptr && col && val && M, "spmm_dense: null operand");
   GNNREC_REQUIRE(acc_mode >= 0 && acc_mode <= 2, "spmm_dense: acc_mode must be 0, 1 or 2");
   GNNREC_REQUIRE(y || acc_mode, "spmm_dense: nothing to write (y == NULL and acc_mode == 0)");
-  GNNREC_REQUIRE(rows_ok(x, ldx) && ldx >= d && rows_ok(resid, ld_resid) && ld_resid >= d,
-                 "spmm_dense: x/resid must be 16-B aligned with ld %% 4 == 0 and ld >= d");
+  GNNREC_REQUIRE(rows_ok(x, ldx) && ldx >= d, "spmm_dense: x must be 16-B aligned, ld %% 4 == 0, ld >= d");
+  GNNREC_REQUIRE(resid ? (rows_ok(resid, ld_resid) && ld_resid >= d) : acc_mode != 1,
+                 "spmm_dense: resid must be 16-B aligned with ld >= d (required by acc_mode 1)");
   GNNREC_REQUIRE(!y || (rows_ok(y, ldy) && ldy >= d), "spmm_dense: bad y");
   GNNREC_REQUIRE(!acc_mode || (rows_ok(acc, ld_acc) && ld_acc >= d), "spmm_dense: bad acc");
   DenseParams p{};

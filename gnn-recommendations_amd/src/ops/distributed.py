@@ -1,0 +1,139 @@
+"""Multi-GPU propagation: destination-row shards + one all-gather per hop.
+
+One process per GPU (torchrun / torch.distributed.run), backend "nccl" = RCCL over xGMI.
+
+Partition: destination rows are split into `world` contiguous ranges balanced by nnz
+(CsrGraph.partition_bounds). Rank p owns rows [b_p, b_{p+1}) of A with its CSR rebased and
+its columns remapped into the *padded* all-gather layout, where global row r of rank q sits
+at q*rows_pad + (r - b_q). Every rank holds the full replicated input table in that layout
+([world*rows_pad, d]) and produces only its own rows.
+
+Per hop:  Y_p = A[R_p, :] X            (local HIP SpMM, fused layer-mean epilogue)
+          X' = all_gather(Y_p)         (RCCL all_gather_into_tensor, equal-size pieces)
+The last hop needs no gather: the layer mean stays row-sharded (scoring can be sharded by
+user range); `gather_output=True` returns the full table.
+
+The local hop is injectable (`hop_fn`, default: the native gnnrec_spmm_csr_f32 wrapper) so
+the partition / gather / epilogue bookkeeping is testable on CPU ranks over gloo with the
+oracle as the local hop (tests/test_distributed.py).
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT, EPI_NO_Y
+from .graph import CsrGraph
+
+HopFn = Callable[..., None]
+
+
+def _native_hop(adj, x, y, *, epi, self_rows, acc, acc_div):
+    from .functional import spmm_into
+    spmm_into(adj, x, y, epi=epi, self_rows=self_rows, acc=acc, acc_div=acc_div)
+
+
+class DistributedGraph:
+    """This rank's shard of the operand plus the padded layout helpers."""
+
+    def __init__(self, full: CsrGraph, rank: int, world: int, device,
+                 balance: str = "nnz", group=None):
+        self.rank, self.world, self.group = rank, world, group
+        self.device = torch.device(device)
+        self.shard = full.shard(rank, world, balance).to(self.device)
+        info = self.shard.shard_info
+        self.bounds = info.bounds
+        self.rows_pad = info.rows_pad
+        self.row_begin, self.row_end = info.row_begin, info.row_end
+        self.n_local = self.row_end - self.row_begin
+        self.n_global = full.shape[0]
+
+    # ---- layout ----------------------------------------------------------------------------
+    def padded_index(self) -> np.ndarray:
+        """Position of every global row in the padded layout."""
+        b = np.asarray(self.bounds)
+        r = np.arange(self.n_global)
+        owner = np.searchsorted(b, r, side="right") - 1
+        return owner * self.rows_pad + (r - b[owner])
+
+    def pad_table(self, x: torch.Tensor) -> torch.Tensor:
+        """[N, d] global table -> [world*rows_pad, d] padded table on this rank's device."""
+        out = torch.zeros((self.world * self.rows_pad, x.shape[1]), dtype=x.dtype,
+                          device=self.device)
+        idx = torch.from_numpy(self.padded_index()).to(self.device)
+        out[idx] = x.to(self.device)
+        return out
+
+    def unpad_table(self, xp: torch.Tensor) -> torch.Tensor:
+        idx = torch.from_numpy(self.padded_index()).to(xp.device)
+        return xp[idx]
+
+    def local_slice(self, xp: torch.Tensor) -> torch.Tensor:
+        o = self.rank * self.rows_pad
+        return xp[o:o + self.n_local]
+
+    # ---- communication ---------------------------------------------------------------------
+    def all_gather(self, out: torch.Tensor, piece: torch.Tensor) -> None:
+        if self.world == 1:
+            out.copy_(piece)
+        else:
+            dist.all_gather_into_tensor(out, piece, group=self.group)
+
+
+def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers: int, *,
+                            gather_output: bool = False, hop_fn: Optional[HopFn] = None,
+                            work: Optional[tuple] = None) -> torch.Tensor:
+    """LightGCN propagation over a row-sharded operand.
+
+    x0_pad: [world*rows_pad, d] padded initial table (identical on every rank).
+    Returns this rank's rows of mean(x0..xK) ([n_local, d]), or the full [N, d] table when
+    gather_output. `work` (from `make_work`) holds reusable hop buffers. With world == 1
+    the hop outputs feed the next hop directly (no gather, no copy).
+    """
+    hop = hop_fn or _native_hop
+    d = x0_pad.shape[1]
+    if work is None:
+        work = make_work(dg, d, x0_pad.device)
+    Y, Xa, Xb = work
+    acc = torch.empty((dg.n_local, d), dtype=torch.float32, device=x0_pad.device)
+    self_rows = dg.local_slice(x0_pad)
+    if n_layers == 0:
+        acc.copy_(self_rows)
+    x_in = x0_pad
+    for k in range(1, n_layers + 1):
+        last = k == n_layers
+        epi = EPI_ACC_INIT if k == 1 else EPI_ACC_ADD
+        if last:
+            epi |= EPI_ACC_DIV | EPI_NO_Y
+        if dg.world == 1:  # ping-pong the hop outputs themselves
+            y = None if last else (Xa if x_in is not Xa else Xb)
+            hop(dg.shard, x_in, None if last else y[:dg.n_local], epi=epi, self_rows=self_rows,
+                acc=acc, acc_div=float(n_layers + 1))
+            x_in = y
+            continue
+        hop(dg.shard, x_in, None if last else Y[:dg.n_local], epi=epi, self_rows=self_rows,
+            acc=acc, acc_div=float(n_layers + 1))
+        if not last:
+            x_next = Xa if x_in is not Xa else Xb
+            dg.all_gather(x_next, Y)
+            x_in = x_next
+    if not gather_output:
+        return acc
+    if dg.world == 1:
+        return acc
+    Y[:dg.n_local].copy_(acc)
+    full = torch.empty_like(x0_pad)
+    dg.all_gather(full, Y)
+    return dg.unpad_table(full)
+
+
+def make_work(dg: DistributedGraph, d: int, device) -> tuple:
+    """Hop buffers: Y [rows_pad, d] (zero padded tail) and two [world*rows_pad, d] tables."""
+    rows = dg.world * dg.rows_pad
+    # world == 1 ping-pongs Xa/Xb directly, so Y is a placeholder
+    Y = torch.zeros((dg.rows_pad if dg.world > 1 else 1, d), dtype=torch.float32, device=device)
+    return (Y, torch.zeros((rows, d), dtype=torch.float32, device=device),
+            torch.zeros((rows, d), dtype=torch.float32, device=device))

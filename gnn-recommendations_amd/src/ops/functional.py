@@ -194,12 +194,12 @@ def ngcf_layer(adj: CsrGraph, x: torch.Tensor, W1: torch.Tensor, b1: torch.Tenso
 
 
 def dense_layer(adj: CsrGraph, x: torch.Tensor, M: torch.Tensor, c_out: float,
-                resid: torch.Tensor, c_res: float, *, y: Optional[torch.Tensor] = None,
+                resid: Optional[torch.Tensor], c_res: float, *, y: Optional[torch.Tensor] = None,
                 acc: Optional[torch.Tensor] = None, acc_mode: int = 0, w_out: float = 0.0,
                 w_res: float = 0.0, store_y: bool = True) -> Optional[torch.Tensor]:
     """c_out * ((A x) @ M) + c_res * resid, with the optional fused layer sum into `acc`."""
     x = _rowmajor(x)
-    resid = _rowmajor(resid)
+    resid = _rowmajor(resid) if resid is not None else None
     _require_device(adj, x, resid, acc)
     d = x.shape[1]
     if store_y and y is None:
@@ -207,7 +207,8 @@ def dense_layer(adj: CsrGraph, x: torch.Tensor, M: torch.Tensor, c_out: float,
     m = M.detach().to(x.device, torch.float32).contiguous()
     check(_lib.lib().gnnrec_spmm_dense_f32(*_csr_args(adj), ptr(x), x.stride(0),
                                            ptr(y if store_y else None), d, d, ptr(m),
-                                           float(c_out), ptr(resid), resid.stride(0),
+                                           float(c_out), ptr(resid),
+                                           resid.stride(0) if resid is not None else d,
                                            float(c_res), ptr(acc),
                                            acc.stride(0) if acc is not None else d,
                                            int(acc_mode), float(w_out), float(w_res),

@@ -260,12 +260,16 @@ class CsrGraph:
         rows_pad = max(1, (rows_pad + 3) // 4 * 4)
         lo, hi = bounds[rank], bounds[rank + 1]
         k0, k1 = int(rp[lo]), int(rp[hi])
-        col = _np(self.col)[k0:k1].astype(np.int64)
-        owner = np.searchsorted(np.asarray(bounds), col, side="right") - 1
-        col = owner * rows_pad + (col - np.asarray(bounds)[owner])
-        g = CsrGraph(torch.from_numpy(rp[lo:hi + 1] - k0),
-                     torch.from_numpy(col.astype(np.int32)),
-                     self.val.detach().cpu()[k0:k1].clone(), (hi - lo, rows_pad * world),
+        if world == 1:  # identity layout: nothing to remap
+            col_t, val_t, rp_t = self.col, self.val, self.row_ptr
+        else:
+            col = _np(self.col)[k0:k1].astype(np.int64)
+            owner = np.searchsorted(np.asarray(bounds), col, side="right") - 1
+            col = owner * rows_pad + (col - np.asarray(bounds)[owner])
+            col_t = torch.from_numpy(col.astype(np.int32))
+            val_t = self.val.detach().cpu()[k0:k1].clone()
+            rp_t = torch.from_numpy(rp[lo:hi + 1] - k0)
+        g = CsrGraph(rp_t, col_t, val_t, (hi - lo, rows_pad * world),
                      self.n_users, self.n_items, False,
                      ShardInfo(rank, world, lo, hi, rows_pad, bounds))
         return g.to(self.device)

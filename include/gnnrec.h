@@ -120,7 +120,8 @@ int gnnrec_spmm_ngcf_f32(const int64_t* row_ptr, const int32_t* col, const float
  * with M = W_conn @ W_gs[:, perm] composed on the host (d x d, row-major) and
  * c_out = 1 - alpha, c_res = alpha, resid = x_init rows of the destinations.
  * acc_mode 0: no layer sum; 1: acc = fl(w_res*resid) + fl(w_out*out) (layer 0 + layer 1);
- * 2: acc = acc + fl(w_out*out). `y` may be NULL when only acc is wanted.
+ * 2: acc = acc + fl(w_out*out). `y` may be NULL when only acc is wanted; `resid` may be
+ * NULL (no residual term, out = c_out * ((A x) @ M)) unless acc_mode is 1.
  * d must be 32, 64 or 128. */
 int gnnrec_spmm_dense_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
                           int64_t n_rows, const float* x, int64_t ldx, float* y, int64_t ldy,
