@@ -279,7 +279,7 @@ def main(argv=None) -> int:
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
-                "kernel": "spmm_vec4_kernel<64> (one launch per hop)",
+                "kernel": f"spmm_vec_kernel<{d}> (one launch per hop)",
                 "launch_ms": launch_ms,
                 "algorithmic_bytes_per_launch": launch_bytes,
             },

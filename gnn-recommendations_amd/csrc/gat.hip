@@ -1,0 +1,150 @@
+// GAT sparse edge-softmax aggregation (BASELINE config 5), gfx950.
+//
+// Replaces GATLayer.forward's dense path (baselines/gat.py:99-149): the reference builds an
+// [N, N] score matrix per head, masks non-edges with -inf, row-softmaxes and multiplies by
+// h — O(N^2) memory, infeasible past N ~ 2e4. Here each destination row walks its CSR
+// neighbours once: e_j = LeakyReLU(s_self[r,h] + s_neigh[j,h]) with an online max / sum
+// (flash-style rescaling), accumulating p_j * h[j] for every head at the same time.
+// Row mapping as the SpMM (gather.h): F = heads*o_dim features per row, GROUP = F/4 lanes
+// per row, 4 features (one head) per lane; a neighbour costs one F*4-byte row gather plus
+// one 4-byte score gather per lane.
+// Fused epilogue: mean over heads (last layer, gat.py:149), F.elu (gat.py:283) and the
+// layer-mean accumulator (gat.py:287-288, GNNREC_EPI_* flags).
+#include <math.h>
+
+#include "gather.h"
+
+namespace gnnrec {
+
+struct GatParams {
+  Csr A;
+  const float* h;
+  int64_t ldh;
+  const float* s_self;
+  const float* s_neigh;
+  int heads, o_dim;
+  float slope;
+  int mean_heads, apply_elu;
+  float* out;
+  int64_t ldo;
+  int epi;
+  const float* self;
+  int64_t ld_self;
+  float* acc;
+  int64_t ld_acc;
+  float acc_div;
+};
+
+template <int F>
+__global__ __launch_bounds__(kBlock) void gat_kernel(GatParams p) {
+  constexpr int GROUP = F / 4;
+  constexpr int RPW = 64 / GROUP;
+  const int lane = threadIdx.x & 63;
+  const int gl = lane % GROUP;
+  const int64_t r = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
+  if (r >= p.A.n_rows) return;
+  const int hl = p.o_dim / 4;  // lanes per head
+  const int head = gl / hl;
+  const float ss = p.s_self[r * p.heads + head];
+  const int64_t beg = p.A.row_ptr[r], end = p.A.row_ptr[r + 1];
+  float m = -INFINITY, l = 0.f;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t k0 = beg; k0 < end; k0 += kChunk) {
+    constexpr int PER = (GROUP >= kChunk) ? 1 : kChunk / GROUP;
+    int cm[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      int64_t k = k0 + gl + (int64_t)q * GROUP;
+      k = k < end ? k : end - 1;
+      cm[q] = p.A.col[k];
+    }
+    float4 xv[kChunk];
+    float sn[kChunk];
+#pragma unroll
+    for (int t = 0; t < kChunk; ++t) {
+      const int c = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
+      xv[t] = ld4(p.h + (int64_t)c * p.ldh + 4 * gl);
+      sn[t] = p.s_neigh[(int64_t)c * p.heads + head];
+    }
+#pragma unroll
+    for (int t = 0; t < kChunk; ++t) {
+      if (k0 + t < end) {
+        float e = ss + sn[t];
+        e = e > 0.f ? e : e * p.slope;
+        const float mn = fmaxf(m, e);
+        const float sc = expf(m - mn);  // m = -inf on the first neighbour: sc = 0
+        const float pe = expf(e - mn);
+        l = l * sc + pe;
+        a.x = __builtin_fmaf(pe, xv[t].x, a.x * sc);
+        a.y = __builtin_fmaf(pe, xv[t].y, a.y * sc);
+        a.z = __builtin_fmaf(pe, xv[t].z, a.z * sc);
+        a.w = __builtin_fmaf(pe, xv[t].w, a.w * sc);
+        m = mn;
+      }
+    }
+  }
+  // softmax normalisation (l = 0 for an empty row -> 0/0 = NaN, like the reference)
+  float4 o = make_float4(a.x / l, a.y / l, a.z / l, a.w / l);
+  int owner_lanes = GROUP;
+  if (p.mean_heads) {  // mean over heads: lanes fg, fg+hl, ... hold the same features
+    const int fg = gl % hl;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q = 0; q < p.heads; ++q) {
+      const int src = fg + q * hl;
+      const float4 t = make_float4(__shfl(o.x, src, GROUP), __shfl(o.y, src, GROUP),
+                                   __shfl(o.z, src, GROUP), __shfl(o.w, src, GROUP));
+      s = q == 0 ? t : make_float4(s.x + t.x, s.y + t.y, s.z + t.z, s.w + t.w);
+    }
+    const float H = (float)p.heads;
+    o = make_float4(s.x / H, s.y / H, s.z / H, s.w / H);
+    owner_lanes = hl;
+  }
+  if (gl >= owner_lanes) return;
+  if (p.apply_elu) {
+    o.x = o.x > 0.f ? o.x : expm1f(o.x);
+    o.y = o.y > 0.f ? o.y : expm1f(o.y);
+    o.z = o.z > 0.f ? o.z : expm1f(o.z);
+    o.w = o.w > 0.f ? o.w : expm1f(o.w);
+  }
+  if (!(p.epi & GNNREC_EPI_NO_Y)) st4(p.out + r * p.ldo + 4 * gl, o);
+  acc_epilogue(p.epi, o, p.self + r * p.ld_self + 4 * gl, p.acc + r * p.ld_acc + 4 * gl, p.acc_div);
+}
+
+}  // namespace gnnrec
+
+using namespace gnnrec;
+
+extern "C" int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* col, int64_t n_rows,
+                                        const float* hfeat, int64_t ldh, const float* s_self,
+                                        const float* s_neigh, int32_t heads, int32_t o_dim,
+                                        float slope, int32_t mean_heads, int32_t apply_elu,
+                                        float* out, int64_t ldo, int32_t epi, const float* self,
+                                        int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
+                                        gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(n_rows >= 0 && heads >= 1 && o_dim >= 4 && o_dim % 4 == 0, "gat: bad sizes");
+  if (n_rows == 0) return GNNREC_OK;
+  const int F = heads * o_dim;
+  const int width = mean_heads ? o_dim : F;
+  GNNREC_REQUIRE(row_ptr && col && hfeat && s_self && s_neigh, "gat: null operand");
+  GNNREC_REQUIRE(aligned16(hfeat) && !(ldh & 3) && ldh >= F, "gat: hfeat must be 16-B aligned, ld %% 4 == 0, ld >= heads*o_dim");
+  GNNREC_REQUIRE((epi & GNNREC_EPI_NO_Y) || (out && aligned16(out) && !(ldo & 3) && ldo >= width),
+                 "gat: bad out");
+  GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_INIT) || (self && aligned16(self) && !(ld_self & 3) && ld_self >= width),
+                 "gat: ACC_INIT needs 16-B aligned self rows");
+  GNNREC_REQUIRE(!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) ||
+                     (acc && aligned16(acc) && !(ld_acc & 3) && ld_acc >= width),
+                 "gat: ACC needs 16-B aligned acc");
+  GatParams p{Csr{row_ptr, col, nullptr, n_rows}, hfeat, ldh, s_self, s_neigh, heads, o_dim, slope,
+              mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div};
+  hipStream_t s = as_hip(stream);
+  auto grid = [&](int f) { return dim3((unsigned)ceil_div(n_rows, (64 / (f / 4)) * (kBlock / 64))); };
+  switch (F) {
+    case 16: hipLaunchKernelGGL(gat_kernel<16>, grid(16), dim3(kBlock), 0, s, p); break;
+    case 32: hipLaunchKernelGGL(gat_kernel<32>, grid(32), dim3(kBlock), 0, s, p); break;
+    case 64: hipLaunchKernelGGL(gat_kernel<64>, grid(64), dim3(kBlock), 0, s, p); break;
+    case 128: hipLaunchKernelGGL(gat_kernel<128>, grid(128), dim3(kBlock), 0, s, p); break;
+    case 256: hipLaunchKernelGGL(gat_kernel<256>, grid(256), dim3(kBlock), 0, s, p); break;
+    default: set_error("gat: heads*o_dim = %d unsupported (16..256, power of two)", F); return GNNREC_EUNSUPPORTED;
+  }
+  return check_launch("gat_aggregate");
+}

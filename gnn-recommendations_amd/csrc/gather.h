@@ -32,30 +32,30 @@ __device__ __forceinline__ void st4(float* p, const float4& v) {
 
 // One gather step of CH neighbours [k0, k0+CH) of a row ending at `end`. TAIL selects the
 // FMA of out-of-row slots away (their loads are clamped to the row's last element).
-template <int GROUP, bool TAIL>
+template <int GROUP, bool TAIL, int CH = kChunk>
 __device__ __forceinline__ void gather_step(const int32_t* __restrict__ col,
                                             const float* __restrict__ val, int64_t k0,
                                             int64_t end, const float* __restrict__ x,
                                             int64_t ldx, int gl, float4& a) {
-  constexpr int PER = (GROUP >= kChunk) ? 1 : kChunk / GROUP;  // pairs loaded per lane
+  constexpr int PER = (GROUP >= CH) ? 1 : CH / GROUP;  // pairs loaded per lane
   int cm[PER];
   float vm[PER];
 #pragma unroll
   for (int m = 0; m < PER; ++m) {
     int64_t k = k0 + gl + (int64_t)m * GROUP;
     if (TAIL) k = k < end ? k : end - 1;
-    if (GROUP >= kChunk && gl >= kChunk) k = k0;  // idle lanes: any in-row address
-    cm[m] = __builtin_nontemporal_load(col + k);
-    vm[m] = __builtin_nontemporal_load(val + k);
+    if (GROUP >= CH && gl >= CH) k = k0;  // idle lanes: any in-row address
+    cm[m] = col[k];
+    vm[m] = val[k];
   }
-  float4 xv[kChunk];
+  float4 xv[CH];
 #pragma unroll
-  for (int t = 0; t < kChunk; ++t) {
+  for (int t = 0; t < CH; ++t) {
     const int c = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
     xv[t] = ld4(x + (int64_t)c * ldx + 4 * gl);
   }
 #pragma unroll
-  for (int t = 0; t < kChunk; ++t) {
+  for (int t = 0; t < CH; ++t) {
     const float v = __shfl(vm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
     const float4 n = fma4(v, xv[t], a);
     if (TAIL) {
@@ -71,16 +71,115 @@ __device__ __forceinline__ void gather_step(const int32_t* __restrict__ col,
 }
 
 // Sequential-order row reduction: returns the lane's float4 slice of (A x)[r].
-template <int GROUP>
+template <int GROUP, int CH = kChunk>
 __device__ __forceinline__ float4 gather_row(const int32_t* __restrict__ col,
                                              const float* __restrict__ val, int64_t beg,
                                              int64_t end, const float* __restrict__ x,
                                              int64_t ldx, int gl) {
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   int64_t k0 = beg;
-  for (; k0 + kChunk <= end; k0 += kChunk) gather_step<GROUP, false>(col, val, k0, end, x, ldx, gl, a);
-  if (k0 < end) gather_step<GROUP, true>(col, val, k0, end, x, ldx, gl, a);
+  for (; k0 + CH <= end; k0 += CH) gather_step<GROUP, false, CH>(col, val, k0, end, x, ldx, gl, a);
+  if (k0 < end) gather_step<GROUP, true, CH>(col, val, k0, end, x, ldx, gl, a);
   return a;
+}
+
+// ---- VEC-generic form (VEC = 1, 2 or 4 features per lane, GROUP = d / VEC lanes per row) --
+template <int N>
+struct VecF {
+  float v[N];
+};
+
+template <int N>
+__device__ __forceinline__ VecF<N> ldv(const float* p) {
+  VecF<N> r;
+  if constexpr (N == 4) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    r.v[0] = t.x; r.v[1] = t.y; r.v[2] = t.z; r.v[3] = t.w;
+  } else if constexpr (N == 2) {
+    const float2 t = *reinterpret_cast<const float2*>(p);
+    r.v[0] = t.x; r.v[1] = t.y;
+  } else {
+    r.v[0] = *p;
+  }
+  return r;
+}
+
+template <int N>
+__device__ __forceinline__ void stv(float* p, const VecF<N>& a) {
+  if constexpr (N == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(a.v[0], a.v[1], a.v[2], a.v[3]);
+  } else if constexpr (N == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2(a.v[0], a.v[1]);
+  } else {
+    *p = a.v[0];
+  }
+}
+
+template <int VEC, int GROUP, bool TAIL, int CH, bool NT = false>
+__device__ __forceinline__ void gather_step_v(const int32_t* __restrict__ col,
+                                              const float* __restrict__ val, int64_t k0,
+                                              int64_t end, const float* __restrict__ x,
+                                              int64_t ldx, int gl, VecF<VEC>& a) {
+  constexpr int PER = (GROUP >= CH) ? 1 : CH / GROUP;
+  int cm[PER];
+  float vm[PER];
+#pragma unroll
+  for (int m = 0; m < PER; ++m) {
+    int64_t k = k0 + gl + (int64_t)m * GROUP;
+    if (TAIL) k = k < end ? k : end - 1;
+    if (GROUP >= CH && gl >= CH) k = k0;
+    if (NT) {
+      cm[m] = __builtin_nontemporal_load(col + k);
+      vm[m] = __builtin_nontemporal_load(val + k);
+    } else {
+      cm[m] = col[k];
+      vm[m] = val[k];
+    }
+  }
+  VecF<VEC> xv[CH];
+#pragma unroll
+  for (int t = 0; t < CH; ++t) {
+    const int c = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
+    xv[t] = ldv<VEC>(x + (int64_t)c * ldx + VEC * gl);
+  }
+#pragma unroll
+  for (int t = 0; t < CH; ++t) {
+    const float v = __shfl(vm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
+    const bool ok = !TAIL || (k0 + t) < end;
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) {
+      const float n = __builtin_fmaf(v, xv[t].v[q], a.v[q]);
+      a.v[q] = ok ? n : a.v[q];
+    }
+  }
+}
+
+template <int VEC, int GROUP, int CH, bool NT = false>
+__device__ __forceinline__ VecF<VEC> gather_row_v(const int32_t* __restrict__ col,
+                                                  const float* __restrict__ val, int64_t beg,
+                                                  int64_t end, const float* __restrict__ x,
+                                                  int64_t ldx, int gl) {
+  VecF<VEC> a;
+#pragma unroll
+  for (int q = 0; q < VEC; ++q) a.v[q] = 0.f;
+  int64_t k0 = beg;
+  for (; k0 + CH <= end; k0 += CH)
+    gather_step_v<VEC, GROUP, false, CH, NT>(col, val, k0, end, x, ldx, gl, a);
+  if (k0 < end) gather_step_v<VEC, GROUP, true, CH, NT>(col, val, k0, end, x, ldx, gl, a);
+  return a;
+}
+
+template <int VEC>
+__device__ __forceinline__ void acc_epilogue_v(int epi, const VecF<VEC>& y, const float* self_row,
+                                               float* acc_row, float acc_div) {
+  if (!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD))) return;
+  VecF<VEC> b = (epi & GNNREC_EPI_ACC_INIT) ? ldv<VEC>(self_row) : ldv<VEC>(acc_row);
+#pragma unroll
+  for (int q = 0; q < VEC; ++q) {
+    b.v[q] = b.v[q] + y.v[q];
+    if (epi & GNNREC_EPI_ACC_DIV) b.v[q] = b.v[q] / acc_div;
+  }
+  stv<VEC>(acc_row, b);
 }
 
 // ---- GAS (block-diagonal orthogonal transform + column shuffle) -----------------------
@@ -100,6 +199,24 @@ __device__ __forceinline__ float4 gas_row(const float* zrow_lds, const float* w_
     o[q] = s;
   }
   return make_float4(o[0], o[1], o[2], o[3]);
+}
+
+// LightGCN layer-mean epilogue (see GNNREC_EPI_* in gnnrec.h).
+__device__ __forceinline__ void acc_epilogue(int epi, const float4& y, const float* self_row,
+                                             float* acc_row, float acc_div) {
+  if (!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD))) return;
+  float4 b = (epi & GNNREC_EPI_ACC_INIT) ? ld4(self_row) : ld4(acc_row);
+  b.x = b.x + y.x;
+  b.y = b.y + y.y;
+  b.z = b.z + y.z;
+  b.w = b.w + y.w;
+  if (epi & GNNREC_EPI_ACC_DIV) {
+    b.x = b.x / acc_div;
+    b.y = b.y / acc_div;
+    b.z = b.z / acc_div;
+    b.w = b.w / acc_div;
+  }
+  st4(acc_row, b);
 }
 
 }  // namespace gnnrec

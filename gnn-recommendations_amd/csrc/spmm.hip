@@ -11,30 +11,20 @@
 
 namespace gnnrec {
 
-// LightGCN layer-mean epilogue (see GNNREC_EPI_* in gnnrec.h).
-__device__ __forceinline__ void acc_epilogue(int epi, const float4& y, const float* self_row,
-                                             float* acc_row, float acc_div) {
-  if (!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD))) return;
-  float4 b = (epi & GNNREC_EPI_ACC_INIT) ? ld4(self_row) : ld4(acc_row);
-  b.x = b.x + y.x;
-  b.y = b.y + y.y;
-  b.z = b.z + y.z;
-  b.w = b.w + y.w;
-  if (epi & GNNREC_EPI_ACC_DIV) {
-    b.x = b.x / acc_div;
-    b.y = b.y / acc_div;
-    b.z = b.z / acc_div;
-    b.w = b.w / acc_div;
-  }
-  st4(acc_row, b);
-}
+// Lane mapping per d, from the G100M sweep (tools/exp_prod.py, profiles/r01/): VEC features
+// per lane, GROUP = d / VEC lanes per row, CH neighbours in flight per step.
+template <int D> struct SpmmCfg { static constexpr int VEC = 4, CH = 16; };
+template <> struct SpmmCfg<32> { static constexpr int VEC = 2, CH = 16; };
+template <> struct SpmmCfg<64> { static constexpr int VEC = 1, CH = 8; };   // wave per row
+template <> struct SpmmCfg<128> { static constexpr int VEC = 2, CH = 16; };  // wave per row
 
 template <int D>
-__global__ __launch_bounds__(kBlock) void spmm_vec4_kernel(
+__global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
     Csr A, const float* __restrict__ x, int64_t ldx, float* __restrict__ y, int64_t ldy,
     int epi, const float* __restrict__ self, int64_t ld_self, float* __restrict__ acc,
     int64_t ld_acc, float acc_div) {
-  constexpr int GROUP = D / 4;
+  constexpr int VEC = SpmmCfg<D>::VEC, CH = SpmmCfg<D>::CH;
+  constexpr int GROUP = D / VEC;
   constexpr int RPW = 64 / GROUP;
   const int lane = threadIdx.x & 63;
   const int gl = lane % GROUP;
@@ -42,9 +32,9 @@ __global__ __launch_bounds__(kBlock) void spmm_vec4_kernel(
       ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
   if (r >= A.n_rows) return;  // the whole group leaves together
   const int64_t beg = A.row_ptr[r], end = A.row_ptr[r + 1];
-  const float4 a = gather_row<GROUP>(A.col, A.val, beg, end, x, ldx, gl);
-  if (!(epi & GNNREC_EPI_NO_Y)) st4(y + r * ldy + 4 * gl, a);
-  acc_epilogue(epi, a, self + r * ld_self + 4 * gl, acc + r * ld_acc + 4 * gl, acc_div);
+  const VecF<VEC> a = gather_row_v<VEC, GROUP, CH>(A.col, A.val, beg, end, x, ldx, gl);
+  if (!(epi & GNNREC_EPI_NO_Y)) stv<VEC>(y + r * ldy + VEC * gl, a);
+  acc_epilogue_v<VEC>(epi, a, self + r * ld_self + VEC * gl, acc + r * ld_acc + VEC * gl, acc_div);
 }
 
 // Any-d fallback: one wave per row, lanes stride the features (same k order per feature).
@@ -113,9 +103,9 @@ template <int D>
 void launch_spmm_vec4(const Csr& A, const float* x, int64_t ldx, float* y, int64_t ldy, int epi,
                       const float* self, int64_t ld_self, float* acc, int64_t ld_acc,
                       float acc_div, hipStream_t s) {
-  constexpr int RPB = (64 / (D / 4)) * (kBlock / 64);
+  constexpr int RPB = (64 / (D / SpmmCfg<D>::VEC)) * (kBlock / 64);
   const int64_t grid = ceil_div(A.n_rows, RPB);
-  hipLaunchKernelGGL(spmm_vec4_kernel<D>, dim3((unsigned)grid), dim3(kBlock), 0, s, A, x, ldx,
+  hipLaunchKernelGGL(spmm_vec_kernel<D>, dim3((unsigned)grid), dim3(kBlock), 0, s, A, x, ldx,
                      y, ldy, epi, self, ld_self, acc, ld_acc, acc_div);
 }
 

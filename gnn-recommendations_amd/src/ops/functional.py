@@ -214,3 +214,26 @@ def dense_layer(adj: CsrGraph, x: torch.Tensor, M: torch.Tensor, c_out: float,
                                            int(acc_mode), float(w_out), float(w_res),
                                            _lib.stream_of(adj.device)), "gnnrec_spmm_dense_f32")
     return y if store_y else None
+
+
+def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh: torch.Tensor,
+                  heads: int, o_dim: int, slope: float = 0.2, mean_heads: bool = False,
+                  apply_elu: bool = False, *, out: Optional[torch.Tensor] = None, epi: int = 0,
+                  self_rows: Optional[torch.Tensor] = None, acc: Optional[torch.Tensor] = None,
+                  acc_div: float = 1.0) -> Optional[torch.Tensor]:
+    """Sparse edge-softmax aggregation of one GAT layer, all heads (gnnrec_gat_aggregate_f32)."""
+    h = _rowmajor(h)
+    s_self = s_self.contiguous()
+    s_neigh = s_neigh.contiguous()
+    _require_device(adj, h, self_rows, acc)
+    width = o_dim if mean_heads else heads * o_dim
+    if out is None and not (epi & EPI_NO_Y):
+        out = torch.empty((adj.n_rows, width), dtype=torch.float32, device=h.device)
+    check(_lib.lib().gnnrec_gat_aggregate_f32(
+        ptr(adj.row_ptr), ptr(adj.col), adj.n_rows, ptr(h), h.stride(0), ptr(s_self),
+        ptr(s_neigh), int(heads), int(o_dim), float(slope), int(mean_heads), int(apply_elu),
+        ptr(out), out.stride(0) if out is not None else width, int(epi), ptr(self_rows),
+        self_rows.stride(0) if self_rows is not None else width, ptr(acc),
+        acc.stride(0) if acc is not None else width, float(acc_div), _lib.stream_of(adj.device)),
+        "gnnrec_gat_aggregate_f32")
+    return out

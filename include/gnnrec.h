@@ -130,19 +130,24 @@ int gnnrec_spmm_dense_f32(const int64_t* row_ptr, const int32_t* col, const floa
                           int32_t acc_mode, float w_out, float w_res, gnnrec_stream_t stream);
 
 /* ---- a11: GAT sparse edge-softmax aggregation ---------------------------------------
- * Replaces the dense masked softmax + mm of GATLayer.forward (baselines/gat.py:99-149):
- * for every head h and destination row r with neighbours j (CSR pattern; val ignored):
+ * Replaces the dense masked softmax + mm of GATLayer.forward (baselines/gat.py:99-149)
+ * plus the F.elu between layers (gat.py:283) and the layer mean (gat.py:287-288):
+ * for every head h and destination row r with neighbours j (CSR pattern; values ignored):
  *   e_j = LeakyReLU_slope(s_self[r, h] + s_neigh[j, h]);  a = softmax_j(e)
  *   o[r, h, :] = sum_j a_j * hfeat[j, h, :]
- * hfeat: [N, heads*o_dim] (head-major columns, = cat of the per-head W_h x);
- * s_self/s_neigh: [N, heads]. mean_heads = 0: out[r] = cat_h o[r,h,:] ([n_rows, heads*o]);
- * 1: out[r] = mean_h o[r,h,:] ([n_rows, o]). An empty row yields NaN (softmax over an
- * empty set, as the reference's all-(-inf) row). o_dim <= 256. */
+ * (single pass, online max/sum rescaling, fp32). hfeat: [N, heads*o_dim] head-major columns
+ * (= cat of the per-head W_h x); s_self / s_neigh: [N, heads] (ld = heads).
+ * mean_heads = 0: out[r] = cat_h o[r,h,:] ([n_rows, heads*o_dim]); 1: out[r] = mean_h
+ * o[r,h,:] ([n_rows, o_dim]). apply_elu: out = ELU(out) (alpha 1). epi: the ACC_* flags of
+ * gnnrec_spmm_csr_f32 applied to the (ELU'd) output with `self` = the layer input rows.
+ * An empty row yields NaN (softmax over an empty set, as the reference's all -inf row).
+ * heads*o_dim must be 16, 32, 64, 128 or 256 (o_dim a multiple of 4). */
 int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* col, int64_t n_rows,
                              const float* hfeat, int64_t ldh, const float* s_self,
                              const float* s_neigh, int32_t heads, int32_t o_dim, float slope,
-                             int32_t mean_heads, float* out, int64_t ldo,
-                             gnnrec_stream_t stream);
+                             int32_t mean_heads, int32_t apply_elu, float* out, int64_t ldo,
+                             int32_t epi, const float* self, int64_t ld_self, float* acc,
+                             int64_t ld_acc, float acc_div, gnnrec_stream_t stream);
 
 /* ---- a13: scoring + seen-item mask + top-K ------------------------------------------
  * Replaces evaluator.py:96-105 / trainer.py:327-336 for one batch of users:

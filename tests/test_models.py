@@ -1,0 +1,145 @@
+"""Model classes on the CPU: drop-in construction (same parameters for the same seed as the
+reference, pinned by the goldens) and the reference CPU path (torch sparse operand) giving
+the reference's outputs. No GPU needed."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_csr, load_golden
+
+from src.models import GAT, NGCF, LightGCN, OrthogonalBundleGNN
+from src.models.orthogonal_bundle import BundleConnectionLayer, GroupShuffleLayer
+from src.ops import CsrGraph
+
+
+def torch_adj(name="g_small"):
+    rp, col, val, nu, ni = golden_csr(name)
+    g = CsrGraph(torch.from_numpy(rp), torch.from_numpy(col), torch.from_numpy(val),
+                 (rp.size - 1, rp.size - 1), nu, ni, True)
+    return g.to_torch_sparse_coo(), nu, ni
+
+
+@pytest.mark.parametrize("K,d", [(1, 32), (2, 64), (3, 64), (3, 128)])
+def test_lightgcn_seeded_init_matches_reference(K, d):
+    f = load_golden(f"lightgcn_K{K}_d{d}")
+    torch.manual_seed(100 + K * 7 + d)
+    m = LightGCN(300, 500, embedding_dim=d, n_layers=K, init_scale=0.1)
+    np.testing.assert_array_equal(m.user_embedding.weight.detach().numpy(), f["user_w"])
+    np.testing.assert_array_equal(m.item_embedding.weight.detach().numpy(), f["item_w"])
+
+
+def test_lightgcn_cpu_reference_path():
+    f = load_golden("lightgcn_K3_d64")
+    torch.manual_seed(100 + 3 * 7 + 64)
+    m = LightGCN(300, 500, embedding_dim=64, n_layers=3, init_scale=0.1).eval()
+    adj, _, _ = torch_adj()
+    with torch.no_grad():
+        u, i = m(adj)
+        layers = m.get_layer_embeddings(adj)
+    np.testing.assert_array_equal(u.numpy(), f["user_out"])
+    np.testing.assert_array_equal(i.numpy(), f["item_out"])
+    for k in range(4):
+        np.testing.assert_array_equal(layers[k].numpy(), f["layers"][k])
+    with pytest.raises(ValueError):
+        m.predict(torch.tensor([0]), torch.tensor([0]))
+
+
+def test_ngcf_seeded_init_and_cpu_path():
+    f = load_golden("ngcf_d64")
+    torch.manual_seed(11)
+    m = NGCF(300, 500, embedding_dim=64, layer_sizes=[64, 64, 64], dropout=0.1, init_scale=0.01)
+    np.testing.assert_array_equal(m.user_embedding.weight.detach().numpy(), f["user_w"])
+    for li, L in enumerate(m.layers):
+        np.testing.assert_array_equal(L.W1.weight.detach().numpy(), f[f"W1_{li}"])
+        np.testing.assert_array_equal(L.W2.weight.detach().numpy(), f[f"W2_{li}"])
+        with torch.no_grad():
+            L.W1.bias.copy_(torch.from_numpy(f[f"b1_{li}"]))
+            L.W2.bias.copy_(torch.from_numpy(f[f"b2_{li}"]))
+    m.eval()
+    adj, _, _ = torch_adj()
+    with torch.no_grad():
+        u, i = m(adj)
+    np.testing.assert_allclose(u.numpy(), f["user_out"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(i.numpy(), f["item_out"], rtol=0, atol=1e-6)
+
+
+def load_ob(f):
+    torch.manual_seed(31)
+    m = OrthogonalBundleGNN(300, 500, embedding_dim=64, n_layers=3, block_size=8,
+                            residual_alpha=0.1, dropout=0.0, init_scale=0.01,
+                            use_parallel_transport=True)
+    with torch.no_grad():
+        m.layer_weights.copy_(torch.tensor([0.3, -0.2, 0.5, 0.1]))
+        for L in list(m.local_transform_layers) + list(m.connection_layers):
+            for p in L.skew_params:
+                p.mul_(20.0)
+    return m
+
+
+def test_ob_seeded_init_and_cpu_path():
+    f = load_golden("ob_d64")
+    m = load_ob(f)
+    np.testing.assert_array_equal(m.user_embedding.weight.detach().numpy(), f["user_w"])
+    for li in range(3):
+        gs, bc = m.local_transform_layers[li], m.connection_layers[li]
+        np.testing.assert_array_equal(np.stack([p.detach().numpy() for p in gs.skew_params]),
+                                      f[f"gs_skew_{li}"])
+        np.testing.assert_array_equal(gs.perm.numpy(), f[f"gs_perm_{li}"])
+        np.testing.assert_array_equal(np.stack([p.detach().numpy() for p in bc.skew_params]),
+                                      f[f"bc_skew_{li}"])
+        np.testing.assert_array_equal(bc.shuffle_perm.numpy(), f[f"bc_perm_{li}"])
+    m.eval()
+    adj, _, _ = torch_adj()
+    with torch.no_grad():
+        u, i = m(adj_matrix=adj)
+        layers = m.get_layer_embeddings(adj_matrix=adj)
+    np.testing.assert_allclose(u.numpy(), f["user_out"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(i.numpy(), f["item_out"], rtol=0, atol=1e-6)
+    for k in range(4):
+        np.testing.assert_allclose(layers[k].numpy(), f["layers"][k], rtol=0, atol=1e-6)
+
+
+def test_gas_and_bundle_layers_match_reference():
+    f = load_golden("gas_d64_bs8")
+    torch.manual_seed(21)
+    gs = GroupShuffleLayer(64, 8, init_scale=0.01)
+    with torch.no_grad():
+        for p in gs.skew_params:
+            p.mul_(30.0)
+        y = gs(torch.from_numpy(f["x"]))
+    np.testing.assert_array_equal(gs.perm.numpy(), f["perm"])
+    np.testing.assert_allclose(y.numpy(), f["y"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(gs.blocks().detach().numpy(), f["blocks"], rtol=0, atol=1e-7)
+    fro, mx = gs.get_orthogonality_metrics()
+    assert fro.item() < 1e-4 and mx.item() < 1e-5
+    b = load_golden("bundle_d64_bs8")
+    torch.manual_seed(22)
+    bc = BundleConnectionLayer(64, 8)
+    with torch.no_grad():
+        np.testing.assert_array_equal(bc().numpy(), b["W"])
+
+
+def test_gat_seeded_init_and_cpu_path():
+    f = load_golden("gat_d64_h4")
+    nu, ni = int(f["n_users"]), int(f["n_items"])
+    torch.manual_seed(42)
+    m = GAT(nu, ni, embedding_dim=64, n_layers=3, n_heads=4, dropout=0.1, alpha=0.2,
+            init_scale=0.1).eval()
+    np.testing.assert_array_equal(m.user_embedding.weight.detach().numpy(), f["user_w"])
+    for li, L in enumerate(m.layers):
+        np.testing.assert_array_equal(np.stack([w.weight.detach().numpy() for w in L.W]),
+                                      f[f"W_{li}"])
+        assert int(L.concat_heads) == int(f[f"concat_{li}"])
+    G = CsrGraph.from_interactions(f["users"], f["items"], nu, ni)
+    with torch.no_grad():
+        u, i = m(G.to_torch_sparse_coo())
+    np.testing.assert_allclose(u.numpy(), f["user_out"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(i.numpy(), f["item_out"], rtol=0, atol=1e-6)
+
+
+def test_cpu_csrgraph_operand_is_rejected():
+    """No silent CPU fallback: a CsrGraph must live on a ROCm device."""
+    g = CsrGraph.from_interactions([0, 1], [1, 0], 2, 2)
+    m = LightGCN(2, 2, embedding_dim=8, n_layers=1)
+    with pytest.raises(ValueError, match="ROCm"):
+        m(g)

@@ -1,0 +1,154 @@
+"""The drop-in model classes on a ROCm device: the native kernels behind the reference's
+model API give the reference's outputs (bit-exact for LightGCN, 1e-5 otherwise)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_csr, load_golden
+from test_models import load_ob
+
+from src.models import GAT, NGCF, LightGCN, NGCFGroupShuffle
+from src.ops import CsrGraph, uses_native
+
+pytestmark = pytest.mark.gpu
+
+
+def golden_graph(cuda, name="g_small"):
+    rp, col, val, nu, ni = golden_csr(name)
+    return CsrGraph(torch.from_numpy(rp), torch.from_numpy(col), torch.from_numpy(val),
+                    (rp.size - 1, rp.size - 1), nu, ni, True).to(cuda)
+
+
+def bits(t):
+    return t.detach().cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("operand", ["csr", "torch_coo"])
+def test_lightgcn_model_bit_exact(cuda, operand):
+    f = load_golden("lightgcn_K3_d64")
+    torch.manual_seed(100 + 3 * 7 + 64)
+    m = LightGCN(300, 500, embedding_dim=64, n_layers=3, init_scale=0.1).to(cuda).eval()
+    g = golden_graph(cuda)
+    adj = g if operand == "csr" else g.to_torch_sparse_coo()  # reference-style operand on GPU
+    assert uses_native(adj)
+    with torch.no_grad():
+        u, i = m.get_all_embeddings(adj)
+        layers = m.get_layer_embeddings(adj)
+    np.testing.assert_array_equal(bits(u), f["user_out"].view(np.uint32))
+    np.testing.assert_array_equal(bits(i), f["item_out"].view(np.uint32))
+    for k in range(4):
+        np.testing.assert_array_equal(bits(layers[k]), f["layers"][k].view(np.uint32))
+    s = m.predict(torch.arange(5, device=cuda), torch.arange(5, device=cuda), adj)
+    ref = (torch.from_numpy(f["user_out"][:5]) * torch.from_numpy(f["item_out"][:5])).sum(1)
+    np.testing.assert_allclose(s.detach().cpu().numpy(), ref.numpy(), rtol=0, atol=1e-7)
+
+
+def test_lightgcn_model_training_grads(cuda):
+    f = load_golden("lightgcn_grad_K3_d64")
+    torch.manual_seed(7)
+    m = LightGCN(300, 500, embedding_dim=64, n_layers=3, init_scale=0.1).to(cuda)
+    u, i = m(golden_graph(cuda))
+    g_u = torch.from_numpy(f["g_u"]).to(cuda)
+    g_i = torch.from_numpy(f["g_i"]).to(cuda)
+    ((u * g_u).sum() + (i * g_i).sum()).backward()
+    np.testing.assert_allclose(m.user_embedding.weight.grad.cpu().numpy(), f["grad_user"],
+                               rtol=0, atol=1e-6)
+    np.testing.assert_allclose(m.item_embedding.weight.grad.cpu().numpy(), f["grad_item"],
+                               rtol=0, atol=1e-6)
+
+
+def ngcf_from_golden(f, cuda):
+    torch.manual_seed(11)
+    m = NGCF(300, 500, embedding_dim=64, layer_sizes=[64, 64, 64], dropout=0.1, init_scale=0.01)
+    with torch.no_grad():
+        for li, L in enumerate(m.layers):
+            L.W1.bias.copy_(torch.from_numpy(f[f"b1_{li}"]))
+            L.W2.bias.copy_(torch.from_numpy(f[f"b2_{li}"]))
+    return m.to(cuda).eval()
+
+
+def test_ngcf_model_fused(cuda):
+    f = load_golden("ngcf_d64")
+    m = ngcf_from_golden(f, cuda)
+    with torch.no_grad():
+        u, i = m(golden_graph(cuda))
+    np.testing.assert_allclose(u.cpu().numpy(), f["user_out"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(i.cpu().numpy(), f["item_out"], rtol=0, atol=1e-5)
+
+
+def test_ngcf_model_training_path(cuda):
+    """With autograd on: native SpMM (differentiable) + torch Linear, same outputs."""
+    f = load_golden("ngcf_d64")
+    m = ngcf_from_golden(f, cuda)
+    u, i = m(golden_graph(cuda))
+    np.testing.assert_allclose(u.detach().cpu().numpy(), f["user_out"], rtol=0, atol=1e-5)
+    (u.sum() + i.sum()).backward()
+    assert m.layers[0].W1.weight.grad is not None
+    assert torch.isfinite(m.user_embedding.weight.grad).all()
+
+
+def test_ngcf_group_shuffle_fused_vs_composed(cuda):
+    torch.manual_seed(3)
+    m = NGCFGroupShuffle(300, 500, embedding_dim=64, layer_sizes=[64, 64, 64], dropout=0.1,
+                         gs_init_scale=0.3).eval()
+    rp, col, val, nu, ni = golden_csr("g_small")
+    cpu_adj = CsrGraph(torch.from_numpy(rp), torch.from_numpy(col), torch.from_numpy(val),
+                       (rp.size - 1, rp.size - 1), nu, ni, True).to_torch_sparse_coo()
+    with torch.no_grad():
+        ref_u, ref_i = m(cpu_adj)             # composed torch path on the CPU
+        m = m.to(cuda)
+        u, i = m(golden_graph(cuda))          # one fused kernel per layer
+    np.testing.assert_allclose(u.cpu().numpy(), ref_u.numpy(), rtol=0, atol=1e-5)
+    np.testing.assert_allclose(i.cpu().numpy(), ref_i.numpy(), rtol=0, atol=1e-5)
+
+
+def test_orthogonal_bundle_model_fused(cuda):
+    f = load_golden("ob_d64")
+    m = load_ob(f).to(cuda).eval()
+    g = golden_graph(cuda)
+    with torch.no_grad():
+        u, i = m(adj_matrix=g)
+        layers = m.get_layer_embeddings(adj_matrix=g)
+    np.testing.assert_allclose(u.cpu().numpy(), f["user_out"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(i.cpu().numpy(), f["item_out"], rtol=0, atol=1e-5)
+    for k in range(4):
+        np.testing.assert_allclose(layers[k].cpu().numpy(), f["layers"][k], rtol=0, atol=1e-5)
+
+
+def test_orthogonal_bundle_edge_index_path(cuda):
+    """use_edge_index=True: edge-list transport mapped onto the CSR kernel, vs the torch path."""
+    f = load_golden("ob_d64")
+    m = load_ob(f)
+    m.use_edge_index = True
+    rp, col, val, nu, ni = golden_csr("g_small")
+    rows = np.repeat(np.arange(rp.size - 1), np.diff(rp))
+    ei = torch.from_numpy(np.vstack([col.astype(np.int64), rows]))  # src -> dst
+    with torch.no_grad():
+        ref_u, ref_i = m(edge_index=ei)
+        m = m.to(cuda).eval()
+        u, i = m(edge_index=ei.to(cuda))
+    np.testing.assert_allclose(u.cpu().numpy(), ref_u.numpy(), rtol=0, atol=2e-5)
+    np.testing.assert_allclose(i.cpu().numpy(), ref_i.numpy(), rtol=0, atol=2e-5)
+
+
+def test_gat_model_sparse(cuda):
+    f = load_golden("gat_d64_h4")
+    nu, ni = int(f["n_users"]), int(f["n_items"])
+    torch.manual_seed(42)
+    m = GAT(nu, ni, embedding_dim=64, n_layers=3, n_heads=4, dropout=0.1, alpha=0.2,
+            init_scale=0.1).to(cuda).eval()
+    g = CsrGraph.from_interactions(f["users"], f["items"], nu, ni).to(cuda)
+    with torch.no_grad():
+        u, i = m(g)
+    np.testing.assert_allclose(u.cpu().numpy(), f["user_out"], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(i.cpu().numpy(), f["item_out"], rtol=0, atol=2e-5)
+
+
+def test_gat_isolated_node_row_is_nan_only_locally(cuda):
+    torch.manual_seed(0)
+    m = GAT(4, 3, embedding_dim=16, n_layers=2, n_heads=4, dropout=0.0).to(cuda).eval()
+    g = CsrGraph.from_interactions([0, 1, 2, 0], [0, 1, 2, 1], 4, 3).to(cuda)  # user 3 isolated
+    with torch.no_grad():
+        u, i = m(g)
+    assert torch.isnan(u[3]).all()
+    assert torch.isfinite(u[:3]).all() and torch.isfinite(i).all()
