@@ -1,0 +1,232 @@
+// Scoring GEMM + seen-item mask + per-user top-K (evaluator.py:96-105, trainer.py:327-336).
+//
+// The reference computes scores = U[b] @ I^T with MKL sgemm, sets the train/valid items of
+// each user to -inf in a Python loop, calls torch.topk (tie order unspecified) and copies
+// the indices to the host. Here one kernel does all of it on the device:
+//   * scores on the matrix cores: v_mfma_f32_16x16x4_f32 is an exact k-ordered fmaf chain,
+//     and the k-steps are issued in ascending k, so score[b,i] is bit-identical to
+//     `acc = 0; for f in 0..d-1: acc = fmaf(u[b,f], v[i,f], acc)` (the oracle's definition);
+//   * a per-user top-K list lives in LDS; a candidate enters only if it beats the list's
+//     current worst entry under the fixed order (score desc, item index asc), so after the
+//     first tiles almost no lane does more than one compare per score;
+//   * seen items are masked lazily: only a candidate that would enter the list is looked up
+//     (binary search in the user's sorted seen list) and, if seen, re-scored as -inf.
+// Workgroup = 4 waves = 64 users (16 per wave); item tiles of 64 rows are staged in LDS
+// ([64][d+2]: d+2 == 2 mod 32 makes the B-fragment reads conflict-free) and reused by the
+// four waves.
+#include <math.h>
+
+#include "gather.h"
+
+namespace gnnrec {
+
+typedef float floatx4_t __attribute__((ext_vector_type(4)));
+
+struct TopkParams {
+  const float* u;
+  int64_t ldu;
+  int64_t nb;
+  const float* v;
+  int64_t ldv;
+  int64_t n_items;
+  const int64_t* seen_ptr;
+  const int32_t* seen_col;
+  int k;
+  int64_t* out_idx;
+  float* out_score;
+};
+
+// a strictly precedes b in the output order
+__device__ __forceinline__ bool better(float sa, int ia, float sb, int ib) {
+  return sa > sb || (sa == sb && ia < ib);
+}
+
+__device__ __forceinline__ bool is_seen(const TopkParams& p, int64_t user, int item) {
+  if (!p.seen_ptr) return false;
+  int64_t lo = p.seen_ptr[user], hi = p.seen_ptr[user + 1];
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    const int c = p.seen_col[mid];
+    if (c == item) return true;
+    if (c < item) lo = mid + 1; else hi = mid;
+  }
+  return false;
+}
+
+// Wave-wide: position of the worst entry of one user's list (entries [0, KM)).
+template <int KM>
+__device__ __forceinline__ int find_worst(const float* ls, const int* li, int lane) {
+  float ws = INFINITY;
+  int wi = -1, wp = 0;
+  for (int e = lane; e < KM; e += 64) {
+    const float s = ls[e];
+    const int i = li[e];
+    if (wi == -1 || better(ws, wi, s, i)) { ws = s; wi = i; wp = e; }
+  }
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float os = __shfl_xor(ws, off, 64);
+    const int oi = __shfl_xor(wi, off, 64);
+    const int op = __shfl_xor(wp, off, 64);
+    const bool take = (wi == -1) || (oi != -1 && better(ws, wi, os, oi)) ||
+                      (oi != -1 && ws == os && wi == oi && op < wp);
+    if (take) { ws = os; wi = oi; wp = op; }
+  }
+  return __shfl(wp, 0, 64);
+}
+
+template <int D, int KM>
+__global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
+  constexpr int STEPS = D / 4;
+  constexpr int TI = 64;       // items per LDS tile
+  constexpr int LDV = D + 2;
+  constexpr int UPB = 64;      // users per workgroup
+  __shared__ __attribute__((aligned(16))) float v_lds[TI * LDV];
+  __shared__ float l_score[UPB][KM];
+  __shared__ int l_item[UPB][KM];
+  __shared__ float l_worst_s[UPB];
+  __shared__ int l_worst_i[UPB];
+  __shared__ int l_worst_p[UPB];
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i16 = lane & 15, k4 = lane >> 4;
+  const int64_t ub = (int64_t)blockIdx.x * UPB;
+  // A fragments: this wave's 16 users, k = 4s + k4 (ascending k per MFMA chain)
+  float af[STEPS];
+  {
+    const int64_t user = ub + 16 * wave + i16;
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) af[s] = user < p.nb ? p.u[user * p.ldu + 4 * s + k4] : 0.f;
+  }
+  for (int e = threadIdx.x; e < UPB * KM; e += kBlock) {
+    l_score[e / KM][e % KM] = -INFINITY;
+    l_item[e / KM][e % KM] = INT_MAX;  // sentinel: loses to every real item
+  }
+  for (int e = threadIdx.x; e < UPB; e += kBlock) {
+    l_worst_s[e] = -INFINITY;
+    l_worst_i[e] = INT_MAX;
+    l_worst_p[e] = 0;
+  }
+  __syncthreads();
+
+  for (int64_t t0 = 0; t0 < p.n_items; t0 += TI) {
+    // stage 64 item rows (zero rows past the end)
+    for (int e = threadIdx.x; e < TI * (D / 4); e += kBlock) {
+      const int r = e / (D / 4), c4 = e % (D / 4);
+      const int64_t item = t0 + r;
+      const float4 q = item < p.n_items ? ld4(p.v + item * p.ldv + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float* dst = &v_lds[r * LDV + 4 * c4];
+      dst[0] = q.x; dst[1] = q.y; dst[2] = q.z; dst[3] = q.w;
+    }
+    __syncthreads();
+    floatx4_t acc[TI / 16];
+#pragma unroll
+    for (int nt = 0; nt < TI / 16; ++nt) {
+      floatx4_t c = {0.f, 0.f, 0.f, 0.f};
+      const float* brow = &v_lds[(16 * nt + i16) * LDV + k4];
+#pragma unroll
+      for (int s = 0; s < STEPS; ++s) c = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], brow[4 * s], c, 0, 0, 0);
+      acc[nt] = c;
+    }
+    // candidates: lane holds users 16*wave + 4*k4 + q (q = reg) x items t0 + 16*nt + i16
+#pragma unroll
+    for (int nt = 0; nt < TI / 16; ++nt) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ul = 16 * wave + 4 * k4 + q;
+        const int64_t user = ub + ul;
+        const int64_t item64 = t0 + 16 * nt + i16;
+        float s = acc[nt][q];
+        if (s != s) s = -INFINITY;  // NaN scores rank last
+        const int item = (int)item64;
+        bool cand = user < p.nb && item64 < p.n_items &&
+                    better(s, item, l_worst_s[ul], l_worst_i[ul]);
+        // serialize the (rare) insertions of this wave, one candidate at a time
+        unsigned long long m = __ballot(cand);
+        while (m) {
+          const int src = __ffsll((long long)m) - 1;
+          m &= m - 1;
+          const int cu = __shfl(ul, src, 64);
+          const int ci = __shfl(item, src, 64);
+          float cs = __shfl(s, src, 64);
+          if (is_seen(p, ub + cu, ci)) cs = -INFINITY;
+          if (better(cs, ci, l_worst_s[cu], l_worst_i[cu])) {
+            if (lane == 0) {
+              const int wp = l_worst_p[cu];
+              l_score[cu][wp] = cs;
+              l_item[cu][wp] = ci;
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            const int wp = find_worst<KM>(&l_score[cu][0], &l_item[cu][0], lane);
+            if (lane == 0) {
+              l_worst_s[cu] = l_score[cu][wp];
+              l_worst_i[cu] = l_item[cu][wp];
+              l_worst_p[cu] = wp;
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // emit each user's list sorted by (score desc, item asc): rank by counting
+  for (int ul = 16 * wave; ul < 16 * wave + 16; ++ul) {
+    const int64_t user = ub + ul;
+    if (user >= p.nb) break;
+    for (int e = lane; e < KM; e += 64) {
+      const float s = l_score[ul][e];
+      const int i = l_item[ul][e];
+      int rank = 0;
+      for (int f = 0; f < KM; ++f) {  // identical sentinels are ordered by slot
+        const float sf = l_score[ul][f];
+        const int jf = l_item[ul][f];
+        rank += (better(sf, jf, s, i) || (sf == s && jf == i && f < e)) ? 1 : 0;
+      }
+      if (rank < p.k) {
+        p.out_idx[user * p.k + rank] = i == INT_MAX ? -1 : (int64_t)i;
+        p.out_score[user * p.k + rank] = s;
+      }
+    }
+  }
+}
+
+}  // namespace gnnrec
+
+using namespace gnnrec;
+
+namespace {
+template <int D, int KM>
+void launch_topk(const TopkParams& p, hipStream_t s) {
+  hipLaunchKernelGGL((score_topk_kernel<D, KM>), dim3((unsigned)ceil_div(p.nb, 64)), dim3(kBlock), 0, s, p);
+}
+template <int D>
+int dispatch_k(const TopkParams& p, hipStream_t s) {
+  if (p.k <= 32) launch_topk<D, 32>(p, s);
+  else if (p.k <= 64) launch_topk<D, 64>(p, s);
+  else launch_topk<D, 128>(p, s);
+  return check_launch("score_topk");
+}
+}  // namespace
+
+extern "C" int gnnrec_score_topk_f32(const float* u, int64_t ldu, int64_t n_users_batch,
+                                     const float* v, int64_t ldv, int64_t n_items, int32_t d,
+                                     const int64_t* seen_ptr, const int32_t* seen_col, int32_t k,
+                                     int64_t* out_idx, float* out_score, gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(n_users_batch >= 0 && n_items >= 0 && k >= 1 && k <= 128, "score_topk: need 1 <= k <= 128");
+  if (n_users_batch == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(n_items < (int64_t)INT32_MAX, "score_topk: n_items must fit int32");
+  GNNREC_REQUIRE(u && v && out_idx && out_score, "score_topk: null operand");
+  GNNREC_REQUIRE(ldu >= d && ldv >= d && aligned16(v) && !(ldv & 3), "score_topk: v must be 16-B aligned rows");
+  GNNREC_REQUIRE(!seen_ptr || seen_col || n_users_batch == 0, "score_topk: seen_ptr without seen_col");
+  const TopkParams p{u, ldu, n_users_batch, v, ldv, n_items, seen_ptr, seen_col, k, out_idx, out_score};
+  hipStream_t s = as_hip(stream);
+  switch (d) {
+    case 16: return dispatch_k<16>(p, s);
+    case 32: return dispatch_k<32>(p, s);
+    case 64: return dispatch_k<64>(p, s);
+    case 128: return dispatch_k<128>(p, s);
+    default: set_error("score_topk: d=%d unsupported (16, 32, 64, 128)", d); return GNNREC_EUNSUPPORTED;
+  }
+}

@@ -19,10 +19,10 @@ import torch
 from .graph import CsrGraph, ShardInfo, inv_sqrt_degrees
 from . import functional
 from .functional import (dense_layer, gas, gat_aggregate, lightgcn_propagate, ngcf_layer,
-                         spmm, spmm_gas)
+                         score_topk, spmm, spmm_gas)
 
 __all__ = ["CsrGraph", "ShardInfo", "inv_sqrt_degrees", "functional", "spmm", "spmm_gas",
-           "gas", "ngcf_layer", "dense_layer", "gat_aggregate", "lightgcn_propagate", "as_operand",
+           "gas", "ngcf_layer", "dense_layer", "gat_aggregate", "score_topk", "lightgcn_propagate", "as_operand",
            "sparse_mm", "uses_native"]
 
 _CACHE: dict = {}

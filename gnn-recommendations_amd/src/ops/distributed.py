@@ -79,6 +79,11 @@ class DistributedGraph:
     def all_gather(self, out: torch.Tensor, piece: torch.Tensor) -> None:
         if self.world == 1:
             out.copy_(piece)
+        elif out.is_cuda and dist.get_backend(self.group) == "gloo":
+            # test harness only (several ranks sharing one GPU): stage through the host
+            host = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_gather_into_tensor(host, piece.cpu(), group=self.group)
+            out.copy_(host)
         else:
             dist.all_gather_into_tensor(out, piece, group=self.group)
 

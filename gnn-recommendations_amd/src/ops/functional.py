@@ -237,3 +237,28 @@ def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh:
         acc.stride(0) if acc is not None else width, float(acc_div), _lib.stream_of(adj.device)),
         "gnnrec_gat_aggregate_f32")
     return out
+
+
+def score_topk(user_emb: torch.Tensor, item_emb: torch.Tensor, k: int,
+               seen_ptr: Optional[torch.Tensor] = None,
+               seen_col: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Top-k items per user by score = sequential-fmaf dot product, seen items excluded,
+    order (score desc, item index asc) (gnnrec_score_topk_f32; evaluator.py:96-105).
+    seen_ptr [B+1] int64 / seen_col int32: per-user sorted seen item lists (CSR)."""
+    u = _rowmajor(user_emb)
+    v = _rowmajor(item_emb)
+    if not (u.is_cuda and v.is_cuda and u.device == v.device):
+        raise ValueError("score_topk needs both tables on the same ROCm device")
+    if u.dtype != torch.float32 or v.dtype != torch.float32:
+        raise TypeError("score_topk needs float32 tables")
+    B, d = u.shape
+    idx = torch.empty((B, k), dtype=torch.int64, device=u.device)
+    sc = torch.empty((B, k), dtype=torch.float32, device=u.device)
+    if seen_ptr is not None:
+        seen_ptr = seen_ptr.to(u.device, torch.int64).contiguous()
+        seen_col = seen_col.to(u.device, torch.int32).contiguous()
+    check(_lib.lib().gnnrec_score_topk_f32(ptr(u), u.stride(0), B, ptr(v), v.stride(0),
+                                           v.shape[0], d, ptr(seen_ptr), ptr(seen_col), int(k),
+                                           ptr(idx), ptr(sc), _lib.stream_of(u.device)),
+          "gnnrec_score_topk_f32")
+    return idx, sc
