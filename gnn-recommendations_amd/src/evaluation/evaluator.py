@@ -1,0 +1,96 @@
+"""Test-time evaluation over the native scoring/top-K kernel (reference: evaluator.py:52-124).
+
+Propagate once, then for batches of users one kernel scores every item (MFMA, sequential-k
+fmaf order), masks the train+valid items and keeps the top-K under the fixed order
+(score desc, item asc) — instead of U[b] @ I^T + a Python masking loop + torch.topk + copy.
+On CPU operands the same semantics run in torch (stable sort for the tie order).
+"""
+from __future__ import annotations
+
+from collections import defaultdict
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..ops import CsrGraph, score_topk, uses_native
+
+
+def compute_metrics_from_topk(topk_items, user_ids: List[int], ground_truth: Dict[int, List[int]],
+                              n_items: int, k_values=(10, 20)) -> Dict[str, float]:
+    """recall / ndcg / precision / coverage / gini @k (metrics.py:355-432)."""
+    topk = np.asarray(topk_items.cpu() if torch.is_tensor(topk_items) else topk_items)
+    if topk.size == 0:
+        return {}
+    out = {}
+    for k in k_values:
+        k = min(k, topk.shape[1])
+        rec, nd, pre = [], [], []
+        disc = 1.0 / np.log2(np.arange(k) + 2)
+        for row, u in enumerate(user_ids):
+            rel = set(ground_truth.get(u, ()))
+            if not rel:
+                continue
+            pred = topk[row, :k]
+            hit = np.array([p in rel for p in pred])
+            rec.append(hit.sum() / len(rel))
+            pre.append(hit.sum() / k)
+            idcg = disc[:min(len(rel), k)].sum()
+            nd.append((disc * hit).sum() / idcg if idcg > 0 else 0.0)
+        out[f"recall@{k}"] = float(np.mean(rec)) if rec else 0.0
+        out[f"ndcg@{k}"] = float(np.mean(nd)) if nd else 0.0
+        out[f"precision@{k}"] = float(np.mean(pre)) if pre else 0.0
+        flat = topk[:, :k].ravel()
+        flat = flat[flat >= 0]
+        out[f"coverage@{k}"] = len(set(flat.tolist())) / max(1, n_items)
+        counts = np.sort(np.bincount(flat, minlength=n_items))
+        n = counts.size
+        out[f"gini@{k}"] = float(2 * np.sum((np.arange(n) + 1) * counts) / (n * counts.sum())
+                                 - (n + 1) / n) if counts.sum() > 0 else 0.0
+    return out
+
+
+class Evaluator:
+    def __init__(self, k_values=(10, 20), device: Optional[torch.device] = None):
+        self.k_values = list(k_values)
+        self.device = device or torch.device("cuda" if torch.cuda.is_available() else "cpu")
+
+    def topk(self, user_emb, item_emb, users, k, seen_ptr, seen_col, batch_size=2048):
+        """[len(users), k] int64 top-k item ids (fixed tie order)."""
+        rows = []
+        for s in range(0, len(users), batch_size):
+            b = torch.as_tensor(users[s:s + batch_size], dtype=torch.long, device=user_emb.device)
+            bp = seen_ptr[b.cpu().numpy()]
+            counts = seen_ptr[b.cpu().numpy() + 1] - bp
+            sub_ptr = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+            sub_col = np.concatenate([seen_col[p:p + c] for p, c in zip(bp, counts)]) \
+                if counts.sum() else np.zeros(0, np.int32)
+            if user_emb.is_cuda:
+                idx, _ = score_topk(user_emb[b], item_emb, k, torch.from_numpy(sub_ptr),
+                                    torch.from_numpy(sub_col.astype(np.int32)))
+            else:
+                sc = user_emb[b] @ item_emb.T
+                for r in range(len(b)):
+                    sc[r, torch.from_numpy(sub_col[sub_ptr[r]:sub_ptr[r + 1]].astype(np.int64))] = float("-inf")
+                order = torch.sort(sc, dim=1, descending=True, stable=True).indices
+                idx = order[:, :k]
+            rows.append(idx.cpu())
+        return torch.cat(rows)
+
+    def evaluate(self, model, dataset, test_data=None, adj_matrix=None) -> Dict[str, float]:
+        model.eval()
+        test_data = dataset.test_data if test_data is None else test_data
+        with torch.no_grad():
+            adj = adj_matrix if adj_matrix is not None else (
+                dataset.get_graph(self.device) if self.device.type == "cuda"
+                else dataset.get_torch_adjacency())
+            user_emb, item_emb = model.get_all_embeddings(adj)
+            gt = defaultdict(list)
+            for u, i in zip(test_data["userId"].to_numpy(), test_data["itemId"].to_numpy()):
+                gt[int(u)].append(int(i))
+            users = sorted(gt)
+            if not users:
+                return {}
+            seen_ptr, seen_col = dataset.seen_items()
+            topk = self.topk(user_emb, item_emb, users, max(self.k_values), seen_ptr, seen_col)
+            return compute_metrics_from_topk(topk, users, gt, dataset.n_items, self.k_values)

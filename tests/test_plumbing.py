@@ -1,0 +1,67 @@
+"""Host plumbing around the path (CPU): the graph_builder API, dataset split, run_all.py."""
+import json
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from conftest import PKG, load_golden
+
+from src.data import (build_bipartite_graph, build_csr_graph, convert_to_torch_sparse,
+                      load_adjacency_matrix, normalize_adjacency_matrix, save_adjacency_matrix)
+from src.data.dataset import RecommendationDataset
+from src.evaluation import compute_metrics_from_topk
+
+
+@pytest.mark.parametrize("name", ["g_small", "g_dup", "g_selfloop"])
+def test_graph_builder_api_matches_reference(name, tmp_path):
+    g = load_golden(f"graph_{name}")
+    df = pd.DataFrame({"userId": g["users"], "itemId": g["items"]})
+    adj = build_bipartite_graph(df, int(g["n_users"]), int(g["n_items"]),
+                                self_loop=bool(g["self_loop"]))
+    norm = normalize_adjacency_matrix(adj)
+    np.testing.assert_array_equal(norm.row, g["row"])
+    np.testing.assert_array_equal(norm.col, g["col"])
+    np.testing.assert_array_equal(norm.data.view(np.uint32), g["val"].view(np.uint32))
+    t = convert_to_torch_sparse(norm)
+    assert t.dtype == torch.float32 and t._indices().dtype == torch.int64 and not t.is_coalesced()
+    for fmt in ("npz", "pt"):
+        p = str(tmp_path / f"a.{fmt}")
+        save_adjacency_matrix(norm, p, fmt)
+        back = load_adjacency_matrix(p, fmt).tocsr()
+        assert (abs(back - norm.tocsr()) > 0).nnz == 0
+    G = build_csr_graph(df, int(g["n_users"]), int(g["n_items"]), self_loop=bool(g["self_loop"]))
+    np.testing.assert_array_equal(G.val.numpy().view(np.uint32), g["val"].view(np.uint32))
+
+
+def test_temporal_split_rules():
+    r = pd.DataFrame({"userId": [1, 1, 1, 1, 2, 2, 3] * 1, "itemId": [10, 11, 12, 13, 10, 11, 12],
+                      "rating": [5] * 7, "timestamp": [4, 1, 3, 2, 9, 8, 1]})
+    ds = RecommendationDataset.from_ratings(r, min_user=1, min_item=1)
+    # user 1 (4 items): last (t=4, item 10) test, t=3 (item 12) valid, rest train
+    assert len(ds.test_data) == 2 and len(ds.valid_data) == 1
+    assert len(ds.train_data) == 4
+    assert ds.n_users == 3 and ds.n_items == 4
+
+
+def test_metrics_from_topk():
+    topk = np.array([[0, 1, 2], [3, 4, 5]])
+    m = compute_metrics_from_topk(topk, [0, 1], {0: [1], 1: [9]}, n_items=10, k_values=[2])
+    assert m["recall@2"] == 0.5 and m["precision@2"] == 0.25
+    assert abs(m["ndcg@2"] - 0.5 * (1 / np.log2(3))) < 1e-12
+
+
+def test_run_all_config1_cpu(tmp_path):
+    """BASELINE config 1: LightGCN K=1 d=32 on the ML-100K shape through run_all.py (CPU)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("run_all", PKG / "run_all.py")
+    ra = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ra)
+    out = tmp_path / "r.json"
+    rc = ra.main(["--quick", "--skip-check", "--models", "lightgcn", "--n_layers", "1",
+                  "--embedding_dim", "32", "--device", "cpu", "--epochs", "1",
+                  "--output", str(out)])
+    res = json.loads(out.read_text())
+    assert rc == 0 and res[0]["status"] == "success"
+    assert 0.0 <= res[0]["test_metrics"]["recall@10"] <= 1.0

@@ -55,3 +55,33 @@ def test_topk_fewer_items_than_k(cuda):
     oi, osc = oracle.score_topk(U.cpu().numpy(), I.cpu().numpy(), 16)
     np.testing.assert_array_equal(idx.cpu().numpy(), oi)
     assert (idx[:, 10:] == -1).all() and torch.isinf(sc[:, 10:]).all()
+
+
+def test_evaluator_native_matches_cpu_path(cuda):
+    from src.data.dataset import RecommendationDataset
+    from src.evaluation import Evaluator
+    from src.models import LightGCN
+    ds = RecommendationDataset.synthetic_movielens(n_users=300, n_items=500, n_ratings=8000)
+    torch.manual_seed(0)
+    m = LightGCN(ds.n_users, ds.n_items, embedding_dim=64, n_layers=2, init_scale=0.1)
+    cpu = Evaluator(device=torch.device("cpu")).evaluate(m, ds)
+    gpu = Evaluator(device=cuda).evaluate(m.to(cuda), ds)
+    assert cpu.keys() == gpu.keys()
+    for k in cpu:  # same embeddings; only near-tie order between MKL and fmaf scores may move
+        assert abs(cpu[k] - gpu[k]) < 5e-3, (k, cpu[k], gpu[k])
+
+
+@pytest.mark.parametrize("model", ["lightgcn", "ngcf", "ngcf_gs", "orthogonal_bundle", "gat"])
+def test_run_all_on_gpu(cuda, model, tmp_path):
+    import importlib.util
+    import json
+    from conftest import PKG
+    spec = importlib.util.spec_from_file_location("run_all", PKG / "run_all.py")
+    ra = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ra)
+    out = tmp_path / "r.json"
+    rc = ra.main(["--quick", "--skip-check", "--models", model, "--epochs", "1",
+                  "--device", "cuda", "--output", str(out)])
+    res = json.loads(out.read_text())
+    assert rc == 0, res
+    assert res[0]["status"] == "success"
