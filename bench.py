@@ -175,6 +175,9 @@ def main(argv=None) -> int:
     ap.add_argument("--verify", action="store_true",
                     help="after timing, compare this rank's rows bit for bit with a single-device "
                          "propagation of the whole graph")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "allgather", "p2p"],
+                    help="per-hop exchange: allgather, bipartite point-to-point, or auto "
+                         "(time both before the timed region, keep the faster)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: test harness for several ranks sharing one GPU (host-staged "
                          "all-gather); the benchmark itself uses nccl = RCCL")
@@ -210,7 +213,8 @@ def main(argv=None) -> int:
     x0 = torch.randn(N, d, dtype=torch.float32) * 0.1  # nn.init.normal_(std=init_scale=0.1)
 
     t0 = time.perf_counter()
-    dg = DistributedGraph(full, rank, world, device)
+    dg = DistributedGraph(full, rank, world, device,
+                          exchange="p2p" if a.exchange == "auto" else a.exchange)
     src = distinct_cols(dg.shard, dg.shard.shape[1])
     x0_pad = dg.pad_table(x0)
     work = make_work(dg, d, device)
@@ -222,9 +226,37 @@ def main(argv=None) -> int:
     del full
 
     timer = HopTimer()
+    chunks = 1
 
     def step():
-        return lightgcn_propagate_dist(dg, x0_pad, K, hop_fn=timer.hop, work=work)
+        return lightgcn_propagate_dist(dg, x0_pad, K, hop_fn=timer.hop, work=work,
+                                       overlap_chunks=chunks)
+
+    # Exchange form (N > 1): time whole steps of each candidate before the timed region and
+    # keep the fastest (same decision on every rank: max over ranks).
+    exchange_info = {"mode": dg.exchange_mode, "overlap_chunks": 1}
+    if world > 1:
+        cands = [("allgather", 1)]
+        if not bool(dg.needs.all()) and a.exchange in ("auto", "p2p"):
+            cands = ([] if a.exchange == "p2p" else cands) + [("p2p", 1), ("p2p", 4), ("p2p", 8)]
+        elif a.exchange == "p2p":
+            cands = [("p2p", 1)]
+        tried = {}
+        for mode, ch in cands:
+            dg.exchange_mode, chunks = mode, ch
+            step()
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize()
+            tt = torch.tensor([(time.perf_counter() - t0) / 3 * 1e3], dtype=torch.float64, device=device)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            tried[f"{mode}_x{ch}_ms"] = float(tt.item())
+        best = min(cands, key=lambda c: tried[f"{c[0]}_x{c[1]}_ms"])
+        dg.exchange_mode, chunks = best
+        exchange_info = {"mode": best[0], "overlap_chunks": best[1], "candidates_ms_per_step": tried}
 
     for _ in range(a.warmup):
         step()
@@ -250,7 +282,9 @@ def main(argv=None) -> int:
     durs = timer.durations_ms()
     per_hop = hop_bytes(dg.shard.nnz, dg.n_local, src, d, K, world)
     launch_bytes = float(np.mean(per_hop))
-    launch_ms = float(np.mean(durs))
+    # kernel time per hop (= per launch at N=1; the sum of its chunk launches when the hop is
+    # split into overlap chunks)
+    launch_ms = float(np.sum(durs)) / (a.steps * K)
     achieved = launch_bytes / (launch_ms * 1e-3) / 1e9
 
     # cross-rank totals
@@ -296,7 +330,9 @@ def main(argv=None) -> int:
                             + ("G100M" if nnz_total == G100M_NNZ else f"{a.users}x{a.items} synthetic"),
                 "graph": f"{a.users} users x {a.items} items, {a.pairs} pairs default_rng({a.seed}), deduplicated",
                 "nnz": int(nnz_total), "n_nodes": N, "n_layers": K, "dim": d,
-                "parallelism": f"dst-row shards x{world}" + (" + per-hop RCCL all-gather" if world > 1 else ""),
+                "parallelism": f"dst-row shards x{world}" + (
+                    f" + per-hop RCCL exchange ({exchange_info['mode']}, "
+                    f"{exchange_info['overlap_chunks']} overlap chunks)" if world > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm",
@@ -313,6 +349,8 @@ def main(argv=None) -> int:
             "edges_per_s_per_interaction": value / 2.0,
             "hbm_gbps_algorithmic_step": K * launch_bytes * world / (ms_per_step * 1e-3) / 1e9,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
+            "exchange": dict(exchange_info, recv_bytes_per_hop_per_rank=dg.recv_rows() * d * 4)
+            if world > 1 else None,
         }
         if check:
             line["verify"] = check

@@ -49,20 +49,28 @@ struct DenseParams {
   float w_out, w_res;
 };
 
-template <int D, int MODE>
-__global__ __launch_bounds__(kBlock) void spmm_mfma_kernel(DenseParams p) {
-  constexpr int GROUP = D / 4;
+// GATHER = true: the A rows are gathered here (fused hop). GATHER = false: p.x already holds
+// the hop output n = A x (rows read straight, float4 per lane) and only the transform runs.
+template <int D, int MODE, int NW, bool GATHER>
+__global__ __launch_bounds__(64 * NW) void spmm_mfma_kernel(DenseParams p) {
+  constexpr int NTH = 64 * NW;
+  // gather mapping of the plain hop (SpmmCfg, gather.h): VEC features per lane
+  constexpr int VEC = GATHER ? SpmmCfg<D>::VEC : 4, CH = SpmmCfg<D>::CH;
+  constexpr int GROUP = D / VEC;
   constexpr int RPW = 64 / GROUP;
-  constexpr int PASS_ROWS = RPW * (kBlock / 64);
-  constexpr int TR = PASS_ROWS > 16 ? PASS_ROWS : 16;  // rows per tile
+  constexpr int PASS_ROWS = RPW * NW;
+  constexpr int TR = PASS_ROWS > 4 * NW ? PASS_ROWS : 4 * NW;  // rows per tile (16 per 4 waves)
   constexpr int PASSES = TR / PASS_ROWS;
   constexpr int KD = MODE == 0 ? 2 * D : D;  // contraction length
-  constexpr int LDA = KD + 2;                // == 2 mod 32: conflict-free ds_read_b32 A reads
+  constexpr int LDA = KD + 2;                // == 2 mod 32: conflict-free A-fragment reads
+  constexpr int LDB = D + 16;                // == 16 mod 32: conflict-free B-fragment reads
+  constexpr bool B_LDS = KD * LDB * 4 <= 48 * 1024;
   constexpr int MT = TR / 16, NT = D / 16, TILES = MT * NT;
-  constexpr int TPW = (TILES + 3) / 4;  // MFMA output tiles per wave
+  constexpr int TPW = (TILES + NW - 1) / NW;  // MFMA output tiles per wave
   constexpr int STEPS = KD / 4;
   __shared__ __attribute__((aligned(16))) float a_lds[TR * LDA];
   __shared__ __attribute__((aligned(16))) float o_lds[TR][D + 4];
+  __shared__ __attribute__((aligned(16))) float b_lds[B_LDS ? KD * LDB : 4];
   __shared__ __attribute__((aligned(16))) float w_gas[MODE == 0 ? D * 32 : 4];
 
   const int lane = threadIdx.x & 63;
@@ -70,33 +78,41 @@ __global__ __launch_bounds__(kBlock) void spmm_mfma_kernel(DenseParams p) {
   const int gl = lane % GROUP;
   const int i16 = lane & 15, k4 = lane >> 4;
 
-  // Weight slabs -> VGPRs, once per workgroup.
-  float bf[TPW][STEPS];
+  // B = [W1^T ; W2^T] (MODE 0) or M (MODE 1), K-major: B[k][j]
+  auto bval = [&](int k, int j) -> float {
+    if (MODE == 0) return k < D ? p.W1[j * D + k] : p.W2[j * D + (k - D)];
+    return p.M[k * D + j];
+  };
+  float bf[B_LDS ? 1 : TPW][B_LDS ? 1 : STEPS];
+  if constexpr (B_LDS) {
+    for (int e = threadIdx.x; e < KD * D; e += NTH) b_lds[(e / D) * LDB + e % D] = bval(e / D, e % D);
+  } else {
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      const int t = wave + NW * i;
+      const int j = 16 * ((t < TILES ? t : 0) % NT) + i16;
+#pragma unroll
+      for (int s = 0; s < STEPS; ++s) bf[i][s] = bval(4 * s + k4, j);
+    }
+  }
   float bias1[TPW], bias2[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
-    const int t = wave + 4 * i;
+    const int t = wave + NW * i;
     const int j = 16 * ((t < TILES ? t : 0) % NT) + i16;
-#pragma unroll
-    for (int s = 0; s < STEPS; ++s) {
-      const int k = 4 * s + k4;
-      if (MODE == 0)
-        bf[i][s] = k < D ? p.W1[j * D + k] : p.W2[j * D + (k - D)];
-      else
-        bf[i][s] = p.M[k * D + j];
-    }
-    if (MODE == 0) {
-      bias1[i] = p.b1[j];
-      bias2[i] = p.b2[j];
-    }
+    bias1[i] = MODE == 0 ? p.b1[j] : 0.f;
+    bias2[i] = MODE == 0 ? p.b2[j] : 0.f;
   }
   const bool gas = MODE == 0 && p.gas_blocks != nullptr;
-  int pj[4] = {0, 0, 0, 0};
-  if (gas) {
-    for (int i = threadIdx.x; i < D * p.gas_bs; i += kBlock) w_gas[i] = p.gas_blocks[i];
+  int pj[VEC];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) pj[q] = p.gas_perm[4 * gl + q];
+  for (int q = 0; q < VEC; ++q) pj[q] = 0;
+  if (gas) {
+    for (int i = threadIdx.x; i < D * p.gas_bs; i += NTH) w_gas[i] = p.gas_blocks[i];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) pj[q] = p.gas_perm[VEC * gl + q];
   }
+  __syncthreads();
 
   const int64_t n_tiles = ceil_div(p.A.n_rows, TR);
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
@@ -106,36 +122,42 @@ __global__ __launch_bounds__(kBlock) void spmm_mfma_kernel(DenseParams p) {
     for (int ps = 0; ps < PASSES; ++ps) {
       const int slot = ps * PASS_ROWS + wave * RPW + lane / GROUP;
       const int64_t r = row0 + slot;
-      float4 n = make_float4(0.f, 0.f, 0.f, 0.f), xs = n;
+      VecF<VEC> n, xs;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) n.v[q] = xs.v[q] = 0.f;
       if (r < p.A.n_rows) {
-        n = gather_row<GROUP>(p.A.col, p.A.val, p.A.row_ptr[r], p.A.row_ptr[r + 1], p.x, p.ldx, gl);
-        if (MODE == 0) xs = ld4(p.x_self + r * p.ld_self + 4 * gl);
+        if constexpr (GATHER)
+          n = gather_row_v<VEC, GROUP, CH>(p.A.col, p.A.val, p.A.row_ptr[r], p.A.row_ptr[r + 1],
+                                           p.x, p.ldx, gl);
+        else
+          n = ldv<VEC>(p.x + r * p.ldx + VEC * gl);
+        if (MODE == 0) xs = ldv<VEC>(p.x_self + r * p.ld_self + VEC * gl);
       }
-      float2* a2 = reinterpret_cast<float2*>(&a_lds[slot * LDA + 4 * gl]);
-      a2[0] = make_float2(n.x, n.y);
-      a2[1] = make_float2(n.z, n.w);
-      if (MODE == 0) {
-        float2* i2 = reinterpret_cast<float2*>(&a_lds[slot * LDA + D + 4 * gl]);
-        i2[0] = make_float2(xs.x * n.x, xs.y * n.y);
-        i2[1] = make_float2(xs.z * n.z, xs.w * n.w);
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) {
+        a_lds[slot * LDA + VEC * gl + q] = n.v[q];
+        if (MODE == 0) a_lds[slot * LDA + D + VEC * gl + q] = xs.v[q] * n.v[q];
       }
     }
     __syncthreads();
     // ---- phase 2: MFMA
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
-      const int t = wave + 4 * i;
+      const int t = wave + NW * i;
       if (t < TILES) {
         const int mt = t / NT, nt = t % NT;
         floatx4 c1 = {0.f, 0.f, 0.f, 0.f}, c2 = {0.f, 0.f, 0.f, 0.f};
         const float* arow = &a_lds[(16 * mt + i16) * LDA + k4];
+        const float* bcol = &b_lds[k4 * LDB + 16 * nt + i16];
 #pragma unroll
         for (int s = 0; s < STEPS; ++s) {
           const float a = arow[4 * s];
+          float b;
+          if constexpr (B_LDS) b = bcol[4 * s * LDB]; else b = bf[i][s];
           if (MODE == 0 && s >= STEPS / 2)
-            c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bf[i][s], c2, 0, 0, 0);
+            c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c2, 0, 0, 0);
           else
-            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bf[i][s], c1, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c1, 0, 0, 0);
         }
         const int j = 16 * nt + i16;
 #pragma unroll
@@ -158,29 +180,37 @@ __global__ __launch_bounds__(kBlock) void spmm_mfma_kernel(DenseParams p) {
       const int slot = ps * PASS_ROWS + wave * RPW + lane / GROUP;
       const int64_t r = row0 + slot;
       if (r >= p.A.n_rows) continue;
-      float4 o;
+      VecF<VEC> o;
       if (MODE == 0) {
-        o = gas ? gas_row<D>(&o_lds[slot][0], w_gas, p.gas_bs, pj) : ld4(&o_lds[slot][4 * gl]);
+        if (gas) {
+          o = gas_row_v<VEC>(&o_lds[slot][0], w_gas, p.gas_bs, pj);
+        } else {
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) o.v[q] = o_lds[slot][VEC * gl + q];
+        }
       } else {
-        const float4 t = ld4(&o_lds[slot][4 * gl]);
-        const float4 rs = p.resid ? ld4(p.resid + r * p.ld_resid + 4 * gl)
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
-        if (p.resid)
-          o = make_float4(p.c_out * t.x + p.c_res * rs.x, p.c_out * t.y + p.c_res * rs.y,
-                          p.c_out * t.z + p.c_res * rs.z, p.c_out * t.w + p.c_res * rs.w);
-        else
-          o = make_float4(p.c_out * t.x, p.c_out * t.y, p.c_out * t.z, p.c_out * t.w);
+        VecF<VEC> rs;
+        if (p.resid) rs = ldv<VEC>(p.resid + r * p.ld_resid + VEC * gl);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) {
+          const float t = o_lds[slot][VEC * gl + q];
+          o.v[q] = p.resid ? p.c_out * t + p.c_res * rs.v[q] : p.c_out * t;
+        }
         if (p.acc_mode) {
-          float* ar = p.acc + r * p.ld_acc + 4 * gl;
-          const float4 base =
-              p.acc_mode == 1
-                  ? make_float4(p.w_res * rs.x, p.w_res * rs.y, p.w_res * rs.z, p.w_res * rs.w)
-                  : ld4(ar);
-          st4(ar, make_float4(base.x + p.w_out * o.x, base.y + p.w_out * o.y,
-                              base.z + p.w_out * o.z, base.w + p.w_out * o.w));
+          float* ar = p.acc + r * p.ld_acc + VEC * gl;
+          VecF<VEC> base;
+          if (p.acc_mode == 1) {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) base.v[q] = p.w_res * rs.v[q];
+          } else {
+            base = ldv<VEC>(ar);
+          }
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) base.v[q] = base.v[q] + p.w_out * o.v[q];
+          stv<VEC>(ar, base);
         }
       }
-      if (p.y) st4(p.y + r * p.ldy + 4 * gl, o);
+      if (p.y) stv<VEC>(p.y + r * p.ldy + VEC * gl, o);
     }
   }
 }
@@ -191,21 +221,43 @@ using namespace gnnrec;
 
 namespace {
 
-template <int MODE>
+// Two forms (measured on G100M, tools/bench_configs.py config 3):
+//  * split (default when the caller passes a workspace): the plain hop kernel writes
+//    n = A x at full gather efficiency, then this kernel streams n (and x) rows through the
+//    MFMA transform: ~1 GB more HBM traffic per layer but the gather keeps the hop's
+//    occupancy;
+//  * fused (no workspace): gather + MFMA in one kernel.
+// Waves per workgroup: 8 for d <= 64 (weights in LDS), 4 for d = 128 (weights in VGPRs).
+template <int MODE, bool GATHER>
 int launch_dense(const DenseParams& p, int d, hipStream_t s) {
-  const int tr = (d == 32) ? 32 : 16;
-  const int64_t tiles = ceil_div(p.A.n_rows, tr);
-  const unsigned grid = (unsigned)(tiles < 2048 ? tiles : 2048);
+  auto go = [&](auto kern, int nw) {
+    const int64_t tiles = ceil_div(p.A.n_rows, 4 * nw);
+    const unsigned grid = (unsigned)(tiles < 2048 ? tiles : 2048);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * nw), 0, s, p);
+  };
   switch (d) {
-    case 32: hipLaunchKernelGGL((spmm_mfma_kernel<32, MODE>), dim3(grid), dim3(kBlock), 0, s, p); break;
-    case 64: hipLaunchKernelGGL((spmm_mfma_kernel<64, MODE>), dim3(grid), dim3(kBlock), 0, s, p); break;
-    case 128: hipLaunchKernelGGL((spmm_mfma_kernel<128, MODE>), dim3(grid), dim3(kBlock), 0, s, p); break;
+    case 32: go(spmm_mfma_kernel<32, MODE, 8, GATHER>, 8); break;
+    case 64: go(spmm_mfma_kernel<64, MODE, 8, GATHER>, 8); break;
+    case 128: go(spmm_mfma_kernel<128, MODE, 4, GATHER>, 4); break;
     default: set_error("dense epilogue: d=%d unsupported (32, 64, 128)", d); return GNNREC_EUNSUPPORTED;
   }
   return check_launch(MODE == 0 ? "spmm_ngcf" : "spmm_dense");
 }
 
-bool rows_ok(const float* p, int64_t ld) { return p && aligned16(p) && !(ld & 3); }
+// Runs the hop into `work` (n_rows x d) and the transform over it, or the fused kernel.
+template <int MODE>
+int run_dense(DenseParams p, int d, float* work, hipStream_t s) {
+  if (!work) return launch_dense<MODE, true>(p, d, s);
+  const int rc = gnnrec_spmm_csr_f32(p.A.row_ptr, p.A.col, p.A.val, p.A.n_rows, p.x, p.ldx, work,
+                                     d, d, 0, nullptr, d, nullptr, d, 1.f,
+                                     reinterpret_cast<gnnrec_stream_t>(s));
+  if (rc != GNNREC_OK) return rc;
+  p.x = work;
+  p.ldx = d;
+  return launch_dense<MODE, false>(p, d, s);
+}
+
+bool rows_ok(const float* p, int64_t ld) { return p && aligned16(p) && !(ld & 3); }  // float4 rows
 
 }  // namespace
 
@@ -214,7 +266,7 @@ extern "C" int gnnrec_spmm_ngcf_f32(const int64_t* row_ptr, const int32_t* col, 
                                     const float* x_self, int64_t ld_self, float* y, int64_t ldy,
                                     int32_t d, const float* W1, const float* b1, const float* W2,
                                     const float* b2, float slope, const float* gas_blocks,
-                                    const int32_t* gas_perm, int32_t gas_bs,
+                                    const int32_t* gas_perm, int32_t gas_bs, float* work,
                                     gnnrec_stream_t stream) {
   GNNREC_REQUIRE(n_rows >= 0, "spmm_ngcf: n_rows < 0");
   if (n_rows == 0) return GNNREC_OK;
@@ -231,7 +283,8 @@ extern "C" int gnnrec_spmm_ngcf_f32(const int64_t* row_ptr, const int32_t* col, 
   p.x = x; p.ldx = ldx; p.x_self = x_self; p.ld_self = ld_self; p.y = y; p.ldy = ldy;
   p.W1 = W1; p.b1 = b1; p.W2 = W2; p.b2 = b2; p.slope = slope;
   p.gas_blocks = gas_blocks; p.gas_perm = gas_perm; p.gas_bs = gas_bs;
-  return launch_dense<0>(p, d, as_hip(stream));
+  GNNREC_REQUIRE(!work || aligned16(work), "spmm_ngcf: work must be 16-B aligned");
+  return run_dense<0>(p, d, work, as_hip(stream));
 }
 
 extern "C" int gnnrec_spmm_dense_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
@@ -239,7 +292,7 @@ extern "C" int gnnrec_spmm_dense_f32(const int64_t* row_ptr, const int32_t* col,
                                      int64_t ldy, int32_t d, const float* M, float c_out,
                                      const float* resid, int64_t ld_resid, float c_res, float* acc,
                                      int64_t ld_acc, int32_t acc_mode, float w_out, float w_res,
-                                     gnnrec_stream_t stream) {
+                                     float* work, gnnrec_stream_t stream) {
   GNNREC_REQUIRE(n_rows >= 0, "spmm_dense: n_rows < 0");
   if (n_rows == 0) return GNNREC_OK;
   GNNREC_REQUIRE(row_ptr && col && val && M, "spmm_dense: null operand");
@@ -255,5 +308,6 @@ extern "C" int gnnrec_spmm_dense_f32(const int64_t* row_ptr, const int32_t* col,
   p.x = x; p.ldx = ldx; p.y = y; p.ldy = ldy;
   p.M = M; p.c_out = c_out; p.c_res = c_res; p.resid = resid; p.ld_resid = ld_resid;
   p.acc = acc; p.ld_acc = ld_acc; p.acc_mode = acc_mode; p.w_out = w_out; p.w_res = w_res;
-  return launch_dense<1>(p, d, as_hip(stream));
+  GNNREC_REQUIRE(!work || aligned16(work), "spmm_dense: work must be 16-B aligned");
+  return run_dense<1>(p, d, work, as_hip(stream));
 }

@@ -33,22 +33,46 @@ struct GatParams {
   float* acc;
   int64_t ld_acc;
   float acc_div;
+  int64_t max_row_len;  // rows longer than this are left to the split path (0: none)
 };
 
-template <int F>
-__global__ __launch_bounds__(kBlock) void gat_kernel(GatParams p) {
-  constexpr int GROUP = F / 4;
-  constexpr int RPW = 64 / GROUP;
-  const int lane = threadIdx.x & 63;
-  const int gl = lane % GROUP;
-  const int64_t r = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
-  if (r >= p.A.n_rows) return;
-  const int hl = p.o_dim / 4;  // lanes per head
+// Softmax normalisation + head mean + ELU + store + layer-mean epilogue of one row.
+template <int GROUP>
+__device__ __forceinline__ void gat_finish(const GatParams& p, int64_t r, float4 o, int gl) {
+  const int hl = p.o_dim / 4;
+  int owner_lanes = GROUP;
+  if (p.mean_heads) {  // mean over heads: lanes fg, fg+hl, ... hold the same features
+    const int fg = gl % hl;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q = 0; q < p.heads; ++q) {
+      const int src = fg + q * hl;
+      const float4 t = make_float4(__shfl(o.x, src, GROUP), __shfl(o.y, src, GROUP),
+                                   __shfl(o.z, src, GROUP), __shfl(o.w, src, GROUP));
+      s = q == 0 ? t : make_float4(s.x + t.x, s.y + t.y, s.z + t.z, s.w + t.w);
+    }
+    const float H = (float)p.heads;
+    o = make_float4(s.x / H, s.y / H, s.z / H, s.w / H);
+    owner_lanes = hl;
+  }
+  if (gl >= owner_lanes) return;
+  if (p.apply_elu) {
+    o.x = o.x > 0.f ? o.x : expm1f(o.x);
+    o.y = o.y > 0.f ? o.y : expm1f(o.y);
+    o.z = o.z > 0.f ? o.z : expm1f(o.z);
+    o.w = o.w > 0.f ? o.w : expm1f(o.w);
+  }
+  if (!(p.epi & GNNREC_EPI_NO_Y)) st4(p.out + r * p.ldo + 4 * gl, o);
+  acc_epilogue(p.epi, o, p.self + r * p.ld_self + 4 * gl, p.acc + r * p.ld_acc + 4 * gl, p.acc_div);
+}
+
+// Online-softmax accumulation of neighbours [beg, end) of row r (head of this lane).
+template <int GROUP>
+__device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, int64_t beg,
+                                               int64_t end, int gl, float& m, float& l,
+                                               float4& a) {
+  const int hl = p.o_dim / 4;
   const int head = gl / hl;
   const float ss = p.s_self[r * p.heads + head];
-  const int64_t beg = p.A.row_ptr[r], end = p.A.row_ptr[r + 1];
-  float m = -INFINITY, l = 0.f;
-  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int64_t k0 = beg; k0 < end; k0 += kChunk) {
     constexpr int PER = (GROUP >= kChunk) ? 1 : kChunk / GROUP;
     int cm[PER];
@@ -83,31 +107,82 @@ __global__ __launch_bounds__(kBlock) void gat_kernel(GatParams p) {
       }
     }
   }
+}
+
+template <int F>
+__global__ __launch_bounds__(kBlock) void gat_kernel(GatParams p) {
+  constexpr int GROUP = F / 4;
+  constexpr int RPW = 64 / GROUP;
+  const int lane = threadIdx.x & 63;
+  const int gl = lane % GROUP;
+  const int64_t r = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
+  if (r >= p.A.n_rows) return;
+  const int64_t beg = p.A.row_ptr[r], end = p.A.row_ptr[r + 1];
+  if (p.max_row_len > 0 && end - beg > p.max_row_len) return;  // heavy row: split path
+  float m = -INFINITY, l = 0.f;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  gat_accumulate<GROUP>(p, r, beg, end, gl, m, l, a);
   // softmax normalisation (l = 0 for an empty row -> 0/0 = NaN, like the reference)
-  float4 o = make_float4(a.x / l, a.y / l, a.z / l, a.w / l);
-  int owner_lanes = GROUP;
-  if (p.mean_heads) {  // mean over heads: lanes fg, fg+hl, ... hold the same features
-    const int fg = gl % hl;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int q = 0; q < p.heads; ++q) {
-      const int src = fg + q * hl;
-      const float4 t = make_float4(__shfl(o.x, src, GROUP), __shfl(o.y, src, GROUP),
-                                   __shfl(o.z, src, GROUP), __shfl(o.w, src, GROUP));
-      s = q == 0 ? t : make_float4(s.x + t.x, s.y + t.y, s.z + t.z, s.w + t.w);
-    }
-    const float H = (float)p.heads;
-    o = make_float4(s.x / H, s.y / H, s.z / H, s.w / H);
-    owner_lanes = hl;
+  gat_finish<GROUP>(p, r, make_float4(a.x / l, a.y / l, a.z / l, a.w / l), gl);
+}
+
+// Heavy rows, pass 1: one row group per segment -> partial (acc[F], m[H], l[H]).
+struct GatSplit {
+  const int64_t* seg_row;
+  const int64_t* seg_beg;
+  const int64_t* seg_end;
+  int64_t n_seg;
+  const int64_t* heavy_rows;
+  const int64_t* heavy_seg_ptr;
+  int64_t n_heavy;
+  float* work;  // [n_seg][F] acc | [n_seg][H] m | [n_seg][H] l
+};
+
+template <int F>
+__global__ __launch_bounds__(kBlock) void gat_partial_kernel(GatParams p, GatSplit sp) {
+  constexpr int GROUP = F / 4;
+  constexpr int RPW = 64 / GROUP;
+  const int lane = threadIdx.x & 63;
+  const int gl = lane % GROUP;
+  const int64_t sg = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
+  if (sg >= sp.n_seg) return;
+  float m = -INFINITY, l = 0.f;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  gat_accumulate<GROUP>(p, sp.seg_row[sg], sp.seg_beg[sg], sp.seg_end[sg], gl, m, l, a);
+  st4(sp.work + sg * F + 4 * gl, a);
+  const int hl = p.o_dim / 4;
+  if (gl % hl == 0) {
+    float* ml = sp.work + sp.n_seg * F;
+    ml[sg * p.heads + gl / hl] = m;
+    ml[sp.n_seg * p.heads + sg * p.heads + gl / hl] = l;
   }
-  if (gl >= owner_lanes) return;
-  if (p.apply_elu) {
-    o.x = o.x > 0.f ? o.x : expm1f(o.x);
-    o.y = o.y > 0.f ? o.y : expm1f(o.y);
-    o.z = o.z > 0.f ? o.z : expm1f(o.z);
-    o.w = o.w > 0.f ? o.w : expm1f(o.w);
+}
+
+// Heavy rows, pass 2: merge the segments of each heavy row (max-rescaled sums), finish.
+template <int F>
+__global__ __launch_bounds__(kBlock) void gat_merge_kernel(GatParams p, GatSplit sp) {
+  constexpr int GROUP = F / 4;
+  constexpr int RPW = 64 / GROUP;
+  const int lane = threadIdx.x & 63;
+  const int gl = lane % GROUP;
+  const int64_t h = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
+  if (h >= sp.n_heavy) return;
+  const int hl = p.o_dim / 4, head = gl / hl;
+  const float* mm = sp.work + sp.n_seg * F;
+  const float* ll = mm + sp.n_seg * p.heads;
+  const int64_t s0 = sp.heavy_seg_ptr[h], s1 = sp.heavy_seg_ptr[h + 1];
+  float M = -INFINITY;
+  for (int64_t s = s0; s < s1; ++s) M = fmaxf(M, mm[s * p.heads + head]);
+  float L = 0.f;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t s = s0; s < s1; ++s) {
+    const float w = expf(mm[s * p.heads + head] - M);
+    const float4 t = ld4(sp.work + s * F + 4 * gl);
+    L = __builtin_fmaf(ll[s * p.heads + head], w, L);
+    a = make_float4(__builtin_fmaf(t.x, w, a.x), __builtin_fmaf(t.y, w, a.y),
+                    __builtin_fmaf(t.z, w, a.z), __builtin_fmaf(t.w, w, a.w));
   }
-  if (!(p.epi & GNNREC_EPI_NO_Y)) st4(p.out + r * p.ldo + 4 * gl, o);
-  acc_epilogue(p.epi, o, p.self + r * p.ld_self + 4 * gl, p.acc + r * p.ld_acc + 4 * gl, p.acc_div);
+  gat_finish<GROUP>(p, sp.heavy_rows[h], make_float4(a.x / L, a.y / L, a.z / L, a.w / L), gl);
 }
 
 }  // namespace gnnrec
@@ -120,7 +195,7 @@ extern "C" int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* c
                                         float slope, int32_t mean_heads, int32_t apply_elu,
                                         float* out, int64_t ldo, int32_t epi, const float* self,
                                         int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
-                                        gnnrec_stream_t stream) {
+                                        int64_t max_row_len, gnnrec_stream_t stream) {
   GNNREC_REQUIRE(n_rows >= 0 && heads >= 1 && o_dim >= 4 && o_dim % 4 == 0, "gat: bad sizes");
   if (n_rows == 0) return GNNREC_OK;
   const int F = heads * o_dim;
@@ -135,7 +210,7 @@ extern "C" int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* c
                      (acc && aligned16(acc) && !(ld_acc & 3) && ld_acc >= width),
                  "gat: ACC needs 16-B aligned acc");
   GatParams p{Csr{row_ptr, col, nullptr, n_rows}, hfeat, ldh, s_self, s_neigh, heads, o_dim, slope,
-              mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div};
+              mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, max_row_len};
   hipStream_t s = as_hip(stream);
   auto grid = [&](int f) { return dim3((unsigned)ceil_div(n_rows, (64 / (f / 4)) * (kBlock / 64))); };
   switch (F) {
@@ -147,4 +222,38 @@ extern "C" int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* c
     default: set_error("gat: heads*o_dim = %d unsupported (16..256, power of two)", F); return GNNREC_EUNSUPPORTED;
   }
   return check_launch("gat_aggregate");
+}
+
+extern "C" int gnnrec_gat_heavy_f32(const int32_t* col, const int64_t* seg_row,
+                                    const int64_t* seg_beg, const int64_t* seg_end, int64_t n_seg,
+                                    const int64_t* heavy_rows, const int64_t* heavy_seg_ptr,
+                                    int64_t n_heavy, float* work, const float* hfeat, int64_t ldh,
+                                    const float* s_self, const float* s_neigh, int32_t heads,
+                                    int32_t o_dim, float slope, int32_t mean_heads,
+                                    int32_t apply_elu, float* out, int64_t ldo, int32_t epi,
+                                    const float* self, int64_t ld_self, float* acc, int64_t ld_acc,
+                                    float acc_div, gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(n_seg >= 0 && n_heavy >= 0 && heads >= 1 && o_dim >= 4 && o_dim % 4 == 0,
+                 "gat_heavy: bad sizes");
+  if (n_heavy == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(col && seg_row && seg_beg && seg_end && heavy_rows && heavy_seg_ptr && work &&
+                     hfeat && s_self && s_neigh && aligned16(work) && aligned16(hfeat) && !(ldh & 3),
+                 "gat_heavy: null or misaligned operand");
+  const int F = heads * o_dim;
+  GatParams p{Csr{nullptr, col, nullptr, 0}, hfeat, ldh, s_self, s_neigh, heads, o_dim, slope,
+              mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, 0};
+  GatSplit sp{seg_row, seg_beg, seg_end, n_seg, heavy_rows, heavy_seg_ptr, n_heavy, work};
+  hipStream_t s = as_hip(stream);
+  auto g = [&](int64_t n, int f) { return dim3((unsigned)ceil_div(n, (64 / (f / 4)) * (kBlock / 64))); };
+  switch (F) {
+#define GAT_HEAVY(FF)                                                                          \
+  case FF:                                                                                     \
+    hipLaunchKernelGGL(gat_partial_kernel<FF>, g(n_seg, FF), dim3(kBlock), 0, s, p, sp);       \
+    hipLaunchKernelGGL(gat_merge_kernel<FF>, g(n_heavy, FF), dim3(kBlock), 0, s, p, sp);       \
+    break;
+    GAT_HEAVY(16) GAT_HEAVY(32) GAT_HEAVY(64) GAT_HEAVY(128) GAT_HEAVY(256)
+#undef GAT_HEAVY
+    default: set_error("gat_heavy: heads*o_dim = %d unsupported", F); return GNNREC_EUNSUPPORTED;
+  }
+  return check_launch("gat_heavy");
 }

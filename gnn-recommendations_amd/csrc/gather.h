@@ -182,6 +182,13 @@ __device__ __forceinline__ void acc_epilogue_v(int epi, const VecF<VEC>& y, cons
   stv<VEC>(acc_row, b);
 }
 
+// Lane mapping per d, from the G100M sweep (tools/exp_prod.py, profiles/r01/): VEC features
+// per lane, GROUP = d / VEC lanes per row, CH neighbours in flight per step.
+template <int D> struct SpmmCfg { static constexpr int VEC = 4, CH = 16; };
+template <> struct SpmmCfg<32> { static constexpr int VEC = 2, CH = 16; };
+template <> struct SpmmCfg<64> { static constexpr int VEC = 1, CH = 8; };   // wave per row
+template <> struct SpmmCfg<128> { static constexpr int VEC = 2, CH = 16; };  // wave per row
+
 // ---- GAS (block-diagonal orthogonal transform + column shuffle) -----------------------
 // y[r, j] = sum_{c<bs} z[r, bs*b + c] * W_b[c, e],  perm[j] = bs*b + e  (sequential fmaf in c).
 // The row z is parked in LDS so every lane can read the bs inputs of its 4 outputs.
@@ -199,6 +206,23 @@ __device__ __forceinline__ float4 gas_row(const float* zrow_lds, const float* w_
     o[q] = s;
   }
   return make_float4(o[0], o[1], o[2], o[3]);
+}
+
+// VEC-output form: outputs j = VEC*gl + q, q < VEC (pj holds perm[VEC*gl + q]).
+template <int VEC>
+__device__ __forceinline__ VecF<VEC> gas_row_v(const float* zrow_lds, const float* w_lds, int bs,
+                                               const int (&pj)[VEC]) {
+  VecF<VEC> o;
+#pragma unroll
+  for (int q = 0; q < VEC; ++q) {
+    const int b = pj[q] / bs, e = pj[q] - b * bs;
+    const float* z = zrow_lds + b * bs;
+    const float* w = w_lds + (b * bs) * bs + e;
+    float s = 0.f;
+    for (int c = 0; c < bs; ++c) s = __builtin_fmaf(z[c], w[c * bs], s);
+    o.v[q] = s;
+  }
+  return o;
 }
 
 // LightGCN layer-mean epilogue (see GNNREC_EPI_* in gnnrec.h).

@@ -11,13 +11,6 @@
 
 namespace gnnrec {
 
-// Lane mapping per d, from the G100M sweep (tools/exp_prod.py, profiles/r01/): VEC features
-// per lane, GROUP = d / VEC lanes per row, CH neighbours in flight per step.
-template <int D> struct SpmmCfg { static constexpr int VEC = 4, CH = 16; };
-template <> struct SpmmCfg<32> { static constexpr int VEC = 2, CH = 16; };
-template <> struct SpmmCfg<64> { static constexpr int VEC = 1, CH = 8; };   // wave per row
-template <> struct SpmmCfg<128> { static constexpr int VEC = 2, CH = 16; };  // wave per row
-
 template <int D>
 __global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
     Csr A, const float* __restrict__ x, int64_t ldx, float* __restrict__ y, int64_t ldy,

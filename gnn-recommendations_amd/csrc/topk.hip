@@ -227,6 +227,7 @@ extern "C" int gnnrec_score_topk_f32(const float* u, int64_t ldu, int64_t n_user
     case 32: return dispatch_k<32>(p, s);
     case 64: return dispatch_k<64>(p, s);
     case 128: return dispatch_k<128>(p, s);
-    default: set_error("score_topk: d=%d unsupported (16, 32, 64, 128)", d); return GNNREC_EUNSUPPORTED;
+    case 256: return dispatch_k<256>(p, s);
+    default: set_error("score_topk: d=%d unsupported (16, 32, 64, 128, 256)", d); return GNNREC_EUNSUPPORTED;
   }
 }

@@ -27,6 +27,7 @@ class NGCFLayer(nn.Module):
         self.W2 = nn.Linear(in_dim, out_dim, bias=True)
         self.dropout = nn.Dropout(dropout)
         self.activation = nn.LeakyReLU(negative_slope=0.2)
+        self.single_kernel = False  # True: gather + MFMA in one launch (see ops.ngcf_layer)
 
     def _fused_ok(self, x: torch.Tensor, a) -> bool:
         return (isinstance(a, CsrGraph) and not (torch.is_grad_enabled() and (
@@ -41,7 +42,7 @@ class NGCFLayer(nn.Module):
             blocks, perm = (gas.blocks(), gas.perm) if gas is not None else (None, None)
             return ops.ngcf_layer(a, x, self.W1.weight, self.W1.bias, self.W2.weight,
                                   self.W2.bias, self.activation.negative_slope,
-                                  gas_blocks=blocks, gas_perm=perm)
+                                  gas_blocks=blocks, gas_perm=perm, fused=self.single_kernel)
         n = ops.sparse_mm(a, x)
         out = self.W1(n) + self.W2(x * n)
         out = self.dropout(self.activation(out))

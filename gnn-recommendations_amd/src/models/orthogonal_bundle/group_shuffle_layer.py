@@ -15,6 +15,11 @@ import torch.nn as nn
 from ... import ops
 
 
+def param_key(params) -> tuple:
+    """Identity + in-place version of a parameter list (cache key for derived matrices)."""
+    return tuple((p.data_ptr(), p._version, p.device) for p in params)
+
+
 class GroupShuffleLayer(nn.Module):
     def __init__(self, dim: int, block_size: int, init_scale: float = 0.01):
         super().__init__()
@@ -33,7 +38,19 @@ class GroupShuffleLayer(nn.Module):
 
     # ---- the orthogonal group element ------------------------------------------------------
     def blocks(self) -> torch.Tensor:
-        """[n_blocks, bs, bs] = expm(P_b - P_b^T) (group_shuffle_layer.py:110-124)."""
+        """[n_blocks, bs, bs] = expm(P_b - P_b^T) (group_shuffle_layer.py:110-124).
+        Without autograd the result is cached until a parameter changes (matrix_exp on the
+        device synchronises with the host, so recomputing it every forward costs more than
+        the propagation kernels)."""
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.skew_params):
+            return self._compute_blocks()
+        key = param_key(self.skew_params)
+        if getattr(self, "_blocks_key", None) != key:
+            self._blocks_cache = self._compute_blocks().detach()
+            self._blocks_key = key
+        return self._blocks_cache
+
+    def _compute_blocks(self) -> torch.Tensor:
         out = []
         for p in self.skew_params:
             a = p - p.T

@@ -21,7 +21,7 @@ from ..base import BaseRecommender
 from ... import ops
 from ...ops.graph import CsrGraph
 from .bundle_layer import BundleConnectionLayer
-from .group_shuffle_layer import GroupShuffleLayer
+from .group_shuffle_layer import GroupShuffleLayer, param_key
 from .parallel_transport import parallel_transport_along_edges
 
 
@@ -54,7 +54,20 @@ class OrthogonalBundleGNN(BaseRecommender):
 
     # ---- helpers ----------------------------------------------------------------------------
     def composed_transform(self, layer_idx: int) -> torch.Tensor:
-        """M_l = W_conn_l @ W_gs_l[:, perm_l]  (or W_gs_l[:, perm_l] without transport)."""
+        """M_l = W_conn_l @ W_gs_l[:, perm_l]  (or W_gs_l[:, perm_l] without transport);
+        cached between calls while no parameter changes (inference)."""
+        gs = self.local_transform_layers[layer_idx]
+        params = list(gs.skew_params) + (list(self.connection_layers[layer_idx].skew_params)
+                                         if self.use_parallel_transport else [])
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            return self._compose(layer_idx)
+        key = param_key(params)
+        cache = self.__dict__.setdefault("_composed_cache", {})
+        if cache.get(layer_idx, (None,))[0] != key:
+            cache[layer_idx] = (key, self._compose(layer_idx).detach())
+        return cache[layer_idx][1]
+
+    def _compose(self, layer_idx: int) -> torch.Tensor:
         gs = self.local_transform_layers[layer_idx]
         W_gs = gs._build_orthogonal_matrix()[:, gs.perm]
         if self.use_parallel_transport:

@@ -41,11 +41,13 @@ _SIGNATURES = {
     "gnnrec_gas_f32": [_p, _i64, _i64, _i32, _i32, _p, _p, _p, _i64, _p],
     "gnnrec_spmm_gas_f32": [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i32, _i32, _p, _p, _p],
     "gnnrec_spmm_ngcf_f32": [_p, _p, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _i32, _p, _p, _p,
-                             _p, _f32, _p, _p, _i32, _p],
+                             _p, _f32, _p, _p, _i32, _p, _p],
     "gnnrec_spmm_dense_f32": [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i32, _p, _f32, _p, _i64,
-                              _f32, _p, _i64, _i32, _f32, _f32, _p],
+                              _f32, _p, _i64, _i32, _f32, _f32, _p, _p],
     "gnnrec_gat_aggregate_f32": [_p, _p, _i64, _p, _i64, _p, _p, _i32, _i32, _f32, _i32, _i32,
-                                 _p, _i64, _i32, _p, _i64, _p, _i64, _f32, _p],
+                                 _p, _i64, _i32, _p, _i64, _p, _i64, _f32, _i64, _p],
+    "gnnrec_gat_heavy_f32": [_p, _p, _p, _p, _i64, _p, _p, _i64, _p, _p, _i64, _p, _p, _i32,
+                             _i32, _f32, _i32, _i32, _p, _i64, _i32, _p, _i64, _p, _i64, _f32, _p],
     "gnnrec_score_topk_f32": [_p, _i64, _i64, _p, _i64, _i64, _i32, _p, _p, _i32, _p, _p, _p],
     "gnnrec_build_bipartite_csr": [_p, _p, _i64, _i64, _i64, _i32, _p, _p, _p, _p, _p, _i32],
     "gnnrec_normalize_values": [_p, _p, _p, _i64, _p, _i32, _p, _i32],

@@ -9,7 +9,13 @@ at q*rows_pad + (r - b_q). Every rank holds the full replicated input table in t
 ([world*rows_pad, d]) and produces only its own rows.
 
 Per hop:  Y_p = A[R_p, :] X            (local HIP SpMM, fused layer-mean epilogue)
-          X' = all_gather(Y_p)         (RCCL all_gather_into_tensor, equal-size pieces)
+          X' = exchange(Y_p)           (RCCL, equal-size pieces of rows_pad rows)
+The exchange sends a rank's piece only to the ranks whose shard references it. For a
+general graph every pair is needed and it is one all_gather_into_tensor. For the bipartite
+user-item graph a user shard references only item rows and vice versa, so the pieces go as
+direct point-to-point transfers (batched isend/irecv: one xGMI link per peer, all links in
+parallel) and each rank receives only the opposite side: (P/2)/(P-1) of the all-gather
+bytes (4/7 at 8 GPUs).
 The last hop needs no gather: the layer mean stays row-sharded (scoring can be sharded by
 user range); `gather_output=True` returns the full table.
 
@@ -40,7 +46,7 @@ class DistributedGraph:
     """This rank's shard of the operand plus the padded layout helpers."""
 
     def __init__(self, full: CsrGraph, rank: int, world: int, device,
-                 balance: str = "nnz", group=None):
+                 balance: str = "nnz", group=None, exchange: str = "auto"):
         self.rank, self.world, self.group = rank, world, group
         self.device = torch.device(device)
         self.shard = full.shard(rank, world, balance).to(self.device)
@@ -50,6 +56,32 @@ class DistributedGraph:
         self.row_begin, self.row_end = info.row_begin, info.row_end
         self.n_local = self.row_end - self.row_begin
         self.n_global = full.shape[0]
+        self.needs = self._needs_matrix()
+        if exchange == "auto":
+            exchange = "allgather" if bool(self.needs.all()) else "p2p"
+        if exchange not in ("allgather", "p2p"):
+            raise ValueError(f"unknown exchange: {exchange}")
+        self.exchange_mode = exchange
+
+    def _needs_matrix(self) -> torch.Tensor:
+        """needs[p, q]: rank p's shard references rows owned by rank q (all ranks agree)."""
+        mine = torch.zeros(self.world, dtype=torch.int32)
+        if self.shard.nnz:
+            owners = torch.unique(self.shard.col.to(torch.int64) // self.rows_pad).cpu()
+            mine[owners] = 1
+        if self.world == 1:
+            return mine.view(1, 1).bool()
+        backend = dist.get_backend(self.group)
+        t = mine.to(self.device) if backend != "gloo" else mine
+        allm = torch.empty((self.world, self.world), dtype=torch.int32, device=t.device)
+        dist.all_gather_into_tensor(allm.view(-1), t, group=self.group)
+        return allm.cpu().bool()
+
+    def recv_rows(self) -> int:
+        if self.exchange_mode == "allgather":
+            return (self.world - 1) * self.rows_pad
+        return int(sum(self.rows_pad for q in range(self.world)
+                       if q != self.rank and self.needs[self.rank, q]))
 
     # ---- layout ----------------------------------------------------------------------------
     def padded_index(self) -> np.ndarray:
@@ -76,6 +108,70 @@ class DistributedGraph:
         return xp[o:o + self.n_local]
 
     # ---- communication ---------------------------------------------------------------------
+    def exchange(self, out: torch.Tensor, piece: torch.Tensor) -> None:
+        """Deliver every rank's piece to the ranks that reference it (see module doc)."""
+        if self.world == 1 or self.exchange_mode == "allgather":
+            return self.all_gather(out, piece)
+        rp, me = self.rows_pad, self.rank
+        staged = out.is_cuda and dist.get_backend(self.group) == "gloo"  # 1-GPU test harness
+        src = piece.cpu() if staged else piece
+        ops, landing = [], []
+        for q in range(self.world):
+            if q == me:
+                continue
+            if self.needs[q, me]:
+                ops.append(dist.P2POp(dist.isend, src, q, self.group))
+            if self.needs[me, q]:
+                dst = out[q * rp:(q + 1) * rp]
+                buf = torch.empty(dst.shape, dtype=dst.dtype) if staged else dst
+                ops.append(dist.P2POp(dist.irecv, buf, q, self.group))
+                landing.append((dst, buf))
+        if self.needs[me, me]:
+            out[me * rp:(me + 1) * rp].copy_(piece)
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        if staged:
+            for dst, buf in landing:
+                dst.copy_(buf)
+
+    def chunk_bounds(self, chunks: int):
+        """Row boundaries of the overlap chunks inside a rows_pad piece (multiples of 4)."""
+        step = -(-self.rows_pad // chunks)
+        step = -(-step // 4) * 4
+        b = list(range(0, self.rows_pad, step)) + [self.rows_pad]
+        return list(zip(b[:-1], b[1:]))
+
+    def post_chunk(self, out: torch.Tensor, piece: torch.Tensor, c0: int, c1: int) -> list:
+        """Start the point-to-point exchange of rows [c0, c1) of every piece (async)."""
+        rp, me = self.rows_pad, self.rank
+        staged = out.is_cuda and dist.get_backend(self.group) == "gloo"
+        src = piece[c0:c1].cpu() if staged else piece[c0:c1]
+        ops, landing = [], []
+        for q in range(self.world):
+            if q == me:
+                continue
+            if self.needs[q, me]:
+                ops.append(dist.P2POp(dist.isend, src, q, self.group))
+            if self.needs[me, q]:
+                dst = out[q * rp + c0:q * rp + c1]
+                buf = torch.empty(dst.shape, dtype=dst.dtype) if staged else dst
+                ops.append(dist.P2POp(dist.irecv, buf, q, self.group))
+                if staged:
+                    landing.append((dst, buf))
+        if self.needs[me, me]:
+            out[me * rp + c0:me * rp + c1].copy_(piece[c0:c1])
+        reqs = dist.batch_isend_irecv(ops) if ops else []
+        return [(reqs, landing)]
+
+    @staticmethod
+    def finish(pending: list) -> None:
+        for reqs, landing in pending:
+            for r in reqs:
+                r.wait()
+            for dst, buf in landing:
+                dst.copy_(buf)
+
     def all_gather(self, out: torch.Tensor, piece: torch.Tensor) -> None:
         if self.world == 1:
             out.copy_(piece)
@@ -90,13 +186,16 @@ class DistributedGraph:
 
 def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers: int, *,
                             gather_output: bool = False, hop_fn: Optional[HopFn] = None,
-                            work: Optional[tuple] = None) -> torch.Tensor:
+                            work: Optional[tuple] = None, overlap_chunks: int = 1) -> torch.Tensor:
     """LightGCN propagation over a row-sharded operand.
 
     x0_pad: [world*rows_pad, d] padded initial table (identical on every rank).
     Returns this rank's rows of mean(x0..xK) ([n_local, d]), or the full [N, d] table when
     gather_output. `work` (from `make_work`) holds reusable hop buffers. With world == 1
     the hop outputs feed the next hop directly (no gather, no copy).
+    overlap_chunks > 1 (point-to-point exchange only): the hop runs in that many row chunks
+    and each chunk's transfer is posted as soon as its kernel is queued, so the exchange of
+    chunk c overlaps the SpMM of chunk c+1.
     """
     hop = hop_fn or _native_hop
     d = x0_pad.shape[1]
@@ -108,6 +207,7 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
     if n_layers == 0:
         acc.copy_(self_rows)
     x_in = x0_pad
+    chunked = overlap_chunks > 1 and dg.world > 1 and dg.exchange_mode == "p2p"
     for k in range(1, n_layers + 1):
         last = k == n_layers
         epi = EPI_ACC_INIT if k == 1 else EPI_ACC_ADD
@@ -119,12 +219,24 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
                 acc=acc, acc_div=float(n_layers + 1))
             x_in = y
             continue
-        hop(dg.shard, x_in, None if last else Y[:dg.n_local], epi=epi, self_rows=self_rows,
-            acc=acc, acc_div=float(n_layers + 1))
-        if not last:
-            x_next = Xa if x_in is not Xa else Xb
-            dg.all_gather(x_next, Y)
-            x_in = x_next
+        if last or not chunked:
+            hop(dg.shard, x_in, None if last else Y[:dg.n_local], epi=epi, self_rows=self_rows,
+                acc=acc, acc_div=float(n_layers + 1))
+            if not last:
+                x_next = Xa if x_in is not Xa else Xb
+                dg.exchange(x_next, Y)
+                x_in = x_next
+            continue
+        x_next = Xa if x_in is not Xa else Xb
+        pending = []
+        for c0, c1 in dg.chunk_bounds(overlap_chunks):
+            r1 = min(c1, dg.n_local)
+            if r1 > c0:
+                hop(dg.shard.row_slice(c0, r1), x_in, Y[c0:r1], epi=epi,
+                    self_rows=self_rows[c0:r1], acc=acc[c0:r1], acc_div=float(n_layers + 1))
+            pending += dg.post_chunk(x_next, Y, c0, c1)
+        dg.finish(pending)
+        x_in = x_next
     if not gather_output:
         return acc
     if dg.world == 1:

@@ -165,8 +165,10 @@ def ngcf_layer(adj: CsrGraph, x: torch.Tensor, W1: torch.Tensor, b1: torch.Tenso
                W2: torch.Tensor, b2: torch.Tensor, slope: float = 0.2,
                x_self: Optional[torch.Tensor] = None,
                gas_blocks: Optional[torch.Tensor] = None,
-               gas_perm: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """NGCFLayer.forward in eval mode (ngcf.py:69-84), optionally followed by GAS."""
+               gas_perm: Optional[torch.Tensor] = None, fused: bool = False) -> torch.Tensor:
+    """NGCFLayer.forward in eval mode (ngcf.py:69-84), optionally followed by GAS.
+    fused=False (default): hop into a scratch table + streaming MFMA transform (faster on
+    gather-bound graphs); fused=True: one kernel."""
     x = _rowmajor(x)
     if x_self is None:
         x_self = x
@@ -186,17 +188,20 @@ def ngcf_layer(adj: CsrGraph, x: torch.Tensor, W1: torch.Tensor, b1: torch.Tenso
         gb = gas_blocks.detach().to(dev, torch.float32).contiguous()
         gp = gas_perm.to(dev, torch.int32).contiguous()
         bs = gb.shape[1]
+    work = None if fused else torch.empty((adj.n_rows, d), dtype=torch.float32, device=x.device)
     check(_lib.lib().gnnrec_spmm_ngcf_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(x_self),
                                           x_self.stride(0), ptr(y), d, d, ptr(w1), ptr(bb1),
                                           ptr(w2), ptr(bb2), float(slope), ptr(gb), ptr(gp), bs,
-                                          _lib.stream_of(adj.device)), "gnnrec_spmm_ngcf_f32")
+                                          ptr(work), _lib.stream_of(adj.device)),
+          "gnnrec_spmm_ngcf_f32")
     return y
 
 
 def dense_layer(adj: CsrGraph, x: torch.Tensor, M: torch.Tensor, c_out: float,
                 resid: Optional[torch.Tensor], c_res: float, *, y: Optional[torch.Tensor] = None,
                 acc: Optional[torch.Tensor] = None, acc_mode: int = 0, w_out: float = 0.0,
-                w_res: float = 0.0, store_y: bool = True) -> Optional[torch.Tensor]:
+                w_res: float = 0.0, store_y: bool = True,
+                fused: bool = False) -> Optional[torch.Tensor]:
     """c_out * ((A x) @ M) + c_res * resid, with the optional fused layer sum into `acc`."""
     x = _rowmajor(x)
     resid = _rowmajor(resid) if resid is not None else None
@@ -212,16 +217,25 @@ def dense_layer(adj: CsrGraph, x: torch.Tensor, M: torch.Tensor, c_out: float,
                                            float(c_res), ptr(acc),
                                            acc.stride(0) if acc is not None else d,
                                            int(acc_mode), float(w_out), float(w_res),
+                                           ptr(None if fused else torch.empty(
+                                               (adj.n_rows, d), dtype=torch.float32,
+                                               device=x.device)),
                                            _lib.stream_of(adj.device)), "gnnrec_spmm_dense_f32")
     return y if store_y else None
+
+
+GAT_HEAVY_THRESHOLD = 2048   # rows with more neighbours go to the split (segment) path
+GAT_SEGMENT = 1024
 
 
 def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh: torch.Tensor,
                   heads: int, o_dim: int, slope: float = 0.2, mean_heads: bool = False,
                   apply_elu: bool = False, *, out: Optional[torch.Tensor] = None, epi: int = 0,
                   self_rows: Optional[torch.Tensor] = None, acc: Optional[torch.Tensor] = None,
-                  acc_div: float = 1.0) -> Optional[torch.Tensor]:
-    """Sparse edge-softmax aggregation of one GAT layer, all heads (gnnrec_gat_aggregate_f32)."""
+                  acc_div: float = 1.0,
+                  heavy_threshold: int = GAT_HEAVY_THRESHOLD) -> Optional[torch.Tensor]:
+    """Sparse edge-softmax aggregation of one GAT layer, all heads (gnnrec_gat_aggregate_f32),
+    with rows longer than `heavy_threshold` split into segments (gnnrec_gat_heavy_f32)."""
     h = _rowmajor(h)
     s_self = s_self.contiguous()
     s_neigh = s_neigh.contiguous()
@@ -229,13 +243,25 @@ def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh:
     width = o_dim if mean_heads else heads * o_dim
     if out is None and not (epi & EPI_NO_Y):
         out = torch.empty((adj.n_rows, width), dtype=torch.float32, device=h.device)
-    check(_lib.lib().gnnrec_gat_aggregate_f32(
-        ptr(adj.row_ptr), ptr(adj.col), adj.n_rows, ptr(h), h.stride(0), ptr(s_self),
-        ptr(s_neigh), int(heads), int(o_dim), float(slope), int(mean_heads), int(apply_elu),
-        ptr(out), out.stride(0) if out is not None else width, int(epi), ptr(self_rows),
-        self_rows.stride(0) if self_rows is not None else width, ptr(acc),
-        acc.stride(0) if acc is not None else width, float(acc_div), _lib.stream_of(adj.device)),
-        "gnnrec_gat_aggregate_f32")
+    plan = adj.heavy_plan(heavy_threshold, GAT_SEGMENT) if heavy_threshold > 0 else None
+    common = (ptr(h), h.stride(0), ptr(s_self), ptr(s_neigh), int(heads), int(o_dim),
+              float(slope), int(mean_heads), int(apply_elu), ptr(out),
+              out.stride(0) if out is not None else width, int(epi), ptr(self_rows),
+              self_rows.stride(0) if self_rows is not None else width, ptr(acc),
+              acc.stride(0) if acc is not None else width, float(acc_div))
+    L = _lib.lib()
+    stream = _lib.stream_of(adj.device)
+    check(L.gnnrec_gat_aggregate_f32(ptr(adj.row_ptr), ptr(adj.col), adj.n_rows, *common,
+                                     int(heavy_threshold if plan is not None else 0), stream),
+          "gnnrec_gat_aggregate_f32")
+    if plan is not None:
+        n_seg = plan["seg_row"].numel()
+        work = torch.empty(n_seg * (heads * o_dim + 2 * heads) + 4, dtype=torch.float32,
+                           device=h.device)
+        check(L.gnnrec_gat_heavy_f32(ptr(adj.col), ptr(plan["seg_row"]), ptr(plan["seg_beg"]),
+                                     ptr(plan["seg_end"]), n_seg, ptr(plan["heavy_rows"]),
+                                     ptr(plan["heavy_seg_ptr"]), plan["heavy_rows"].numel(),
+                                     ptr(work), *common, stream), "gnnrec_gat_heavy_f32")
     return out
 
 
@@ -252,6 +278,13 @@ def score_topk(user_emb: torch.Tensor, item_emb: torch.Tensor, k: int,
     if u.dtype != torch.float32 or v.dtype != torch.float32:
         raise TypeError("score_topk needs float32 tables")
     B, d = u.shape
+    dp = next((w for w in (16, 32, 64, 128, 256) if w >= d), None)
+    if dp is None:
+        raise NotImplementedError(f"score_topk: d={d} > 256")
+    if dp != d:  # zero columns leave every fmaf chain unchanged
+        u = torch.nn.functional.pad(u, (0, dp - d))
+        v = torch.nn.functional.pad(v, (0, dp - d))
+        d = dp
     idx = torch.empty((B, k), dtype=torch.int64, device=u.device)
     sc = torch.empty((B, k), dtype=torch.float32, device=u.device)
     if seen_ptr is not None:

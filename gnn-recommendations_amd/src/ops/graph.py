@@ -65,6 +65,7 @@ class CsrGraph:
     symmetric: bool = False
     shard_info: Optional[ShardInfo] = None
     _transpose: Optional["CsrGraph"] = field(default=None, repr=False)
+    _plans: dict = field(default_factory=dict, repr=False)
 
     # ---- reference-adjacency look-alike -------------------------------------------
     is_sparse = True
@@ -273,6 +274,36 @@ class CsrGraph:
                      self.n_users, self.n_items, False,
                      ShardInfo(rank, world, lo, hi, rows_pad, bounds))
         return g.to(self.device)
+
+    def row_slice(self, r0: int, r1: int) -> "CsrGraph":
+        """View of rows [r0, r1) (row_ptr keeps absolute offsets: no copy of col/val)."""
+        return CsrGraph(self.row_ptr[r0:r1 + 1], self.col, self.val, (r1 - r0, self.shape[1]),
+                        self.n_users, self.n_items, False, self.shard_info)
+
+    def heavy_plan(self, threshold: int, seg_len: int):
+        """Degree buckets for the skew-tolerant kernels (cached): rows with more than
+        `threshold` neighbours, cut into `seg_len` segments. Returns None when there are none,
+        else dict(heavy_rows, heavy_seg_ptr, seg_row, seg_beg, seg_end) on this device."""
+        key = ("heavy", threshold, seg_len)
+        if key not in self._plans:
+            rp = self.row_ptr
+            deg = rp[1:] - rp[:-1]
+            heavy = torch.nonzero(deg > threshold).flatten()
+            if heavy.numel() == 0:
+                self._plans[key] = None
+            else:
+                nseg = (deg[heavy] + seg_len - 1) // seg_len
+                seg_ptr = torch.zeros(heavy.numel() + 1, dtype=torch.int64, device=rp.device)
+                seg_ptr[1:] = torch.cumsum(nseg, 0)
+                seg_row = torch.repeat_interleave(heavy, nseg)
+                j = torch.arange(int(seg_ptr[-1]), device=rp.device) - torch.repeat_interleave(
+                    seg_ptr[:-1], nseg)
+                seg_beg = rp[seg_row] + j * seg_len
+                seg_end = torch.minimum(seg_beg + seg_len, rp[seg_row + 1])
+                self._plans[key] = dict(heavy_rows=heavy.contiguous(), heavy_seg_ptr=seg_ptr,
+                                        seg_row=seg_row.contiguous(), seg_beg=seg_beg.contiguous(),
+                                        seg_end=seg_end.contiguous())
+        return self._plans[key]
 
     def __repr__(self) -> str:  # keep it short: the tensors are huge
         return (f"CsrGraph(shape={self.shape}, nnz={self.nnz}, device={self.device}, "

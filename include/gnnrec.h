@@ -105,13 +105,16 @@ int gnnrec_spmm_gas_f32(const int64_t* row_ptr, const int32_t* col, const float*
  * x_self: the input-table rows of the destination rows ([n_rows, ld_self]).
  * If gas_blocks != NULL, GAS(gas_blocks, gas_perm, gas_bs) is applied to `out` before the
  * store (BASELINE config 3: x_{l+1} = GS_l(NGCFLayer_l(x_l))).
+ * work: NULL = one fused kernel; else an [n_rows, d] scratch table (16-B aligned): the hop
+ * runs as gnnrec_spmm_csr_f32 into it and a streaming MFMA kernel applies the rest (faster
+ * on gather-bound graphs: the hop keeps its occupancy). Same results either way.
  * d must be 32, 64 or 128 (MFMA f32 16x16x4 tiles). */
 int gnnrec_spmm_ngcf_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
                          int64_t n_rows, const float* x, int64_t ldx, const float* x_self,
                          int64_t ld_self, float* y, int64_t ldy, int32_t d, const float* W1,
                          const float* b1, const float* W2, const float* b2, float slope,
                          const float* gas_blocks, const int32_t* gas_perm, int32_t gas_bs,
-                         gnnrec_stream_t stream);
+                         float* work, gnnrec_stream_t stream);
 
 /* ---- a9: OrthogonalBundle layer (SpMM + composed 64x64 transform + residual) ---------
  * Replaces orthogonal_bundle/model.py:171-195 (adjacency path) plus the softmax-weighted
@@ -122,12 +125,14 @@ int gnnrec_spmm_ngcf_f32(const int64_t* row_ptr, const int32_t* col, const float
  * acc_mode 0: no layer sum; 1: acc = fl(w_res*resid) + fl(w_out*out) (layer 0 + layer 1);
  * 2: acc = acc + fl(w_out*out). `y` may be NULL when only acc is wanted; `resid` may be
  * NULL (no residual term, out = c_out * ((A x) @ M)) unless acc_mode is 1.
+ * work: as gnnrec_spmm_ngcf_f32 (NULL = fused, else [n_rows, d] scratch for the split form).
  * d must be 32, 64 or 128. */
 int gnnrec_spmm_dense_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
                           int64_t n_rows, const float* x, int64_t ldx, float* y, int64_t ldy,
                           int32_t d, const float* M, float c_out, const float* resid,
                           int64_t ld_resid, float c_res, float* acc, int64_t ld_acc,
-                          int32_t acc_mode, float w_out, float w_res, gnnrec_stream_t stream);
+                          int32_t acc_mode, float w_out, float w_res, float* work,
+                          gnnrec_stream_t stream);
 
 /* ---- a11: GAT sparse edge-softmax aggregation ---------------------------------------
  * Replaces the dense masked softmax + mm of GATLayer.forward (baselines/gat.py:99-149)
@@ -141,20 +146,37 @@ int gnnrec_spmm_dense_f32(const int64_t* row_ptr, const int32_t* col, const floa
  * o[r,h,:] ([n_rows, o_dim]). apply_elu: out = ELU(out) (alpha 1). epi: the ACC_* flags of
  * gnnrec_spmm_csr_f32 applied to the (ELU'd) output with `self` = the layer input rows.
  * An empty row yields NaN (softmax over an empty set, as the reference's all -inf row).
- * heads*o_dim must be 16, 32, 64, 128 or 256 (o_dim a multiple of 4). */
+ * heads*o_dim must be 16, 32, 64, 128 or 256 (o_dim a multiple of 4).
+ * max_row_len > 0: rows with more neighbours are skipped here and must be finished by
+ * gnnrec_gat_heavy_f32 (power-law degree buckets; 0 = every row here). */
 int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* col, int64_t n_rows,
                              const float* hfeat, int64_t ldh, const float* s_self,
                              const float* s_neigh, int32_t heads, int32_t o_dim, float slope,
                              int32_t mean_heads, int32_t apply_elu, float* out, int64_t ldo,
                              int32_t epi, const float* self, int64_t ld_self, float* acc,
-                             int64_t ld_acc, float acc_div, gnnrec_stream_t stream);
+                             int64_t ld_acc, float acc_div, int64_t max_row_len,
+                             gnnrec_stream_t stream);
+
+/* Heavy-row bucket of the GAT aggregation: every heavy row is cut into segments (seg_row /
+ * seg_beg / seg_end: its row id and CSR range, n_seg in all; heavy_seg_ptr[n_heavy+1] the
+ * segments of heavy_rows[h]); one row group per segment computes a partial (sum, max, total)
+ * and a merge pass rescales and combines them, then applies the same epilogue as
+ * gnnrec_gat_aggregate_f32. work: n_seg * (heads*o_dim + 2*heads) floats, 16-B aligned. */
+int gnnrec_gat_heavy_f32(const int32_t* col, const int64_t* seg_row, const int64_t* seg_beg,
+                         const int64_t* seg_end, int64_t n_seg, const int64_t* heavy_rows,
+                         const int64_t* heavy_seg_ptr, int64_t n_heavy, float* work,
+                         const float* hfeat, int64_t ldh, const float* s_self,
+                         const float* s_neigh, int32_t heads, int32_t o_dim, float slope,
+                         int32_t mean_heads, int32_t apply_elu, float* out, int64_t ldo,
+                         int32_t epi, const float* self, int64_t ld_self, float* acc,
+                         int64_t ld_acc, float acc_div, gnnrec_stream_t stream);
 
 /* ---- a13: scoring + seen-item mask + top-K ------------------------------------------
  * Replaces evaluator.py:96-105 / trainer.py:327-336 for one batch of users:
  *   score[b, i] = sum_{f<d} u[b, f] * v[i, f]   (sequential fmaf over f, from +0.0f)
  *   score[b, i] = -inf for items i in the seen list of user b (CSR seen_ptr/seen_col)
  *   top-k by (score desc, item index asc) -> out_idx[b, :k] (int64), out_score[b, :k].
- * k <= 128. */
+ * k <= 128; d in {16, 32, 64, 128, 256} (callers zero-pad other widths: exact). */
 int gnnrec_score_topk_f32(const float* u, int64_t ldu, int64_t n_users_batch,
                           const float* v, int64_t ldv, int64_t n_items, int32_t d,
                           const int64_t* seen_ptr, const int32_t* seen_col, int32_t k,

@@ -40,7 +40,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, K, balance, q):
+def _worker(rank, world, port, K, balance, q, exchange="auto", chunks=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -49,27 +49,35 @@ def _worker(rank, world, port, K, balance, q):
                         (rp.size - 1, rp.size - 1), nu, ni, True)
         torch.manual_seed(5)
         x0 = torch.randn(full.shape[0], 32) * 0.1
-        dg = DistributedGraph(full, rank, world, "cpu", balance=balance)
+        dg = DistributedGraph(full, rank, world, "cpu", balance=balance, exchange=exchange)
         xp = dg.pad_table(x0)
-        local = lightgcn_propagate_dist(dg, xp, K, hop_fn=cpu_hop)
-        whole = lightgcn_propagate_dist(dg, xp, K, hop_fn=cpu_hop, gather_output=True)
+        local = lightgcn_propagate_dist(dg, xp, K, hop_fn=cpu_hop, overlap_chunks=chunks)
+        whole = lightgcn_propagate_dist(dg, xp, K, hop_fn=cpu_hop, gather_output=True,
+                                        overlap_chunks=chunks)
         if rank == 0:
             ref = oracle.lightgcn(rp, col, val, x0.numpy(), K)
-            q.put((whole.numpy(), ref, local.numpy(), ref[dg.row_begin:dg.row_end]))
+            q.put((whole.numpy(), ref, local.numpy(), ref[dg.row_begin:dg.row_end],
+                   dg.exchange_mode, dg.needs.numpy()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,K,balance", [(2, 3, "nnz"), (3, 2, "rows"), (2, 1, "nnz")])
-def test_sharded_propagation_matches_single_device(world, K, balance):
+@pytest.mark.parametrize("world,K,balance,exchange,chunks", [
+    (2, 3, "nnz", "auto", 1), (3, 2, "rows", "auto", 1), (2, 1, "nnz", "allgather", 1),
+    (4, 3, "nnz", "auto", 1), (4, 2, "nnz", "allgather", 1), (4, 3, "nnz", "p2p", 3),
+    (3, 3, "rows", "p2p", 4)])
+def test_sharded_propagation_matches_single_device(world, K, balance, exchange, chunks):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, K, balance, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, K, balance, q, exchange, chunks))
              for r in range(world)]
     for p in procs:
         p.start()
-    whole, ref, local, ref_local = q.get(timeout=120)
+    whole, ref, local, ref_local, mode, needs = q.get(timeout=120)
+    if exchange == "auto" and world == 4:
+        # bipartite graph, nnz-balanced: users on ranks 0-1, items on 2-3 -> point-to-point
+        assert mode == "p2p" and not needs.all()
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -154,14 +154,15 @@ def test_spmm_gas_fused(cuda):
     np.testing.assert_array_equal(bits(y), bits(ref))
 
 
-def test_ngcf_layers_vs_reference(cuda):
+@pytest.mark.parametrize("fused", [False, True])
+def test_ngcf_layers_vs_reference(cuda, fused):
     f = load_golden("ngcf_d64")
     g, _ = graph_from_golden("g_small", cuda)
     x = torch.from_numpy(np.concatenate([f["user_w"], f["item_w"]])).to(cuda)
     outs = [x]
     for li in range(3):
         t = lambda k: torch.from_numpy(f[f"{k}_{li}"]).to(cuda)  # noqa: E731
-        x = F.ngcf_layer(g, x, t("W1"), t("b1"), t("W2"), t("b2"), 0.2)
+        x = F.ngcf_layer(g, x, t("W1"), t("b1"), t("W2"), t("b2"), 0.2, fused=fused)
         outs.append(x)
     cat = torch.cat(outs, 1).cpu().numpy()
     nu = f["user_out"].shape[0]
@@ -169,8 +170,9 @@ def test_ngcf_layers_vs_reference(cuda):
     np.testing.assert_allclose(cat[nu:], f["item_out"], rtol=0, atol=1e-5)
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("d", [32, 64, 128])
-def test_ngcf_gas_vs_oracle(cuda, d):
+def test_ngcf_gas_vs_oracle(cuda, d, fused):
     g, (rp, col, val) = random_graph(700, 900, 9000, d, cuda)
     rng = np.random.default_rng(d)
     x = rng.standard_normal((g.shape[0], d)).astype(np.float32) * 0.1
@@ -181,13 +183,14 @@ def test_ngcf_gas_vs_oracle(cuda, d):
     perm = rng.permutation(d).astype(np.int32)
     T = lambda a: torch.from_numpy(a).to(cuda)  # noqa: E731
     y = F.ngcf_layer(g, T(x), T(W1), T(b1), T(W2), T(b2), 0.2, gas_blocks=T(blocks),
-                     gas_perm=T(perm)).cpu().numpy()
+                     gas_perm=T(perm), fused=fused).cpu().numpy()
     ref = oracle.gas(oracle.ngcf_layer(rp, col, val, x, W1, b1, W2, b2, 0.2), blocks, perm)
     np.testing.assert_allclose(y, ref, rtol=0, atol=1e-5)
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("d", [32, 64, 128])
-def test_dense_layer_vs_oracle(cuda, d):
+def test_dense_layer_vs_oracle(cuda, d, fused):
     g, (rp, col, val) = random_graph(500, 800, 7000, 3 * d, cuda)
     rng = np.random.default_rng(d + 1)
     x = rng.standard_normal((g.shape[0], d)).astype(np.float32) * 0.1
@@ -195,13 +198,15 @@ def test_dense_layer_vs_oracle(cuda, d):
     M = (rng.standard_normal((d, d)) / np.sqrt(d)).astype(np.float32)
     T = lambda a: torch.from_numpy(a).to(cuda)  # noqa: E731
     acc = torch.empty(g.shape[0], d, device=cuda)
-    y = F.dense_layer(g, T(x), T(M), 0.9, T(xi), 0.1, acc=acc, acc_mode=1, w_out=0.3, w_res=0.7)
+    y = F.dense_layer(g, T(x), T(M), 0.9, T(xi), 0.1, acc=acc, acc_mode=1, w_out=0.3, w_res=0.7,
+                      fused=fused)
     n = oracle.spmm(rp, col, val, x).astype(np.float64)
     ref = (np.float32(0.9) * (n @ M) + np.float32(0.1) * xi).astype(np.float32)
     np.testing.assert_allclose(y.cpu().numpy(), ref, rtol=0, atol=1e-5)
     np.testing.assert_allclose(acc.cpu().numpy(), np.float32(0.7) * xi + np.float32(0.3) * ref,
                                rtol=0, atol=1e-5)
     acc_before = acc.clone()
-    F.dense_layer(g, T(x), T(M), 0.9, T(xi), 0.1, acc=acc, acc_mode=2, w_out=0.5, store_y=False)
+    F.dense_layer(g, T(x), T(M), 0.9, T(xi), 0.1, acc=acc, acc_mode=2, w_out=0.5, store_y=False,
+                  fused=fused)
     np.testing.assert_allclose(acc.cpu().numpy(), (acc_before + 0.5 * y).cpu().numpy(), rtol=0,
                                atol=1e-6)

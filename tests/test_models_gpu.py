@@ -152,3 +152,33 @@ def test_gat_isolated_node_row_is_nan_only_locally(cuda):
         u, i = m(g)
     assert torch.isnan(u[3]).all()
     assert torch.isfinite(u[:3]).all() and torch.isfinite(i).all()
+
+
+@pytest.mark.parametrize("threshold", [0, 5, 40])
+def test_gat_heavy_row_split_matches_unsplit(cuda, threshold):
+    """Power-law rows: the segment/merge path equals the one-pass path (fp32 tolerance)."""
+    from src.ops import functional as F
+    rng = np.random.default_rng(3)
+    nu, ni = 50, 400
+    u = np.concatenate([rng.integers(0, nu, 3000), np.zeros(390, np.int64), np.arange(nu)])
+    i = np.concatenate([rng.integers(0, ni, 3000), np.arange(390), rng.integers(0, ni, nu)])
+    g = CsrGraph.from_interactions(u, i, nu, ni).to(cuda)
+    N = g.shape[0]
+    for heads, o, mean in [(4, 16, False), (4, 64, True), (2, 8, False)]:
+        h = torch.randn(N, heads * o, device=cuda)
+        ss, sn = torch.randn(N, heads, device=cuda), torch.randn(N, heads, device=cuda)
+        ref = F.gat_aggregate(g, h, ss, sn, heads, o, 0.2, mean, True, heavy_threshold=0)
+        got = F.gat_aggregate(g, h, ss, sn, heads, o, 0.2, mean, True,
+                              heavy_threshold=threshold or 10 ** 9)
+        if threshold:
+            assert g.heavy_plan(threshold, F.GAT_SEGMENT) is not None
+        torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+    # and with a segment length smaller than the rows
+    old = F.GAT_SEGMENT
+    try:
+        F.GAT_SEGMENT = 7
+        got = F.gat_aggregate(g, h, ss, sn, heads, o, 0.2, False, False, heavy_threshold=20)
+        ref = F.gat_aggregate(g, h, ss, sn, heads, o, 0.2, False, False, heavy_threshold=0)
+        torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+    finally:
+        F.GAT_SEGMENT = old

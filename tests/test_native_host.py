@@ -96,3 +96,22 @@ def test_partition_covers_rows_and_remaps_columns(world):
         glob = b[owner] + off
         k0 = G.row_ptr[s.shard_info.row_begin].item()
         np.testing.assert_array_equal(glob, G.col.numpy()[k0:k0 + s.nnz])
+
+
+def test_heavy_row_plan_segments_cover_heavy_rows():
+    rng = np.random.default_rng(0)
+    u = np.concatenate([rng.integers(0, 30, 500), np.zeros(200, np.int64)])
+    i = np.concatenate([rng.integers(0, 300, 500), np.arange(200)])
+    G = CsrGraph.from_interactions(u, i, 30, 300)
+    plan = G.heavy_plan(50, 16)
+    rp = G.row_ptr.numpy()
+    deg = np.diff(rp)
+    np.testing.assert_array_equal(plan["heavy_rows"].numpy(), np.nonzero(deg > 50)[0])
+    sp = plan["heavy_seg_ptr"].numpy()
+    for h, r in enumerate(plan["heavy_rows"].numpy()):
+        segs = range(sp[h], sp[h + 1])
+        b = plan["seg_beg"].numpy()[list(segs)]
+        e = plan["seg_end"].numpy()[list(segs)]
+        assert b[0] == rp[r] and e[-1] == rp[r + 1] and np.all(b[1:] == e[:-1])
+        assert np.all(e - b <= 16) and np.all(plan["seg_row"].numpy()[list(segs)] == r)
+    assert G.heavy_plan(10 ** 6, 16) is None
