@@ -247,6 +247,99 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
     return dg.unpad_table(full)
 
 
+def gather_rows(dg: DistributedGraph, local: torch.Tensor) -> torch.Tensor:
+    """Collect every rank's [n_local, w] rows into the full [N, w] table (global row order)."""
+    if dg.world == 1:
+        return local
+    w = local.shape[1]
+    piece = torch.zeros((dg.rows_pad, w), dtype=local.dtype, device=local.device)
+    piece[:dg.n_local].copy_(local)
+    full = torch.empty((dg.world * dg.rows_pad, w), dtype=local.dtype, device=local.device)
+    dg.all_gather(full, piece)
+    return dg.unpad_table(full)
+
+
+def _exchanged(dg: DistributedGraph, local: torch.Tensor) -> torch.Tensor:
+    """This rank's [n_local, w] rows -> the padded gather table [world*rows_pad, w] holding
+    every row this rank's shard references (one exchange)."""
+    if dg.world == 1:
+        return local
+    piece = torch.zeros((dg.rows_pad, local.shape[1]), dtype=local.dtype, device=local.device)
+    piece[:dg.n_local].copy_(local)
+    table = torch.zeros((dg.world * dg.rows_pad, local.shape[1]), dtype=local.dtype,
+                        device=local.device)
+    dg.exchange(table, piece)
+    return table
+
+
+def _native_ngcf_layer(shard, x_in, x_self, layer, gs, out):
+    from .functional import ngcf_layer
+    blocks, perm = (gs.blocks(), gs.perm) if gs is not None else (None, None)
+    ngcf_layer(shard, x_in, layer.W1.weight, layer.W1.bias, layer.W2.weight, layer.W2.bias,
+               layer.activation.negative_slope, x_self=x_self, gas_blocks=blocks,
+               gas_perm=perm, fused=layer.single_kernel, out=out)
+
+
+def ngcf_forward_dist(dg: DistributedGraph, model, x0_pad: torch.Tensor, *,
+                      gather_output: bool = False, layer_fn: Optional[Callable] = None
+                      ) -> torch.Tensor:
+    """NGCF / NGCFGroupShuffle eval forward over a row-sharded operand (SURVEY §8e step 2:
+    the row-local epilogue runs on the shard). Per layer: the local hop + both Linear layers
+    + LeakyReLU (+ GAS) with x_self = this rank's own rows of the layer input
+    (gnnrec_spmm_ngcf_f32), then one exchange of the layer output. All parameters are
+    replicated. Returns this rank's rows of cat(x0, x1, ..., xK) (ngcf.py:186), or the
+    full table when gather_output. Bit-identical to the single-device forward (every kernel
+    computes a row from that row's inputs only)."""
+    layer_fn = layer_fn or _native_ngcf_layer
+    gs_layers = list(getattr(model, "gs_layers", [None] * len(model.layers)))
+    n = dg.n_local
+    x_local = dg.local_slice(x0_pad)
+    outs = [x_local]
+    x_in = x0_pad
+    for k, (layer, gs) in enumerate(zip(model.layers, gs_layers)):
+        y = torch.empty((n, layer.W1.out_features), dtype=torch.float32, device=x0_pad.device)
+        layer_fn(dg.shard, x_in, x_local, layer, gs, y)
+        outs.append(y)
+        x_local = y
+        if k + 1 < len(model.layers):
+            x_in = _exchanged(dg, y)
+    local = torch.cat(outs, dim=1)
+    return gather_rows(dg, local) if gather_output else local
+
+
+def _native_gat_layer(shard, h, s_self, s_neigh, layer, *, apply_elu, epi, self_rows, acc,
+                      acc_div):
+    from .functional import gat_aggregate
+    return gat_aggregate(shard, h, s_self, s_neigh, layer.n_heads, layer.out_dim, layer.alpha,
+                         mean_heads=not layer.concat_heads, apply_elu=apply_elu, epi=epi,
+                         self_rows=self_rows, acc=acc, acc_div=acc_div)
+
+
+def gat_forward_dist(dg: DistributedGraph, model, x0_pad: torch.Tensor, *,
+                     gather_output: bool = False, layer_fn: Optional[Callable] = None
+                     ) -> torch.Tensor:
+    """GAT eval forward over a row-sharded operand (SURVEY §8e "GAT: all-gather h and the
+    per-node attention scalars instead"). Per layer each rank projects only its own rows
+    (h = x W^T for all heads, s_self, s_neigh), exchanges h and s_neigh (the only per-node
+    values a neighbour reads), and runs the sparse edge-softmax aggregation over its shard
+    with ELU and the layer mean fused (gnnrec_gat_aggregate_f32 + heavy-row split). x itself
+    never moves. Returns this rank's rows of the layer mean (or the full table)."""
+    from ._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT
+    layer_fn = layer_fn or _native_gat_layer
+    x_local = dg.local_slice(x0_pad)
+    acc = torch.empty_like(x_local)
+    L = len(model.layers)
+    for k, layer in enumerate(model.layers, start=1):
+        h, ss, sn = layer.projections(x_local)
+        hp, snp = _exchanged(dg, h), _exchanged(dg, sn.contiguous())
+        epi = EPI_ACC_INIT if k == 1 else EPI_ACC_ADD
+        if k == L:
+            epi |= EPI_ACC_DIV
+        x_local = layer_fn(dg.shard, hp, ss, snp, layer, apply_elu=True, epi=epi,
+                           self_rows=x_local, acc=acc, acc_div=float(L + 1))
+    return gather_rows(dg, acc) if gather_output else acc
+
+
 def make_work(dg: DistributedGraph, d: int, device) -> tuple:
     """Hop buffers: Y [rows_pad, d] (zero padded tail) and two [world*rows_pad, d] tables."""
     rows = dg.world * dg.rows_pad

@@ -165,10 +165,12 @@ def ngcf_layer(adj: CsrGraph, x: torch.Tensor, W1: torch.Tensor, b1: torch.Tenso
                W2: torch.Tensor, b2: torch.Tensor, slope: float = 0.2,
                x_self: Optional[torch.Tensor] = None,
                gas_blocks: Optional[torch.Tensor] = None,
-               gas_perm: Optional[torch.Tensor] = None, fused: bool = False) -> torch.Tensor:
+               gas_perm: Optional[torch.Tensor] = None, fused: bool = False,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """NGCFLayer.forward in eval mode (ngcf.py:69-84), optionally followed by GAS.
     fused=False (default): hop into a scratch table + streaming MFMA transform (faster on
-    gather-bound graphs); fused=True: one kernel."""
+    gather-bound graphs); fused=True: one kernel. x_self: the destination rows' own x (the
+    rows of x by default; a rank's local rows when x is a sharded gather table)."""
     x = _rowmajor(x)
     if x_self is None:
         x_self = x
@@ -176,7 +178,13 @@ def ngcf_layer(adj: CsrGraph, x: torch.Tensor, W1: torch.Tensor, b1: torch.Tenso
     d = x.shape[1]
     if W1.shape != (d, d) or W2.shape != (d, d):
         raise NotImplementedError("fused NGCF kernel needs square d x d Linear layers")
-    y = torch.empty((adj.n_rows, d), dtype=torch.float32, device=x.device)
+    if out is None:
+        y = torch.empty((adj.n_rows, d), dtype=torch.float32, device=x.device)
+    else:
+        y = out
+        if y.shape != (adj.n_rows, d) or y.stride(1) != 1 or y.stride(0) % 4:
+            raise ValueError("out must be a row-major [n_rows, d] view with ld % 4 == 0")
+        _require_device(adj, y)
     dev = x.device
     w1 = W1.detach().to(dev, torch.float32).contiguous()
     w2 = W2.detach().to(dev, torch.float32).contiguous()

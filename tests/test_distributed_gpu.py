@@ -1,0 +1,95 @@
+"""Sharded forwards with the NATIVE kernels: two ranks sharing the one MI355X over gloo
+(host-staged exchange; RCCL refuses two ranks on one GPU). Every rank's rows must equal the
+single-device forward of the whole graph: bit for bit for LightGCN and NGCF+GAS (each kernel
+computes a row from that row's inputs only), within 1e-5 for GAT (its projections are
+library GEMMs over a different number of rows)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _graph():
+    from src.ops import CsrGraph
+    rng = np.random.default_rng(11)
+    nu, ni, n = 3000, 2000, 60000
+    u = rng.integers(0, nu, n)
+    i = np.minimum(rng.zipf(1.6, n) - 1, ni - 1)  # skewed items: some heavy rows
+    u = np.concatenate([u, np.arange(nu), rng.integers(0, nu, ni)])
+    i = np.concatenate([i, rng.integers(0, ni, nu), np.arange(ni)])
+    return CsrGraph.from_interactions(u, i, nu, ni, binary=True), nu, ni
+
+
+def _model(kind, nu, ni, dev):
+    from src.models import GAT, LightGCN, NGCFGroupShuffle
+    torch.manual_seed(7)
+    if kind == "lightgcn":
+        m = LightGCN(nu, ni, 64, 3, 0.1)
+    elif kind == "ngcf_gs":
+        m = NGCFGroupShuffle(nu, ni, 64, [64, 64, 64], 0.1, 0.1, 8, 0.3)
+    else:
+        m = GAT(nu, ni, 64, 3, 4, 0.1, 0.2, 0.1)
+    return m.to(dev).eval()
+
+
+def _worker(rank, world, port, kind, exchange, q):
+    import sys
+    from conftest import PKG, ROOT
+    sys.path[:0] = [str(ROOT), str(PKG)]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from src.ops.distributed import (DistributedGraph, gat_forward_dist,
+                                         lightgcn_propagate_dist, ngcf_forward_dist)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        full, nu, ni = _graph()
+        m = _model(kind, nu, ni, dev)
+        with torch.no_grad():
+            dg = DistributedGraph(full, rank, world, dev, exchange=exchange)
+            x0p = dg.pad_table(m._initial_table())
+            if kind == "lightgcn":
+                mine = lightgcn_propagate_dist(dg, x0p, 3, overlap_chunks=3)
+            elif kind == "ngcf_gs":
+                mine = ngcf_forward_dist(dg, m, x0p)
+            else:
+                mine = gat_forward_dist(dg, m, x0p)
+            u, i = m(full.to(dev))
+            ref = torch.cat([u, i])[dg.row_begin:dg.row_end]
+            q.put((rank, mine.cpu().numpy(), ref.cpu().numpy(), dg.exchange_mode))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,exchange", [("lightgcn", "p2p"), ("lightgcn", "allgather"),
+                                           ("ngcf_gs", "auto"), ("gat", "auto")])
+def test_two_ranks_native_match_single_device(cuda, kind, exchange):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, kind, exchange, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, mine, ref, mode in res:
+        assert mine.shape == ref.shape and mine.shape[0] > 0
+        assert np.isfinite(mine).all()
+        if kind == "gat":
+            np.testing.assert_allclose(mine, ref, rtol=0, atol=1e-5)
+        else:
+            np.testing.assert_array_equal(mine.view(np.uint32), ref.view(np.uint32))

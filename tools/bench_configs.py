@@ -1,28 +1,39 @@
-"""Secondary benchmarks: the BASELINE.json configs other than the headline (1 GPU).
+"""Secondary benchmarks: the BASELINE.json configs other than the headline.
 
-    python tools/bench_configs.py [--configs 2 3 4 5] [--steps 10]
+    python tools/bench_configs.py [--configs 2 3 4 5] [--steps 10] [--g1b]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \\
+        --master-port P tools/bench_configs.py --gpus N --configs 3 4 5
 
   2  ML-1M-shaped LightGCN K=3 d=64 (synthetic 6040 x 3706, 1M ratings -> reference
-     preprocessing), model-class forward
-  3  G100M NGCF K=3 d=64 + GAS after every layer (NGCFGroupShuffle, one fused MFMA kernel
-     per layer), eval forward
-  4  G100M LightGCN K=3 d=128 (the 8-GPU config run on one GPU; the sharded run is bench.py)
-  5  power-law bipartite graph, GAT d=64 4 heads K=3 (a 1-GPU slice of the G1B config:
-     Zipf-popularity users/items, every node degree >= 1)
+     preprocessing), model-class forward (1 GPU only)
+  3  G100M NGCF K=3 d=64 + GAS after every layer (NGCFGroupShuffle: hop + streaming MFMA
+     transform per layer), eval forward
+  4  G100M LightGCN K=3 d=128 (the 8-GPU config; dst-row shards at N > 1)
+  5  power-law bipartite graph, GAT d=64 4 heads K=3: by default a 2M x 2M, 50M-pair slice;
+     --g1b: the full 10M x 10M, 1B-pair configuration (Zipf exponent 0.9, seed 0, every node
+     degree >= 1)
 
-Each config prints one JSON line: ms per forward, edges/s (= layers * nnz / t), and the
-per-kernel times from HIP events where the kernels are called directly.
+N > 1: one process per GPU; every rank builds the same graph and model (same seeds), keeps
+its destination-row shard and runs the sharded forward of src/ops/distributed.py (per layer:
+local kernels, then one exchange of the rows its neighbours read). Time = max over ranks.
+--verify compares every rank's rows with a single-device forward of the whole graph
+(bit-exact for LightGCN and NGCF; GAT's projections are library GEMMs over a different
+number of rows, so it is held to 1e-5).
+
+Each config prints one JSON line: ms per forward and edges/s (= layers * nnz / t).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import os
 import sys
 import time
 from pathlib import Path
 
 import numpy as np
 import torch
+import torch.distributed as dist
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "gnn-recommendations_amd"))
@@ -32,89 +43,185 @@ import bench  # noqa: E402
 from src.data.dataset import RecommendationDataset  # noqa: E402
 from src.models import GAT, LightGCN, NGCFGroupShuffle  # noqa: E402
 from src.ops import CsrGraph  # noqa: E402
+from src.ops.distributed import (DistributedGraph, gat_forward_dist,  # noqa: E402
+                                 lightgcn_propagate_dist, make_work, ngcf_forward_dist)
 
 
-def time_fn(fn, steps, warmup=2):
-    for _ in range(warmup):
-        fn()
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(steps):
-        fn()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) / steps
+def zipf_ids(rng, n: int, count: int, a: float, chunk: int = 1 << 26) -> np.ndarray:
+    """`count` ids in [0, n) with P(k) ~ (k+1)^-a (inverse CDF of the continuous power law on
+    [1, n+1), vectorised in chunks; rng.choice over 10M categories would take minutes)."""
+    out = np.empty(count, dtype=np.int64)
+    e = 1.0 - a
+    top = (n + 1.0) ** e - 1.0
+    for s in range(0, count, chunk):
+        u = rng.random(min(chunk, count - s))
+        k = np.floor((u * top + 1.0) ** (1.0 / e)) - 1.0
+        out[s:s + u.size] = np.minimum(k, n - 1).astype(np.int64)
+    return out
 
 
-def powerlaw_graph(n_users, n_items, n_pairs, a, seed):
+def powerlaw_graph(n_users, n_items, n_pairs, a, seed, threads=16):
     rng = np.random.default_rng(seed)
-    pu = 1.0 / np.arange(1, n_users + 1) ** a
-    pi = 1.0 / np.arange(1, n_items + 1) ** a
-    u = rng.choice(n_users, n_pairs, p=pu / pu.sum())
-    i = rng.choice(n_items, n_pairs, p=pi / pi.sum())
+    u = zipf_ids(rng, n_users, n_pairs, a)
+    i = zipf_ids(rng, n_items, n_pairs, a)
     # min degree >= 1 (the reference's dense GAT turns an isolated node into all-NaN)
     u = np.concatenate([u, np.arange(n_users), rng.integers(0, n_users, n_items)])
     i = np.concatenate([i, rng.integers(0, n_items, n_users), np.arange(n_items)])
-    return CsrGraph.from_interactions(u, i, n_users, n_items, binary=True, n_threads=16)
+    return CsrGraph.from_interactions(u, i, n_users, n_items, binary=True, n_threads=threads)
+
+
+def timed(fn, steps, warmup, world, device):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([(time.perf_counter() - t0) / steps * 1e3], dtype=torch.float64,
+                     device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item()), out
+
+
+def total(v, world, device):
+    t = torch.tensor([float(v)], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t)
+    return float(t.item())
+
+
+def rank_max(v, world, device):
+    t = torch.tensor([float(v)], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def check(mine, ref, exact, world, device):
+    diff = float((mine - ref).abs().max()) if mine.numel() else 0.0
+    ok = torch.equal(mine, ref) if exact else diff <= 1e-5
+    flag = torch.tensor([1 if ok else 0], device=device)
+    if world > 1:
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return {"bit_exact" if exact else "within_1e-5": bool(flag.item()), "max_abs_diff": diff}
 
 
 def main(argv=None):
-    ap = argparse.ArgumentParser()
+    ap = argparse.ArgumentParser(description=__doc__,
+                                 formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--configs", nargs="+", type=int, default=[2, 3, 4, 5])
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--g1b", action="store_true", help="config 5 at full size (10M x 10M, 1B pairs)")
+    ap.add_argument("--verify", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     a = ap.parse_args(argv)
-    dev = torch.device("cuda", 0)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    device = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
+    torch.cuda.set_device(device)
+    if world > 1:
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group("gloo")
+    threads = max(1, bench.host_threads() // world)
     out = []
-    g100 = None
-    if 3 in a.configs or 4 in a.configs:
-        g100 = bench.build_graph(1_000_000, 1_000_000, 100_000_000, 0, 16).to(dev)
+
+    def emit(rec):
+        rec["n_gpus"] = world
+        if rank == 0:
+            print(json.dumps(rec), flush=True)
+        out.append(rec)
+
     with torch.no_grad():
-        if 2 in a.configs:
+        if 2 in a.configs and world == 1:
             ds = RecommendationDataset.synthetic_movielens(6040, 3706, 1_000_209, seed=1, name="ml-1m")
-            g = ds.get_graph(dev)
+            g = ds.get_graph(device)
             torch.manual_seed(0)
-            m = LightGCN(ds.n_users, ds.n_items, 64, 3, 0.1).to(dev).eval()
-            t = time_fn(lambda: m(g), a.steps * 10)
-            out.append({"config": 2, "workload": "ML-1M-shaped LightGCN K=3 d=64 forward",
-                        "nnz": g.nnz, "n_nodes": g.shape[0], "ms": t,
-                        "edges_per_s": 3 * g.nnz / (t * 1e-3)})
+            m = LightGCN(ds.n_users, ds.n_items, 64, 3, 0.1).to(device).eval()
+            t, _ = timed(lambda: m(g), a.steps * 10, a.warmup, 1, device)
+            emit({"config": 2, "workload": "ML-1M-shaped LightGCN K=3 d=64 forward",
+                  "nnz": g.nnz, "n_nodes": g.shape[0], "ms": t,
+                  "edges_per_s": 3 * g.nnz / (t * 1e-3)})
+        g100 = None
+        if 3 in a.configs or 4 in a.configs:
+            g100 = bench.build_graph(1_000_000, 1_000_000, 100_000_000, 0, threads)
         if 3 in a.configs:
             torch.manual_seed(0)
-            m = NGCFGroupShuffle(1_000_000, 1_000_000, 64, [64, 64, 64], 0.1, 0.01, 8, 0.3).to(dev).eval()
-            t = time_fn(lambda: m(g100), a.steps)
-            for L in m.layers:
-                L.single_kernel = True
-            t1 = time_fn(lambda: m(g100), a.steps)
-            out.append({"config": 3, "workload": "G100M NGCF K=3 d=64 + GAS (hop + streaming "
-                        "MFMA transform per layer)", "nnz": g100.nnz, "ms": t,
-                        "edges_per_s": 3 * g100.nnz / (t * 1e-3),
-                        "ms_single_kernel_form": t1,
-                        "mfma_flops_per_s": 3 * 2 * 2_000_000 * 128 * 64 / (t * 1e-3)})
-            del m
+            m = NGCFGroupShuffle(1_000_000, 1_000_000, 64, [64, 64, 64], 0.1, 0.01, 8, 0.3).to(device).eval()
+            dg = DistributedGraph(g100, rank, world, device)
+            x0p = dg.pad_table(m._initial_table())
+            t, mine = timed(lambda: ngcf_forward_dist(dg, m, x0p), a.steps, a.warmup, world, device)
+            rec = {"config": 3, "workload": "G100M NGCF K=3 d=64 + GAS (hop + streaming MFMA "
+                   "transform per layer)", "nnz": g100.nnz, "ms": t,
+                   "edges_per_s": 3 * g100.nnz / (t * 1e-3),
+                   "mfma_flops_per_s": 3 * 2 * 2_000_000 * 128 * 64 / (t * 1e-3),
+                   "exchange": dg.exchange_mode if world > 1 else None}
+            if a.verify:
+                g1 = g100.to(device)
+                u, i = m(g1)
+                rec["verify"] = check(mine, torch.cat([u, i])[dg.row_begin:dg.row_end], True,
+                                      world, device)
+                del g1, u, i
+            emit(rec)
+            del m, dg, x0p, mine
         if 4 in a.configs:
             torch.manual_seed(0)
-            m = LightGCN(1_000_000, 1_000_000, 128, 3, 0.1).to(dev).eval()
-            t = time_fn(lambda: m(g100), a.steps)
-            out.append({"config": 4, "workload": "G100M LightGCN K=3 d=128 on ONE GPU",
-                        "nnz": g100.nnz, "ms": t, "edges_per_s": 3 * g100.nnz / (t * 1e-3)})
-            del m
+            m = LightGCN(1_000_000, 1_000_000, 128, 3, 0.1).to(device).eval()
+            dg = DistributedGraph(g100, rank, world, device)
+            x0p = dg.pad_table(m._initial_table())
+            work = make_work(dg, 128, device)
+            t, mine = timed(lambda: lightgcn_propagate_dist(dg, x0p, 3, work=work),
+                            a.steps, a.warmup, world, device)
+            rec = {"config": 4, "workload": "G100M LightGCN K=3 d=128, dst-row shards",
+                   "nnz": g100.nnz, "ms": t, "edges_per_s": 3 * g100.nnz / (t * 1e-3),
+                   "exchange": dg.exchange_mode if world > 1 else None}
+            if a.verify:
+                g1 = g100.to(device)
+                u, i = m(g1)
+                rec["verify"] = check(mine, torch.cat([u, i])[dg.row_begin:dg.row_end], True,
+                                      world, device)
+                del g1, u, i
+            emit(rec)
+            del m, dg, x0p, work, mine
         del g100
         torch.cuda.empty_cache()
         if 5 in a.configs:
             t0 = time.time()
-            g = powerlaw_graph(2_000_000, 2_000_000, 50_000_000, 0.9, 0).to(dev)
-            deg = torch.diff(g.row_ptr).cpu().numpy()
+            shape = (10_000_000, 10_000_000, 1_000_000_000) if a.g1b else (2_000_000, 2_000_000, 50_000_000)
+            g = powerlaw_graph(*shape, 0.9, 0, threads)
+            build_s = time.time() - t0
+            deg = (g.row_ptr[1:] - g.row_ptr[:-1]).numpy()
             torch.manual_seed(0)
-            m = GAT(2_000_000, 2_000_000, 64, 3, 4, 0.1, 0.2, 0.1).to(dev).eval()
-            t = time_fn(lambda: m(g), a.steps)
-            out.append({"config": 5, "workload": "power-law 2Mx2M (50M pairs, Zipf 0.9) GAT d=64 "
-                        "4 heads K=3 forward (1-GPU slice of the G1B config)",
-                        "nnz": g.nnz, "max_degree": int(deg.max()), "median_degree": float(np.median(deg)),
-                        "ms": t, "edges_per_s": 3 * g.nnz / (t * 1e-3),
-                        "graph_build_s": time.time() - t0})
-    for o in out:
-        print(json.dumps(o), flush=True)
+            m = GAT(shape[0], shape[1], 64, 3, 4, 0.1, 0.2, 0.1).to(device).eval()
+            dg = DistributedGraph(g, rank, world, device)
+            x0p = dg.pad_table(m._initial_table())
+            t, mine = timed(lambda: gat_forward_dist(dg, m, x0p), a.steps, a.warmup, world, device)
+            rec = {"config": 5, "workload": f"power-law {shape[0]}x{shape[1]} ({shape[2]} pairs, "
+                   f"Zipf 0.9, seed 0) GAT d=64 4 heads K=3 forward", "nnz": g.nnz,
+                   "max_degree": int(deg.max()), "median_degree": float(np.median(deg)),
+                   "ms": t, "edges_per_s": 3 * g.nnz / (t * 1e-3), "graph_build_s": build_s,
+                   "shard_nnz_max": int(rank_max(dg.shard.nnz, world, device)),
+                   "exchange": dg.exchange_mode if world > 1 else None}
+            if a.verify:
+                del x0p
+                g1 = g.to(device)
+                u, i = m(g1)
+                rec["verify"] = check(mine, torch.cat([u, i])[dg.row_begin:dg.row_end], False,
+                                      world, device)
+                del g1, u, i
+            emit(rec)
+    if world > 1:
+        dist.destroy_process_group()
+    return out
 
 
 if __name__ == "__main__":
