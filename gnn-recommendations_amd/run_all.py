@@ -25,7 +25,6 @@ from pathlib import Path
 import numpy as np
 import pandas as pd
 import torch
-import torch.nn.functional as F
 import yaml
 
 ROOT = Path(__file__).resolve().parent
@@ -34,6 +33,7 @@ sys.path.insert(0, str(ROOT))
 from src.data import RecommendationDataset  # noqa: E402
 from src.evaluation import Evaluator  # noqa: E402
 from src.models import GAT, NGCF, LightGCN, NGCFGroupShuffle, OrthogonalBundleGNN  # noqa: E402
+from src.training import Trainer  # noqa: E402
 
 MODEL_REGISTRY = {"lightgcn": LightGCN, "ngcf": NGCF, "ngcf_gs": NGCFGroupShuffle, "gat": GAT,
                   "orthogonal_bundle": OrthogonalBundleGNN}
@@ -73,31 +73,14 @@ def load_dataset(name: str, seed: int) -> RecommendationDataset:
 
 
 def train_bpr(model, dataset, adj, cfg: dict, epochs: int, device, seed: int) -> float:
-    """BPR training with full-graph propagation per batch (trainer.py:199-281)."""
+    """BPR training (src/training/trainer.py: the reference's per-batch full-graph propagation,
+    [B, 1] negatives, clipping, Adam) for `epochs` epochs; returns the wall time."""
     if epochs <= 0:
         return 0.0
-    opt = torch.optim.Adam(model.parameters(), lr=float(cfg.get("learning_rate", 1e-3)),
-                           weight_decay=float(cfg.get("weight_decay", 1e-4)))
-    bs = int(cfg.get("batch_size", 512))
-    tr = dataset.train_data
-    users = torch.as_tensor(tr["userId"].to_numpy(), device=device)
-    items = torch.as_tensor(tr["itemId"].to_numpy(), device=device)
-    gen = torch.Generator(device="cpu").manual_seed(seed)
+    t = Trainer(model, dataset, dict(cfg, epochs=epochs), device=device, seed=seed)
     t0 = time.time()
-    model.train()
     for _ in range(epochs):
-        perm = torch.randperm(users.numel(), generator=gen).to(device)
-        for s in range(0, users.numel(), bs):
-            b = perm[s:s + bs]
-            neg = torch.randint(0, dataset.n_items, (b.numel(),), generator=gen).to(device)
-            u_emb, i_emb = model.get_all_embeddings(adj)
-            pos_s = (u_emb[users[b]] * i_emb[items[b]]).sum(1)
-            neg_s = (u_emb[users[b]] * i_emb[neg]).sum(1)
-            loss = -F.logsigmoid(pos_s - neg_s).mean()
-            opt.zero_grad()
-            loss.backward()
-            torch.nn.utils.clip_grad_norm_(model.parameters(), float(cfg.get("max_grad_norm", 1.0)))
-            opt.step()
+        t.train_epoch()
     if device.type == "cuda":
         torch.cuda.synchronize()
     return time.time() - t0

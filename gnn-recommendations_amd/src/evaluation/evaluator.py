@@ -77,7 +77,11 @@ class Evaluator:
             rows.append(idx.cpu())
         return torch.cat(rows)
 
-    def evaluate(self, model, dataset, test_data=None, adj_matrix=None) -> Dict[str, float]:
+    def evaluate(self, model, dataset, test_data=None, adj_matrix=None,
+                 mask_valid: bool = True) -> Dict[str, float]:
+        """Metrics over test_data (default: the test split) with train (+ valid when
+        mask_valid; the trainer's validation masks train items only, trainer.py:321-333)
+        items excluded from the ranking."""
         model.eval()
         test_data = dataset.test_data if test_data is None else test_data
         with torch.no_grad():
@@ -91,6 +95,6 @@ class Evaluator:
             users = sorted(gt)
             if not users:
                 return {}
-            seen_ptr, seen_col = dataset.seen_items()
+            seen_ptr, seen_col = dataset.seen_items(include_valid=mask_valid)
             topk = self.topk(user_emb, item_emb, users, max(self.k_values), seen_ptr, seen_col)
             return compute_metrics_from_topk(topk, users, gt, dataset.n_items, self.k_values)

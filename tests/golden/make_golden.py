@@ -180,6 +180,39 @@ def main():
         arrs[f"bc_perm_{li}"] = bcl.shuffle_perm.numpy()
     np.savez(OUT / "ob_d64.npz", **arrs)
 
+    # ---- §8f1: BPR training (reference sampler RNG order, [B,B] loss quirk, Adam steps) -----
+    from types import SimpleNamespace
+    from src.training.trainer import Trainer as RefTrainer
+    from src.training.losses import BPRLoss as RefBPR
+    pairs = list(zip(u.tolist(), i.tolist()))
+    fake = SimpleNamespace(batch_size=64, negative_samples=1, device=torch.device("cpu"))
+    torch.manual_seed(55)
+    batches = [RefTrainer._sample_batch(fake, pairs, ni) for _ in range(3)]
+    torch.manual_seed(56)
+    m = LightGCN(nu, ni, embedding_dim=64, n_layers=3, init_scale=0.1)
+    w0 = (m.user_embedding.weight.detach().clone(), m.item_embedding.weight.detach().clone())
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2, weight_decay=1e-4)
+    loss_fn = RefBPR()
+    losses = []
+    m.train()
+    for bu, bp, bn in batches:   # the body of trainer.py:248-279
+        ue, ie = m.get_all_embeddings(t_adj)
+        ps = (ue[bu] * ie[bp]).sum(dim=1)
+        ns = (ue[bu].unsqueeze(1) * ie[bn]).sum(dim=2)
+        loss = loss_fn(ps, ns)
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)
+        opt.step()
+        losses.append(loss.item())
+    np.savez(OUT / "bpr_train_K3_d64.npz", graph="g_small",
+             users=np.stack([b[0].numpy() for b in batches]),
+             pos=np.stack([b[1].numpy() for b in batches]),
+             neg=np.stack([b[2].numpy() for b in batches]),
+             user_w0=w0[0].numpy(), item_w0=w0[1].numpy(), losses=np.array(losses),
+             user_w=m.user_embedding.weight.detach().numpy(),
+             item_w=m.item_embedding.weight.detach().numpy())
+
     # ---- a11: GAT eval forward (dense reference; min-degree >= 1 so no NaN rows) -------------
     gu, gi = interactions(41, 60, 80, 500, min_deg=True)
     gnorm, _, gt = ref_graph(gb, gu, gi, 60, 80)

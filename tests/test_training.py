@@ -1,0 +1,98 @@
+"""§8f1 training path: the reference's sampler RNG order, the [B, B] BPR broadcast, and three
+Adam steps of LightGCN against goldens made by running the reference trainer's own code
+(tests/golden/make_golden.py). CPU here; the native (GPU) variant is in test_training_gpu."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_csr, load_golden
+
+from src.models import LightGCN
+from src.ops import CsrGraph
+from src.training import BPRLoss, DeviceSampler, ReferenceSampler, Trainer, bpr_scores, train_step
+
+
+def _golden_graph():
+    rp, col, val, nu, ni = golden_csr("g_small")
+    g = CsrGraph(torch.from_numpy(rp), torch.from_numpy(col), torch.from_numpy(val),
+                 (rp.size - 1, rp.size - 1), nu, ni, True)
+    return g, nu, ni
+
+
+def test_reference_sampler_matches_reference_rng_stream():
+    f = load_golden("bpr_train_K3_d64")
+    gg = load_golden("graph_g_small")
+    pairs = list(zip(gg["users"].tolist(), gg["items"].tolist()))
+    s = ReferenceSampler(pairs, int(gg["n_items"]), 64, 1)
+    torch.manual_seed(55)
+    for b in range(3):
+        u, p, n = s()
+        np.testing.assert_array_equal(u.numpy(), f["users"][b])
+        np.testing.assert_array_equal(p.numpy(), f["pos"][b])
+        np.testing.assert_array_equal(n.numpy(), f["neg"][b])
+        assert n.shape == (64, 1)
+
+
+def test_bpr_loss_keeps_the_broadcast():
+    pos, neg = torch.randn(5), torch.randn(5, 1)
+    ref = -torch.nn.functional.logsigmoid(pos.view(1, 5) - neg.view(5, 1)).mean()
+    assert torch.equal(BPRLoss()(pos, neg), ref)
+
+
+def _run_steps(adj, device):
+    f = load_golden("bpr_train_K3_d64")
+    _, nu, ni = _golden_graph()
+    torch.manual_seed(56)
+    m = LightGCN(nu, ni, embedding_dim=64, n_layers=3, init_scale=0.1).to(device)
+    np.testing.assert_array_equal(m.user_embedding.weight.detach().cpu().numpy(), f["user_w0"])
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2, weight_decay=1e-4)
+    m.train()
+    losses = []
+    for b in range(3):
+        args = [torch.from_numpy(f[k][b]).to(device) for k in ("users", "pos", "neg")]
+        losses.append(float(train_step(m, adj, *args, opt, BPRLoss(), 1.0)))
+    return f, m, np.array(losses)
+
+
+def test_three_adam_steps_match_reference_cpu():
+    g, _, _ = _golden_graph()
+    f, m, losses = _run_steps(g.to_torch_sparse_coo(), "cpu")
+    np.testing.assert_allclose(losses, f["losses"], rtol=1e-6)
+    np.testing.assert_allclose(m.user_embedding.weight.detach().numpy(), f["user_w"], atol=1e-6)
+    np.testing.assert_allclose(m.item_embedding.weight.detach().numpy(), f["item_w"], atol=1e-6)
+
+
+def test_device_sampler_law():
+    rng = np.random.default_rng(0)
+    nu, ni = 50, 40
+    u = rng.integers(0, nu, 1500)
+    i = rng.integers(0, ni, 1500)
+    s = DeviceSampler(u, i, ni, 256, negative_samples=2, device="cpu", seed=3)
+    pos_set = set(zip(u.tolist(), i.tolist()))
+    bu, bp, bn = s()
+    assert bu.shape == (256,) and bn.shape == (256, 2)
+    assert all((a, b) in pos_set for a, b in zip(bu.tolist(), bp.tolist()))
+    # a negative may only be a positive when all ten checked draws were positives
+    dense = np.array([len({b for a, b in pos_set if a == x}) for x in range(nu)]) / ni
+    bad = [(a, n) in pos_set for a, row in zip(bu.tolist(), bn.tolist()) for n in row]
+    assert np.mean(bad) <= max(0.05, 3 * float(np.mean(dense ** 10)))
+    assert s.is_positive(bu, bp).all()
+
+
+def test_trainer_runs_and_learns_on_cpu():
+    from src.data.dataset import RecommendationDataset
+    ds = RecommendationDataset.synthetic_movielens(n_users=120, n_items=200, n_ratings=4000, seed=2)
+    torch.manual_seed(0)
+    m = LightGCN(ds.n_users, ds.n_items, 32, 2, 0.1)
+    cfg = dict(batch_size=256, epochs=3, eval_every=1, learning_rate=5e-3, use_scheduler=True,
+               warmup_epochs=1, validation_metrics=["recall@10", "ndcg@10"])
+    t = Trainer(m, ds, cfg, device="cpu", sampler="reference")
+    res = t.train()
+    assert len(res["train_losses"]) == 3 and res["train_losses"][-1] < res["train_losses"][0]
+    assert set(res["valid_metrics"][0]) >= {"recall@10", "ndcg@10"}
+
+
+def test_bpr_scores_shapes():
+    ue, ie = torch.randn(4, 8), torch.randn(6, 8)
+    p, n = bpr_scores(ue, ie, torch.tensor([0, 1]), torch.tensor([2, 3]), torch.tensor([[4], [5]]))
+    assert p.shape == (2,) and n.shape == (2, 1)

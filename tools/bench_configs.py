@@ -9,6 +9,9 @@
   3  G100M NGCF K=3 d=64 + GAS after every layer (NGCFGroupShuffle: hop + streaming MFMA
      transform per layer), eval forward
   4  G100M LightGCN K=3 d=128 (the 8-GPU config; dst-row shards at N > 1)
+  6  G100M LightGCN K=3 d=64 BPR training step (1 GPU): batch 2048 from the
+     device sampler, full propagation forward + fused backward (same propagation over A^T),
+     the reference's [B, B] BPR loss, clip_grad_norm_, Adam
   5  power-law bipartite graph, GAT d=64 4 heads K=3: by default a 2M x 2M, 50M-pair slice;
      --g1b: the full 10M x 10M, 1B-pair configuration (Zipf exponent 0.9, seed 0, every node
      degree >= 1)
@@ -152,7 +155,7 @@ def main(argv=None):
                   "nnz": g.nnz, "n_nodes": g.shape[0], "ms": t,
                   "edges_per_s": 3 * g.nnz / (t * 1e-3)})
         g100 = None
-        if 3 in a.configs or 4 in a.configs:
+        if 3 in a.configs or 4 in a.configs or (6 in a.configs and world == 1):
             g100 = bench.build_graph(1_000_000, 1_000_000, 100_000_000, 0, threads)
         if 3 in a.configs:
             torch.manual_seed(0)
@@ -192,6 +195,24 @@ def main(argv=None):
                 del g1, u, i
             emit(rec)
             del m, dg, x0p, work, mine
+        if 6 in a.configs and world == 1:
+            from src.training import BPRLoss, DeviceSampler, train_step
+            torch.manual_seed(0)
+            m = LightGCN(1_000_000, 1_000_000, 64, 3, 0.1).to(device).train()
+            g1 = g100.to(device)
+            rp = g100.row_ptr.numpy()
+            users = np.repeat(np.arange(1_000_000), np.diff(rp[:1_000_001]))
+            items = g100.col.numpy()[:rp[1_000_000]] - 1_000_000
+            samp = DeviceSampler(users, items, 1_000_000, 2048, 1, device, seed=0)
+            opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-4)
+            loss_fn = BPRLoss()
+            with torch.enable_grad():
+                t, loss = timed(lambda: train_step(m, g1, *samp(), opt, loss_fn, 1.0),
+                                a.steps, a.warmup, 1, device)
+            emit({"config": 6, "workload": "G100M LightGCN K=3 d=64 BPR train step (batch 2048, "
+                  "fwd + fused bwd propagation, Adam)", "nnz": g1.nnz, "ms": t,
+                  "edges_per_s": 2 * 3 * g1.nnz / (t * 1e-3), "loss": float(loss)})
+            del m, g1, opt, samp
         del g100
         torch.cuda.empty_cache()
         if 5 in a.configs:
