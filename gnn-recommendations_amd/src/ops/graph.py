@@ -164,6 +164,58 @@ class CsrGraph:
         return g.to(device)
 
     @classmethod
+    def from_interactions_device(cls, users, items, n_users: int, n_items: int,
+                                 normalization: str = "symmetric", self_loop: bool = False,
+                                 binary: bool = False, device="cuda") -> "CsrGraph":
+        """from_interactions built in HBM: sort-based CSR construction and the
+        value products run on the GPU (gnnrec_build_bipartite_csr_device /
+        gnnrec_normalize_values_device); only the N degrees make a host round trip for the
+        numpy float32 power of graph_builder.py:119. Bit-identical to from_interactions."""
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            raise ValueError("from_interactions_device needs a ROCm device")
+        u = torch.as_tensor(users, dtype=torch.int64).to(dev).contiguous()
+        i = torch.as_tensor(items, dtype=torch.int64).to(dev).contiguous()
+        if u.shape != i.shape or u.dim() != 1:
+            raise ValueError("users and items must be 1-D and of the same length")
+        N = int(n_users) + int(n_items)
+        P = u.numel()
+        cap = max(2 * P + (N if self_loop else 0), 1)
+        flags = (1 if self_loop else 0) | (2 if binary else 0)
+        L = _lib.lib()
+        stream = _lib.stream_of(dev)
+        row_ptr = torch.empty(N + 1, dtype=torch.int64, device=dev)
+        col = torch.empty(cap, dtype=torch.int32, device=dev)
+        cnt = torch.empty(cap, dtype=torch.float32, device=dev)
+        deg = torch.empty(max(N, 1), dtype=torch.float32, device=dev)
+        nbytes = _lib.C.c_size_t(0)
+        nnz = _lib.C.c_int64(0)
+        args = [_lib.ptr(u), _lib.ptr(i), P, int(n_users), int(n_items), flags,
+                _lib.ptr(row_ptr), _lib.ptr(col), _lib.ptr(cnt), _lib.ptr(deg)]
+        _lib.check(L.gnnrec_build_bipartite_csr_device(*args, _lib.C.addressof(nnz), None,
+                                                        _lib.C.addressof(nbytes), stream),
+                   "build_bipartite_csr_device")
+        work = torch.empty(max(int(nbytes.value), 1), dtype=torch.uint8, device=dev)
+        _lib.check(L.gnnrec_build_bipartite_csr_device(*args, _lib.C.addressof(nnz),
+                                                        _lib.ptr(work), _lib.C.addressof(nbytes),
+                                                        stream), "build_bipartite_csr_device")
+        del work
+        nz = int(nnz.value)
+        col, cnt = col[:nz], cnt[:nz]
+        if normalization == "none":
+            val = cnt
+        else:
+            dis = torch.from_numpy(inv_sqrt_degrees(deg[:N].cpu().numpy(), normalization)).to(dev)
+            val = torch.empty(max(nz, 1), dtype=torch.float32, device=dev)[:nz]
+            _lib.check(L.gnnrec_normalize_values_device(
+                _lib.ptr(row_ptr), _lib.ptr(col), _lib.ptr(cnt), N, _lib.ptr(dis),
+                0 if normalization == "symmetric" else 1, _lib.ptr(val), stream),
+                "normalize_values_device")
+        return cls(row_ptr, col.clone(), val.clone(),
+                   (N, N), int(n_users), int(n_items),
+                   symmetric=normalization in ("symmetric", "none"))
+
+    @classmethod
     def from_scipy(cls, adj, n_users: Optional[int] = None, n_items: Optional[int] = None,
                    symmetric: Optional[bool] = None, device="cpu") -> "CsrGraph":
         """From any scipy sparse matrix (e.g. the reference's norm_adj_matrix)."""

@@ -207,6 +207,27 @@ int gnnrec_normalize_values(const int64_t* row_ptr, const int32_t* col, const fl
                             int64_t n_rows, const float* dis, int32_t mode, float* val,
                             int32_t n_threads);
 
+/* ---- §8f3: on-device operand construction ----------------------------------------------
+ * Same contract and output as gnnrec_build_bipartite_csr (graph_builder.py:16-111) with every
+ * array in device memory: users/items int64 [n_pairs]; row_ptr int64 [N+1]; col int32 and
+ * cnt fp32 with capacity 2*n_pairs (+N with GNNREC_BUILD_SELF_LOOP); deg fp32 [N]. Sort-based
+ * (64-bit row|col keys, radix sort, run-length encode), so rows come out with ascending
+ * columns and duplicate pairs merged exactly as the host builder does. *nnz_out is a HOST
+ * pointer: the call synchronises `stream` before returning. Call first with
+ * workspace == NULL to get *workspace_bytes (about 20 bytes per key, keys = 2*n_pairs (+N)),
+ * then again with a device buffer of that size. Requires 2*n_pairs (+N) < 2^31 and degrees
+ * below 2^24 (they are exact fp32 integers). */
+int gnnrec_build_bipartite_csr_device(const int64_t* users, const int64_t* items,
+                                      int64_t n_pairs, int64_t n_users, int64_t n_items,
+                                      int32_t flags, int64_t* row_ptr, int32_t* col, float* cnt,
+                                      float* deg, int64_t* nnz_out, void* workspace,
+                                      size_t* workspace_bytes, gnnrec_stream_t stream);
+
+/* Device form of gnnrec_normalize_values (graph_builder.py:116-126): same values, async. */
+int gnnrec_normalize_values_device(const int64_t* row_ptr, const int32_t* col, const float* cnt,
+                                   int64_t n_rows, const float* dis, int32_t mode, float* val,
+                                   gnnrec_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
