@@ -107,10 +107,13 @@ class RecommendationDataset:
         key = (str(device), normalized)
         g = self._graphs.get(key)
         if g is None:
-            g = CsrGraph.from_interactions(self.train_data["userId"], self.train_data["itemId"],
-                                           self.n_users, self.n_items,
-                                           normalization="symmetric" if normalized else "none")
-            g = g.to(device)
+            args = (self.train_data["userId"].to_numpy(), self.train_data["itemId"].to_numpy(),
+                    self.n_users, self.n_items)
+            norm = "symmetric" if normalized else "none"
+            if torch.device(device).type == "cuda":   # built in HBM (§8f3)
+                g = CsrGraph.from_interactions_device(*args, normalization=norm, device=device)
+            else:
+                g = CsrGraph.from_interactions(*args, normalization=norm)
             self._graphs[key] = g
         return g
 

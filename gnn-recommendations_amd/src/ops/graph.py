@@ -202,7 +202,7 @@ class CsrGraph:
         del work
         nz = int(nnz.value)
         col, cnt = col[:nz], cnt[:nz]
-        if normalization == "none":
+        if normalization == "none" or nz == 0:
             val = cnt
         else:
             dis = torch.from_numpy(inv_sqrt_degrees(deg[:N].cpu().numpy(), normalization)).to(dev)
