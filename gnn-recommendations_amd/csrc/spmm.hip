@@ -15,7 +15,7 @@ template <int D>
 __global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
     Csr A, const float* __restrict__ x, int64_t ldx, float* __restrict__ y, int64_t ldy,
     int epi, const float* __restrict__ self, int64_t ld_self, float* __restrict__ acc,
-    int64_t ld_acc, float acc_div) {
+    int64_t ld_acc, float acc_div, int64_t skip_len) {
   constexpr int VEC = SpmmCfg<D>::VEC, CH = SpmmCfg<D>::CH;
   constexpr int GROUP = D / VEC;
   constexpr int RPW = 64 / GROUP;
@@ -25,6 +25,7 @@ __global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
       ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
   if (r >= A.n_rows) return;  // the whole group leaves together
   const int64_t beg = A.row_ptr[r], end = A.row_ptr[r + 1];
+  if (skip_len > 0 && end - beg > skip_len) return;  // a heavy row: spmm_heavy_kernel's
   const VecF<VEC> a = gather_row_v<VEC, GROUP, CH>(A.col, A.val, beg, end, x, ldx, gl);
   if (!(epi & GNNREC_EPI_NO_Y)) stv<VEC>(y + r * ldy + VEC * gl, a);
   acc_epilogue_v<VEC>(epi, a, self + r * ld_self + VEC * gl, acc + r * ld_acc + VEC * gl, acc_div);
@@ -34,11 +35,12 @@ __global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
 __global__ __launch_bounds__(kBlock) void spmm_generic_kernel(
     Csr A, const float* __restrict__ x, int64_t ldx, float* __restrict__ y, int64_t ldy,
     int d, int epi, const float* __restrict__ self, int64_t ld_self, float* __restrict__ acc,
-    int64_t ld_acc, float acc_div) {
+    int64_t ld_acc, float acc_div, int64_t skip_len) {
   const int lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   if (r >= A.n_rows) return;
   const int64_t beg = A.row_ptr[r], end = A.row_ptr[r + 1];
+  if (skip_len > 0 && end - beg > skip_len) return;
   for (int f = lane; f < d; f += 64) {
     float a = 0.f;
     for (int64_t k = beg; k < end; ++k) a = __builtin_fmaf(A.val[k], x[(int64_t)A.col[k] * ldx + f], a);
@@ -48,6 +50,108 @@ __global__ __launch_bounds__(kBlock) void spmm_generic_kernel(
       b = b + a;
       if (epi & GNNREC_EPI_ACC_DIV) b = b / acc_div;
       acc[r * ld_acc + f] = b;
+    }
+  }
+}
+
+// Heavy rows (one workgroup of kHeavyThreads per listed row). The bit-exact order makes a row
+// one sequential fmaf chain per feature, so a long row cannot be split; what is parallelised
+// is the GATHER: all 16 waves fetch the next chunk of neighbour rows (kHeavyChunkFloats fp32,
+// 64 KB: 4 float4 per thread in flight) into one half of an LDS double buffer while wave 0
+// runs the chain over the other half. A 3 000-neighbour row costs ~12 such rounds instead of
+// ~375 dependent 8-neighbour steps of one wave in spmm_vec_kernel.
+constexpr int kHeavyThreads = 1024;
+constexpr int kHeavyChunkFloats = 16384;                 // per buffer
+constexpr int kHeavyPieces = kHeavyChunkFloats / 4 / kHeavyThreads;  // float4 per thread
+constexpr size_t kHeavyLds = 2 * kHeavyChunkFloats * sizeof(float) + 2 * 4096 * sizeof(float);
+
+template <int F>  // features per consumer lane: d <= 64 * F
+__global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
+    Csr A, const int64_t* __restrict__ rows, const float* __restrict__ x, int64_t ldx,
+    float* __restrict__ y, int64_t ldy, int d, int epi, const float* __restrict__ self,
+    int64_t ld_self, float* __restrict__ acc, int64_t ld_acc, float acc_div) {
+  extern __shared__ float4 heavy_lds4[];
+  float* buf = reinterpret_cast<float*>(heavy_lds4);     // [2][kHeavyChunkFloats]
+  float* vbuf = buf + 2 * kHeavyChunkFloats;             // [2][4096]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t r = rows[blockIdx.x];
+  const int64_t beg = A.row_ptr[r], end = A.row_ptr[r + 1];
+  const int q4 = d >> 2;                                 // float4 per neighbour row
+  const int chk = kHeavyChunkFloats / d;                 // neighbours per chunk (<= 4096)
+  const int64_t n = end - beg;
+  const int64_t n_chunks = (n + chk - 1) / chk;
+  float4 stage[kHeavyPieces];
+  float vstage[4];
+
+  auto load = [&](int64_t c) {                           // issue the loads of chunk c
+    const int64_t k0 = beg + c * chk;
+#pragma unroll
+    for (int i = 0; i < kHeavyPieces; ++i) {
+      const int p = tid + i * kHeavyThreads, j = p / q4, part = p - j * q4;
+      const int64_t k = k0 + j;
+      stage[i] = (j < chk && k < end)
+                     ? *reinterpret_cast<const float4*>(x + (int64_t)A.col[k] * ldx + 4 * part)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = tid + i * kHeavyThreads;
+      const int64_t k = k0 + j;
+      vstage[i] = (j < chk && k < end) ? A.val[k] : 0.f;
+    }
+  };
+  auto store = [&](int b) {                              // park them in buffer b
+    float4* dst = reinterpret_cast<float4*>(buf + b * kHeavyChunkFloats);
+#pragma unroll
+    for (int i = 0; i < kHeavyPieces; ++i) {
+      const int p = tid + i * kHeavyThreads;
+      if (p / q4 < chk) dst[p] = stage[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = tid + i * kHeavyThreads;
+      if (j < chk) vbuf[b * 4096 + j] = vstage[i];
+    }
+  };
+
+  float a[F];
+#pragma unroll
+  for (int f = 0; f < F; ++f) a[f] = 0.f;
+  if (n_chunks > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  for (int64_t c = 0; c < n_chunks; ++c) {
+    const bool more = c + 1 < n_chunks;
+    if (more) load(c + 1);
+    if (wave == 0) {
+      const float* xb = buf + (c & 1) * kHeavyChunkFloats;
+      const float* vb = vbuf + (c & 1) * 4096;
+      const int m = (int)min<int64_t>(chk, end - (beg + c * chk));
+      for (int j = 0; j < m; ++j) {
+        const float v = vb[j];
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+          const int col_f = lane + 64 * f;
+          if (col_f < d) a[f] = __builtin_fmaf(v, xb[j * d + col_f], a[f]);
+        }
+      }
+    }
+    if (more) store((c + 1) & 1);
+    __syncthreads();
+  }
+  if (wave != 0) return;
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    const int col_f = lane + 64 * f;
+    if (col_f >= d) continue;
+    if (!(epi & GNNREC_EPI_NO_Y)) y[r * ldy + col_f] = a[f];
+    if (epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) {
+      float b = (epi & GNNREC_EPI_ACC_INIT) ? self[r * ld_self + col_f] : acc[r * ld_acc + col_f];
+      b = b + a[f];
+      if (epi & GNNREC_EPI_ACC_DIV) b = b / acc_div;
+      acc[r * ld_acc + col_f] = b;
     }
   }
 }
@@ -95,11 +199,11 @@ namespace {
 template <int D>
 void launch_spmm_vec4(const Csr& A, const float* x, int64_t ldx, float* y, int64_t ldy, int epi,
                       const float* self, int64_t ld_self, float* acc, int64_t ld_acc,
-                      float acc_div, hipStream_t s) {
+                      float acc_div, int64_t skip, hipStream_t s) {
   constexpr int RPB = (64 / (D / SpmmCfg<D>::VEC)) * (kBlock / 64);
   const int64_t grid = ceil_div(A.n_rows, RPB);
   hipLaunchKernelGGL(spmm_vec_kernel<D>, dim3((unsigned)grid), dim3(kBlock), 0, s, A, x, ldx,
-                     y, ldy, epi, self, ld_self, acc, ld_acc, acc_div);
+                     y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip);
 }
 
 bool vec4_ok(int d, const float* x, int64_t ldx, const float* y, int64_t ldy, int epi,
@@ -115,11 +219,13 @@ bool vec4_ok(int d, const float* x, int64_t ldx, const float* y, int64_t ldy, in
 
 }  // namespace
 
-extern "C" int gnnrec_spmm_csr_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
-                                   int64_t n_rows, const float* x, int64_t ldx, float* y,
-                                   int64_t ldy, int32_t d, int32_t epi, const float* self,
-                                   int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
-                                   gnnrec_stream_t stream) {
+extern "C" int gnnrec_spmm_csr_split_f32(const int64_t* row_ptr, const int32_t* col,
+                                         const float* val, int64_t n_rows, const float* x,
+                                         int64_t ldx, float* y, int64_t ldy, int32_t d, int32_t epi,
+                                         const float* self, int64_t ld_self, float* acc,
+                                         int64_t ld_acc, float acc_div, const int64_t* heavy_rows,
+                                         int64_t n_heavy, int64_t heavy_threshold,
+                                         gnnrec_stream_t stream) {
   GNNREC_REQUIRE(n_rows >= 0 && d >= 1, "spmm: bad sizes n_rows=%lld d=%d", (long long)n_rows, d);
   if (n_rows == 0) return GNNREC_OK;
   GNNREC_REQUIRE(row_ptr && x, "spmm: null row_ptr/x");
@@ -130,29 +236,64 @@ extern "C" int gnnrec_spmm_csr_f32(const int64_t* row_ptr, const int32_t* col, c
                  "spmm: ACC needs acc");
   GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_DIV) || (epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)),
                  "spmm: ACC_DIV without ACC_INIT/ACC_ADD");
+  GNNREC_REQUIRE(heavy_threshold >= 0 && n_heavy >= 0, "spmm: negative heavy_threshold/n_heavy");
+  const bool split = heavy_threshold > 0;
+  if (split) {
+    GNNREC_REQUIRE(n_heavy == 0 || heavy_rows, "spmm: null heavy_rows");
+    GNNREC_REQUIRE(d % 4 == 0 && d <= 256 && aligned16(x) && !(ldx & 3),
+                   "spmm: the heavy-row path needs d %% 4 == 0, d <= 256 and a 16-B aligned x "
+                   "with ldx %% 4 == 0");
+  }
   const Csr A{row_ptr, col, val, n_rows};
   hipStream_t s = as_hip(stream);
+  const int64_t skip = split ? heavy_threshold : 0;
   if (vec4_ok(d, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc)) {
     switch (d) {
-      case 8: launch_spmm_vec4<8>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, s); break;
-      case 16: launch_spmm_vec4<16>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, s); break;
-      case 32: launch_spmm_vec4<32>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, s); break;
-      case 64: launch_spmm_vec4<64>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, s); break;
-      case 128: launch_spmm_vec4<128>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, s); break;
-      default: launch_spmm_vec4<256>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, s); break;
+      case 8: launch_spmm_vec4<8>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, s); break;
+      case 16: launch_spmm_vec4<16>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, s); break;
+      case 32: launch_spmm_vec4<32>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, s); break;
+      case 64: launch_spmm_vec4<64>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, s); break;
+      case 128: launch_spmm_vec4<128>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, s); break;
+      default: launch_spmm_vec4<256>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, s); break;
     }
   } else {
     const int64_t grid = ceil_div(n_rows, kBlock / 64);
     hipLaunchKernelGGL(spmm_generic_kernel, dim3((unsigned)grid), dim3(kBlock), 0, s, A, x, ldx,
-                       y, ldy, d, epi, self, ld_self, acc, ld_acc, acc_div);
+                       y, ldy, d, epi, self, ld_self, acc, ld_acc, acc_div, skip);
   }
-  return check_launch("spmm");
+  if (int rc = check_launch("spmm")) return rc;
+  if (split && n_heavy > 0) {
+    GNNREC_REQUIRE(n_heavy < (int64_t)INT32_MAX, "spmm: too many heavy rows");
+    const dim3 grid((unsigned)n_heavy), block(kHeavyThreads);
+    if (d <= 64)
+      hipLaunchKernelGGL(spmm_heavy_kernel<1>, grid, block, kHeavyLds, s, A, heavy_rows, x, ldx, y,
+                         ldy, d, epi, self, ld_self, acc, ld_acc, acc_div);
+    else if (d <= 128)
+      hipLaunchKernelGGL(spmm_heavy_kernel<2>, grid, block, kHeavyLds, s, A, heavy_rows, x, ldx, y,
+                         ldy, d, epi, self, ld_self, acc, ld_acc, acc_div);
+    else
+      hipLaunchKernelGGL(spmm_heavy_kernel<4>, grid, block, kHeavyLds, s, A, heavy_rows, x, ldx, y,
+                         ldy, d, epi, self, ld_self, acc, ld_acc, acc_div);
+    return check_launch("spmm_heavy");
+  }
+  return GNNREC_OK;
 }
 
-extern "C" int gnnrec_lightgcn_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
-                                   int64_t n_rows, const float* x0, int32_t d, int32_t n_layers,
-                                   float* work0, float* work1, float* layers, float* out,
-                                   int64_t ld_out, gnnrec_stream_t stream) {
+extern "C" int gnnrec_spmm_csr_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
+                                   int64_t n_rows, const float* x, int64_t ldx, float* y,
+                                   int64_t ldy, int32_t d, int32_t epi, const float* self,
+                                   int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
+                                   gnnrec_stream_t stream) {
+  return gnnrec_spmm_csr_split_f32(row_ptr, col, val, n_rows, x, ldx, y, ldy, d, epi, self,
+                                   ld_self, acc, ld_acc, acc_div, nullptr, 0, 0, stream);
+}
+
+extern "C" int gnnrec_lightgcn_split_f32(const int64_t* row_ptr, const int32_t* col,
+                                         const float* val, int64_t n_rows, const float* x0,
+                                         int32_t d, int32_t n_layers, float* work0, float* work1,
+                                         float* layers, float* out, int64_t ld_out,
+                                         const int64_t* heavy_rows, int64_t n_heavy,
+                                         int64_t heavy_threshold, gnnrec_stream_t stream) {
   GNNREC_REQUIRE(n_layers >= 0 && d >= 1 && n_rows >= 0, "lightgcn: bad sizes");
   GNNREC_REQUIRE(x0 && out && ld_out >= d, "lightgcn: null x0/out");
   GNNREC_REQUIRE(layers || n_layers <= 1 || (work0 && work1), "lightgcn: need work0/work1 or layers");
@@ -172,12 +313,21 @@ extern "C" int gnnrec_lightgcn_f32(const int64_t* row_ptr, const int32_t* col, c
       epi |= GNNREC_EPI_ACC_DIV;
       if (!layers) epi |= GNNREC_EPI_NO_Y;
     }
-    const int rc = gnnrec_spmm_csr_f32(row_ptr, col, val, n_rows, in, d, yk, d, d, epi, x0, d, out,
-                                       ld_out, (float)(n_layers + 1), stream);
+    const int rc = gnnrec_spmm_csr_split_f32(row_ptr, col, val, n_rows, in, d, yk, d, d, epi, x0,
+                                             d, out, ld_out, (float)(n_layers + 1), heavy_rows,
+                                             n_heavy, heavy_threshold, stream);
     if (rc != GNNREC_OK) return rc;
     in = yk;
   }
   return GNNREC_OK;
+}
+
+extern "C" int gnnrec_lightgcn_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
+                                   int64_t n_rows, const float* x0, int32_t d, int32_t n_layers,
+                                   float* work0, float* work1, float* layers, float* out,
+                                   int64_t ld_out, gnnrec_stream_t stream) {
+  return gnnrec_lightgcn_split_f32(row_ptr, col, val, n_rows, x0, d, n_layers, work0, work1,
+                                   layers, out, ld_out, nullptr, 0, 0, stream);
 }
 
 namespace {

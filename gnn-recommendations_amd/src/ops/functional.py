@@ -40,21 +40,42 @@ def _csr_args(adj: CsrGraph):
     return ptr(adj.row_ptr), ptr(adj.col), ptr(adj.val), adj.n_rows
 
 
+# Rows longer than this go to the workgroup-per-row kernel (bit-exact, LDS-pipelined gather);
+# 0 disables the split. The light kernel's per-row latency grows with the row, the heavy
+# kernel's is ~1.5 us per 64 KB of neighbour rows.
+SPMM_HEAVY_THRESHOLD = 1024
+
+
+def _heavy_args(adj: CsrGraph, x: torch.Tensor, heavy_threshold: int):
+    """(heavy_rows ptr, n_heavy, threshold) for the split launch, or the no-split triple."""
+    d = x.shape[1]
+    if (heavy_threshold <= 0 or d % 4 or d > 256 or x.stride(0) % 4
+            or x.data_ptr() % 16):
+        return None, 0, 0
+    rows = adj.heavy_rows(heavy_threshold)
+    if rows is None:
+        return None, 0, 0
+    return ptr(rows), rows.numel(), int(heavy_threshold)
+
+
 # ---- raw launches (no autograd) ---------------------------------------------------------
 def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi: int = 0,
               self_rows: Optional[torch.Tensor] = None, acc: Optional[torch.Tensor] = None,
-              acc_div: float = 1.0) -> None:
-    """y = A x with an optional fused layer-mean epilogue (gnnrec_spmm_csr_f32)."""
+              acc_div: float = 1.0, heavy_threshold: Optional[int] = None) -> None:
+    """y = A x with an optional fused layer-mean epilogue (gnnrec_spmm_csr_split_f32: rows
+    longer than `heavy_threshold` run on the workgroup-per-row kernel)."""
     _require_device(adj, x, y, self_rows, acc)
     d = x.shape[1]
     if x.shape[0] < adj.shape[1]:
         raise ValueError(f"x has {x.shape[0]} rows, operand has {adj.shape[1]} columns")
     L = _lib.lib()
-    check(L.gnnrec_spmm_csr_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(y),
-                                y.stride(0) if y is not None else d, d, epi, ptr(self_rows),
-                                self_rows.stride(0) if self_rows is not None else d, ptr(acc),
-                                acc.stride(0) if acc is not None else d, float(acc_div),
-                                _lib.stream_of(adj.device)), "gnnrec_spmm_csr_f32")
+    ht = SPMM_HEAVY_THRESHOLD if heavy_threshold is None else heavy_threshold
+    check(L.gnnrec_spmm_csr_split_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(y),
+                                      y.stride(0) if y is not None else d, d, epi, ptr(self_rows),
+                                      self_rows.stride(0) if self_rows is not None else d,
+                                      ptr(acc), acc.stride(0) if acc is not None else d,
+                                      float(acc_div), *_heavy_args(adj, x, ht),
+                                      _lib.stream_of(adj.device)), "gnnrec_spmm_csr_split_f32")
 
 
 def spmm_forward(adj: CsrGraph, x: torch.Tensor) -> torch.Tensor:
@@ -65,7 +86,8 @@ def spmm_forward(adj: CsrGraph, x: torch.Tensor) -> torch.Tensor:
 
 
 def lightgcn_forward(adj: CsrGraph, x0: torch.Tensor, n_layers: int,
-                     return_layers: bool = False) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+                     return_layers: bool = False, heavy_threshold: Optional[int] = None
+                     ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """out = mean(x0, A x0, ..., A^K x0); optionally the K hop outputs [K, N, d]."""
     x0 = x0.contiguous()
     _require_device(adj, x0)
@@ -82,9 +104,11 @@ def lightgcn_forward(adj: CsrGraph, x0: torch.Tensor, n_layers: int,
     elif n_layers == 1:
         work0 = work1 = torch.empty_like(x0)
     L = _lib.lib()
-    check(L.gnnrec_lightgcn_f32(*_csr_args(adj), ptr(x0), d, int(n_layers), ptr(work0),
-                                ptr(work1), ptr(layers), ptr(out), d, _lib.stream_of(adj.device)),
-          "gnnrec_lightgcn_f32")
+    ht = SPMM_HEAVY_THRESHOLD if heavy_threshold is None else heavy_threshold
+    check(L.gnnrec_lightgcn_split_f32(*_csr_args(adj), ptr(x0), d, int(n_layers), ptr(work0),
+                                      ptr(work1), ptr(layers), ptr(out), d,
+                                      *_heavy_args(adj, x0, ht), _lib.stream_of(adj.device)),
+          "gnnrec_lightgcn_split_f32")
     return out, layers
 
 

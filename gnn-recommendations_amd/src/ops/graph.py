@@ -328,9 +328,24 @@ class CsrGraph:
         return g.to(self.device)
 
     def row_slice(self, r0: int, r1: int) -> "CsrGraph":
-        """View of rows [r0, r1) (row_ptr keeps absolute offsets: no copy of col/val)."""
-        return CsrGraph(self.row_ptr[r0:r1 + 1], self.col, self.val, (r1 - r0, self.shape[1]),
-                        self.n_users, self.n_items, False, self.shard_info)
+        """View of rows [r0, r1) (row_ptr keeps absolute offsets: no copy of col/val). Cached,
+        so per-view plans (heavy rows) are computed once."""
+        key = ("slice", r0, r1)
+        if key not in self._plans:
+            self._plans[key] = CsrGraph(self.row_ptr[r0:r1 + 1], self.col, self.val,
+                                        (r1 - r0, self.shape[1]), self.n_users, self.n_items,
+                                        False, self.shard_info)
+        return self._plans[key]
+
+    def heavy_rows(self, threshold: int) -> Optional[torch.Tensor]:
+        """int64 ids of the rows with more than `threshold` neighbours on this device, or None
+        (cached): the SpMM's workgroup-per-row bucket."""
+        key = ("heavy_rows", threshold)
+        if key not in self._plans:
+            deg = self.row_ptr[1:] - self.row_ptr[:-1]
+            rows = torch.nonzero(deg > threshold).flatten().to(torch.int64).contiguous()
+            self._plans[key] = rows if rows.numel() else None
+        return self._plans[key]
 
     def heavy_plan(self, threshold: int, seg_len: int):
         """Degree buckets for the skew-tolerant kernels (cached): rows with more than

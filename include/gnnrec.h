@@ -82,6 +82,27 @@ int gnnrec_lightgcn_f32(const int64_t* row_ptr, const int32_t* col, const float*
                         float* work0, float* work1, float* layers, float* out, int64_t ld_out,
                         gnnrec_stream_t stream);
 
+/* Heavy-row split of the two calls above (same results, bit for bit). Rows with more than
+ * heavy_threshold neighbours are skipped by the row-parallel kernel and run instead one
+ * workgroup per row (1024 threads, 136 KB LDS): the whole workgroup gathers the next 64 KB of
+ * neighbour rows into an LDS double buffer while one wave runs the row's ordered fmaf chain.
+ * heavy_rows (device int64 [n_heavy]) must list exactly the rows longer than heavy_threshold;
+ * heavy_threshold == 0 disables the split. Needs d % 4 == 0, d <= 256, 16-B aligned x with
+ * ldx % 4 == 0 when enabled. Power-law operands (popular items) stop being latency-bound on
+ * their longest rows. */
+int gnnrec_spmm_csr_split_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
+                              int64_t n_rows, const float* x, int64_t ldx, float* y, int64_t ldy,
+                              int32_t d, int32_t epi, const float* self, int64_t ld_self,
+                              float* acc, int64_t ld_acc, float acc_div,
+                              const int64_t* heavy_rows, int64_t n_heavy,
+                              int64_t heavy_threshold, gnnrec_stream_t stream);
+
+int gnnrec_lightgcn_split_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
+                              int64_t n_rows, const float* x0, int32_t d, int32_t n_layers,
+                              float* work0, float* work1, float* layers, float* out,
+                              int64_t ld_out, const int64_t* heavy_rows, int64_t n_heavy,
+                              int64_t heavy_threshold, gnnrec_stream_t stream);
+
 /* ---- a7: Group-and-Shuffle transform -----------------------------------------------
  * Replaces GroupShuffleLayer.forward (orthogonal_bundle/group_shuffle_layer.py:88-94):
  *   y = (x @ blockdiag(W_0..W_{d/bs-1}))[:, perm]

@@ -210,3 +210,62 @@ def test_dense_layer_vs_oracle(cuda, d, fused):
                   fused=fused)
     np.testing.assert_allclose(acc.cpu().numpy(), (acc_before + 0.5 * y).cpu().numpy(), rtol=0,
                                atol=1e-6)
+
+
+# ---- heavy-row split (workgroup-per-row, LDS double-buffered gather) ----------------------
+def powerlaw_graph(seed, device, n_users=400, n_items=6000, n_pairs=30000):
+    rng = np.random.default_rng(seed)
+    u = rng.integers(0, n_users, n_pairs)
+    i = np.minimum(rng.zipf(1.2, n_pairs) - 1, n_items - 1)   # item rows up to ~1e4 long
+    u = np.concatenate([u, np.zeros(5000, np.int64), np.full(4097, 1)])   # user rows 0/1 long
+    i = np.concatenate([i, rng.permutation(n_items)[:5000], rng.permutation(n_items)[:4097]])
+    g = CsrGraph.from_interactions(u, i, n_users, n_items)
+    return g.to(device), (g.row_ptr.numpy(), g.col.numpy(), g.val.numpy())
+
+
+@pytest.mark.parametrize("d", [4, 12, 16, 32, 64, 100, 128, 256])
+def test_spmm_heavy_split_bit_exact(cuda, d):
+    g, (rp, col, val) = powerlaw_graph(d, cuda)
+    deg = np.diff(rp)
+    assert (deg > 1024).sum() >= 3 and deg.max() > 4096
+    x = torch.randn(g.shape[0], d, generator=torch.Generator().manual_seed(d)) * 0.1
+    ref = bits(oracle.spmm(rp, col, val, x.numpy()))
+    xd = x.to(cuda)
+    for thr in (1024, 256):
+        y = torch.full((g.shape[0], d), float("nan"), device=cuda)
+        F.spmm_into(g, xd, y, heavy_threshold=thr)
+        np.testing.assert_array_equal(bits(y.cpu().numpy()), ref)
+    y0 = torch.empty_like(xd)
+    F.spmm_into(g, xd, y0, heavy_threshold=0)             # no split: the same bits
+    np.testing.assert_array_equal(bits(y0.cpu().numpy()), ref)
+
+
+def test_spmm_heavy_split_epilogues_and_strides(cuda):
+    g, (rp, col, val) = powerlaw_graph(7, cuda)
+    n = g.shape[0]
+    big = torch.randn(n, 80, device=cuda) * 0.1
+    x = big[:, 8:72]
+    xs = x.contiguous().cpu().numpy()
+    yr = oracle.spmm(rp, col, val, xs)
+    acc = torch.empty(n, 64, device=cuda)
+    y = torch.full((n, 96), 7.0, device=cuda)
+    F.spmm_into(g, x, y[:, 16:80], epi=_lib.EPI_ACC_INIT, self_rows=x, acc=acc, heavy_threshold=512)
+    np.testing.assert_array_equal(bits(y[:, 16:80].cpu().numpy()), bits(yr))
+    np.testing.assert_array_equal(bits(acc.cpu().numpy()), bits(xs + yr))
+    acc2 = acc.clone()
+    F.spmm_into(g, x, None, epi=_lib.EPI_ACC_ADD | _lib.EPI_ACC_DIV | _lib.EPI_NO_Y, acc=acc2,
+                acc_div=3.0, heavy_threshold=512)
+    np.testing.assert_array_equal(bits(acc2.cpu().numpy()),
+                                  bits((acc.cpu().numpy() + yr) / np.float32(3.0)))
+
+
+@pytest.mark.parametrize("K,d", [(3, 64), (2, 128), (3, 32)])
+def test_lightgcn_heavy_split_bit_exact(cuda, K, d):
+    g, (rp, col, val) = powerlaw_graph(K + d, cuda)
+    x = torch.randn(g.shape[0], d, generator=torch.Generator().manual_seed(3)) * 0.1
+    out, layers = F.lightgcn_forward(g, x.to(cuda), K, return_layers=True)
+    out0, _ = F.lightgcn_forward(g, x.to(cuda), K, heavy_threshold=0)
+    ref = oracle.lightgcn(rp, col, val, x.numpy(), K)
+    np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(ref))
+    np.testing.assert_array_equal(bits(out0.cpu().numpy()), bits(ref))
+    assert g.heavy_rows(1024) is not None
