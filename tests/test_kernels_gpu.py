@@ -213,10 +213,10 @@ def test_dense_layer_vs_oracle(cuda, d, fused):
 
 
 # ---- heavy-row split (workgroup-per-row, LDS double-buffered gather) ----------------------
-def powerlaw_graph(seed, device, n_users=400, n_items=6000, n_pairs=30000):
+def powerlaw_graph(seed, device, n_users=20000, n_items=6000, n_pairs=60000):
     rng = np.random.default_rng(seed)
     u = rng.integers(0, n_users, n_pairs)
-    i = np.minimum(rng.zipf(1.2, n_pairs) - 1, n_items - 1)   # item rows up to ~1e4 long
+    i = np.minimum(rng.zipf(1.1, n_pairs) - 1, n_items - 1)   # item rows up to ~1e4 long
     u = np.concatenate([u, np.zeros(5000, np.int64), np.full(4097, 1)])   # user rows 0/1 long
     i = np.concatenate([i, rng.permutation(n_items)[:5000], rng.permutation(n_items)[:4097]])
     g = CsrGraph.from_interactions(u, i, n_users, n_items)
