@@ -129,7 +129,25 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
       const float* xb = buf + (c & 1) * kHeavyChunkFloats;
       const float* vb = vbuf + (c & 1) * 4096;
       const int m = (int)min<int64_t>(chk, end - (beg + c * chk));
-      for (int j = 0; j < m; ++j) {
+      // 16 neighbours per step: all LDS reads issued before the ordered FMAs
+      int j = 0;
+      for (; j + 16 <= m; j += 16) {
+        float vv[16], xx[16][F];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+          vv[t] = vb[j + t];
+#pragma unroll
+          for (int f = 0; f < F; ++f) {
+            const int col_f = lane + 64 * f;
+            xx[t][f] = col_f < d ? xb[(j + t) * d + col_f] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+#pragma unroll
+          for (int f = 0; f < F; ++f) a[f] = __builtin_fmaf(vv[t], xx[t][f], a[f]);
+      }
+      for (; j < m; ++j) {
         const float v = vb[j];
 #pragma unroll
         for (int f = 0; f < F; ++f) {
