@@ -56,108 +56,144 @@ __global__ __launch_bounds__(kBlock) void spmm_generic_kernel(
 
 // Heavy rows (one workgroup of kHeavyThreads per listed row). The bit-exact order makes a row
 // one sequential fmaf chain per feature, so a long row cannot be split; what is parallelised
-// is the GATHER: all 16 waves fetch the next chunk of neighbour rows (kHeavyChunkFloats fp32,
-// 64 KB: 4 float4 per thread in flight) into one half of an LDS double buffer while wave 0
-// runs the chain over the other half. A 3 000-neighbour row costs ~12 such rounds instead of
-// ~375 dependent 8-neighbour steps of one wave in spmm_vec_kernel.
-constexpr int kHeavyThreads = 1024;
-constexpr int kHeavyChunkFloats = 16384;                 // per buffer
+// is the GATHER: all 8 waves fetch neighbour rows into an LDS double buffer (a chunk =
+// kHeavyChunkFloats fp32 = 64 KB of neighbour rows) while wave 0 runs the chain over the
+// other half. Loads are software-pipelined two chunks deep: in round c the workgroup issues
+// the (col, val) loads of chunk c+3 and the row gathers of chunk c+2 (whose columns arrived in
+// round c-1), wave 0 consumes chunk c from LDS, and chunk c+1 (gathered since round c-1) is
+// parked in the free LDS half. A row gather therefore has two rounds to land and never waits
+// behind its own column load.
+constexpr int kHeavyThreads = 512;
+constexpr int kHeavyChunkFloats = 16384;                 // per LDS buffer
 constexpr int kHeavyPieces = kHeavyChunkFloats / 4 / kHeavyThreads;  // float4 per thread
-constexpr size_t kHeavyLds = 2 * kHeavyChunkFloats * sizeof(float) + 2 * 4096 * sizeof(float);
+constexpr int kHeavyMinD = 16;
+constexpr int kHeavyMaxChunkRows = kHeavyChunkFloats / kHeavyMinD;   // 1024
+constexpr int kHeavyVals = kHeavyMaxChunkRows / kHeavyThreads;       // vals per thread
+constexpr size_t kHeavyLds = 2 * kHeavyChunkFloats * sizeof(float) +
+                             2 * kHeavyMaxChunkRows * sizeof(float);
+
+struct HeavyCols {        // (col, val) of one chunk, as this thread needs them
+  int c[kHeavyPieces];
+  float v[kHeavyVals];
+};
+struct HeavyStage {       // one chunk's gathered rows + vals in flight in registers
+  float4 x[kHeavyPieces];
+  float v[kHeavyVals];
+};
 
 template <int F>  // features per consumer lane: d <= 64 * F
 __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
     Csr A, const int64_t* __restrict__ rows, const float* __restrict__ x, int64_t ldx,
     float* __restrict__ y, int64_t ldy, int d, int epi, const float* __restrict__ self,
     int64_t ld_self, float* __restrict__ acc, int64_t ld_acc, float acc_div) {
+  constexpr int STEP = 16 / F;                           // neighbours per consumer step
   extern __shared__ float4 heavy_lds4[];
   float* buf = reinterpret_cast<float*>(heavy_lds4);     // [2][kHeavyChunkFloats]
-  float* vbuf = buf + 2 * kHeavyChunkFloats;             // [2][4096]
+  float* vbuf = buf + 2 * kHeavyChunkFloats;             // [2][kHeavyMaxChunkRows]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t r = rows[blockIdx.x];
   const int64_t beg = A.row_ptr[r], end = A.row_ptr[r + 1];
   const int q4 = d >> 2;                                 // float4 per neighbour row
   const int chk = kHeavyChunkFloats / d;                 // neighbours per chunk (<= 4096)
-  const int64_t n = end - beg;
-  const int64_t n_chunks = (n + chk - 1) / chk;
-  float4 stage[kHeavyPieces];
-  float vstage[4];
+  const int64_t n_chunks = (end - beg + chk - 1) / chk;
 
-  auto load = [&](int64_t c) {                           // issue the loads of chunk c
+  auto load_cols = [&](int64_t c, HeavyCols& hc) {
     const int64_t k0 = beg + c * chk;
 #pragma unroll
     for (int i = 0; i < kHeavyPieces; ++i) {
-      const int p = tid + i * kHeavyThreads, j = p / q4, part = p - j * q4;
+      const int j = (tid + i * kHeavyThreads) / q4;
       const int64_t k = k0 + j;
-      stage[i] = (j < chk && k < end)
-                     ? *reinterpret_cast<const float4*>(x + (int64_t)A.col[k] * ldx + 4 * part)
-                     : make_float4(0.f, 0.f, 0.f, 0.f);
+      hc.c[i] = (c < n_chunks && j < chk && k < end) ? A.col[k] : -1;
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kHeavyVals; ++i) {
       const int j = tid + i * kHeavyThreads;
       const int64_t k = k0 + j;
-      vstage[i] = (j < chk && k < end) ? A.val[k] : 0.f;
+      hc.v[i] = (c < n_chunks && j < chk && k < end) ? A.val[k] : 0.f;
     }
   };
-  auto store = [&](int b) {                              // park them in buffer b
+  auto gather = [&](const HeavyCols& hc, HeavyStage& st) {
+#pragma unroll
+    for (int i = 0; i < kHeavyPieces; ++i) {
+      const int p = tid + i * kHeavyThreads, part = p - (p / q4) * q4;
+      st.x[i] = hc.c[i] >= 0
+                    ? *reinterpret_cast<const float4*>(x + (int64_t)hc.c[i] * ldx + 4 * part)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < kHeavyVals; ++i) st.v[i] = hc.v[i];
+  };
+  auto park = [&](const HeavyStage& st, int b) {
     float4* dst = reinterpret_cast<float4*>(buf + b * kHeavyChunkFloats);
 #pragma unroll
     for (int i = 0; i < kHeavyPieces; ++i) {
       const int p = tid + i * kHeavyThreads;
-      if (p / q4 < chk) dst[p] = stage[i];
+      if (p / q4 < chk) dst[p] = st.x[i];
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < kHeavyVals; ++i) {
       const int j = tid + i * kHeavyThreads;
-      if (j < chk) vbuf[b * 4096 + j] = vstage[i];
+      if (j < chk) vbuf[b * kHeavyMaxChunkRows + j] = st.v[i];
     }
   };
 
   float a[F];
 #pragma unroll
   for (int f = 0; f < F; ++f) a[f] = 0.f;
-  if (n_chunks > 0) {
-    load(0);
-    store(0);
-  }
-  __syncthreads();
-  for (int64_t c = 0; c < n_chunks; ++c) {
-    const bool more = c + 1 < n_chunks;
-    if (more) load(c + 1);
-    if (wave == 0) {
-      const float* xb = buf + (c & 1) * kHeavyChunkFloats;
-      const float* vb = vbuf + (c & 1) * 4096;
-      const int m = (int)min<int64_t>(chk, end - (beg + c * chk));
-      // 16 neighbours per step: all LDS reads issued before the ordered FMAs
-      int j = 0;
-      for (; j + 16 <= m; j += 16) {
-        float vv[16], xx[16][F];
+  auto consume = [&](int64_t c) {
+    const float* xb = buf + (c & 1) * kHeavyChunkFloats;
+    const float* vb = vbuf + (c & 1) * kHeavyMaxChunkRows;
+    const int m = (int)min<int64_t>(chk, end - (beg + c * chk));
+    int j = 0;
+    for (; j + STEP <= m; j += STEP) {  // all LDS reads of a step before its ordered FMAs
+      float vv[STEP], xx[STEP][F];
 #pragma unroll
-        for (int t = 0; t < 16; ++t) {
-          vv[t] = vb[j + t];
-#pragma unroll
-          for (int f = 0; f < F; ++f) {
-            const int col_f = lane + 64 * f;
-            xx[t][f] = col_f < d ? xb[(j + t) * d + col_f] : 0.f;
-          }
-        }
-#pragma unroll
-        for (int t = 0; t < 16; ++t)
-#pragma unroll
-          for (int f = 0; f < F; ++f) a[f] = __builtin_fmaf(vv[t], xx[t][f], a[f]);
-      }
-      for (; j < m; ++j) {
-        const float v = vb[j];
+      for (int t = 0; t < STEP; ++t) {
+        vv[t] = vb[j + t];
 #pragma unroll
         for (int f = 0; f < F; ++f) {
           const int col_f = lane + 64 * f;
-          if (col_f < d) a[f] = __builtin_fmaf(v, xb[j * d + col_f], a[f]);
+          xx[t][f] = col_f < d ? xb[(j + t) * d + col_f] : 0.f;
         }
       }
+#pragma unroll
+      for (int t = 0; t < STEP; ++t)
+#pragma unroll
+        for (int f = 0; f < F; ++f) a[f] = __builtin_fmaf(vv[t], xx[t][f], a[f]);
     }
-    if (more) store((c + 1) & 1);
+    for (; j < m; ++j) {
+      const float v = vb[j];
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        const int col_f = lane + 64 * f;
+        if (col_f < d) a[f] = __builtin_fmaf(v, xb[j * d + col_f], a[f]);
+      }
+    }
+  };
+
+  // prologue: chunk 0 parked, chunk 1 gathering, columns of chunk 2 loading
+  HeavyCols ca, cb;
+  HeavyStage sa, sb;
+  load_cols(0, ca);
+  gather(ca, sa);
+  load_cols(1, cb);
+  park(sa, 0);
+  gather(cb, sb);
+  load_cols(2, ca);
+  __syncthreads();
+  // round c: columns of c+3 -> gather of c+2 -> consume c -> park c+1 -> barrier.
+  // Unrolled by two so the register sets alternate statically.
+  auto round = [&](int64_t c, HeavyCols& cols_c2, HeavyCols& cols_c3, HeavyStage& st_c1,
+                   HeavyStage& st_c2) {
+    load_cols(c + 3, cols_c3);               // issued first: next round waits on these alone
+    gather(cols_c2, st_c2);                  // columns of c+2 arrived during round c-1
+    if (wave == 0) consume(c);
+    if (c + 1 < n_chunks) park(st_c1, (int)((c + 1) & 1));
     __syncthreads();
+  };
+  for (int64_t c = 0; c < n_chunks; c += 2) {
+    round(c, ca, cb, sb, sa);                // c+1 in sb, c+2 -> sa, cols c+2 in ca, c+3 -> cb
+    if (c + 1 < n_chunks) round(c + 1, cb, ca, sa, sb);
   }
   if (wave != 0) return;
 #pragma unroll
@@ -258,9 +294,9 @@ extern "C" int gnnrec_spmm_csr_split_f32(const int64_t* row_ptr, const int32_t* 
   const bool split = heavy_threshold > 0;
   if (split) {
     GNNREC_REQUIRE(n_heavy == 0 || heavy_rows, "spmm: null heavy_rows");
-    GNNREC_REQUIRE(d % 4 == 0 && d <= 256 && aligned16(x) && !(ldx & 3),
-                   "spmm: the heavy-row path needs d %% 4 == 0, d <= 256 and a 16-B aligned x "
-                   "with ldx %% 4 == 0");
+    GNNREC_REQUIRE(d % 4 == 0 && d >= kHeavyMinD && d <= 256 && aligned16(x) && !(ldx & 3),
+                   "spmm: the heavy-row path needs d %% 4 == 0, 16 <= d <= 256 and a 16-B "
+                   "aligned x with ldx %% 4 == 0");
   }
   const Csr A{row_ptr, col, val, n_rows};
   hipStream_t s = as_hip(stream);

@@ -49,7 +49,7 @@ SPMM_HEAVY_THRESHOLD = 1024
 def _heavy_args(adj: CsrGraph, x: torch.Tensor, heavy_threshold: int):
     """(heavy_rows ptr, n_heavy, threshold) for the split launch, or the no-split triple."""
     d = x.shape[1]
-    if (heavy_threshold <= 0 or d % 4 or d > 256 or x.stride(0) % 4
+    if (heavy_threshold <= 0 or d % 4 or d < 16 or d > 256 or x.stride(0) % 4
             or x.data_ptr() % 16):
         return None, 0, 0
     rows = adj.heavy_rows(heavy_threshold)

@@ -84,10 +84,10 @@ int gnnrec_lightgcn_f32(const int64_t* row_ptr, const int32_t* col, const float*
 
 /* Heavy-row split of the two calls above (same results, bit for bit). Rows with more than
  * heavy_threshold neighbours are skipped by the row-parallel kernel and run instead one
- * workgroup per row (1024 threads, 136 KB LDS): the whole workgroup gathers the next 64 KB of
+ * workgroup per row (512 threads, 136 KB LDS): the whole workgroup gathers the next 64 KB of
  * neighbour rows into an LDS double buffer while one wave runs the row's ordered fmaf chain.
  * heavy_rows (device int64 [n_heavy]) must list exactly the rows longer than heavy_threshold;
- * heavy_threshold == 0 disables the split. Needs d % 4 == 0, d <= 256, 16-B aligned x with
+ * heavy_threshold == 0 disables the split. Needs d % 4 == 0, 16 <= d <= 256, 16-B aligned x with
  * ldx % 4 == 0 when enabled. Power-law operands (popular items) stop being latency-bound on
  * their longest rows. */
 int gnnrec_spmm_csr_split_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
