@@ -81,11 +81,14 @@ struct HeavyStage {       // one chunk's gathered rows + vals in flight in regis
   float v[kHeavyVals];
 };
 
-template <int F>  // features per consumer lane: d <= 64 * F
+// F: features per consumer lane (d <= 64 F); DC: d as a compile-time constant (0 = runtime d),
+// which turns the consumer's LDS addressing into immediate offsets.
+template <int F, int DC>
 __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
     Csr A, const int64_t* __restrict__ rows, const float* __restrict__ x, int64_t ldx,
-    float* __restrict__ y, int64_t ldy, int d, int epi, const float* __restrict__ self,
+    float* __restrict__ y, int64_t ldy, int d_rt, int epi, const float* __restrict__ self,
     int64_t ld_self, float* __restrict__ acc, int64_t ld_acc, float acc_div) {
+  const int d = DC ? DC : d_rt;
   constexpr int STEP = 16 / F;                           // neighbours per consumer step
   extern __shared__ float4 heavy_lds4[];
   float* buf = reinterpret_cast<float*>(heavy_lds4);     // [2][kHeavyChunkFloats]
@@ -140,6 +143,11 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
   float a[F];
 #pragma unroll
   for (int f = 0; f < F; ++f) a[f] = 0.f;
+  // consumer lanes: feature lane + 64 f, clamped into the row so no lane is masked off (a
+  // clamped lane computes a duplicate it never stores) and the LDS reads need no branches
+  int fcol[F];
+#pragma unroll
+  for (int f = 0; f < F; ++f) fcol[f] = min(lane + 64 * f, d - 1);
   auto consume = [&](int64_t c) {
     const float* xb = buf + (c & 1) * kHeavyChunkFloats;
     const float* vb = vbuf + (c & 1) * kHeavyMaxChunkRows;
@@ -148,14 +156,14 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
     for (; j + STEP <= m; j += STEP) {  // all LDS reads of a step before its ordered FMAs
       float vv[STEP], xx[STEP][F];
 #pragma unroll
-      for (int t = 0; t < STEP; ++t) {
-        vv[t] = vb[j + t];
-#pragma unroll
-        for (int f = 0; f < F; ++f) {
-          const int col_f = lane + 64 * f;
-          xx[t][f] = col_f < d ? xb[(j + t) * d + col_f] : 0.f;
-        }
+      for (int t = 0; t < STEP; t += 4) {   // vals: one 16-B broadcast read per 4 neighbours
+        const float4 v4 = *reinterpret_cast<const float4*>(vb + j + t);
+        vv[t] = v4.x; vv[t + 1] = v4.y; vv[t + 2] = v4.z; vv[t + 3] = v4.w;
       }
+#pragma unroll
+      for (int t = 0; t < STEP; ++t)
+#pragma unroll
+        for (int f = 0; f < F; ++f) xx[t][f] = xb[(j + t) * d + fcol[f]];
 #pragma unroll
       for (int t = 0; t < STEP; ++t)
 #pragma unroll
@@ -164,10 +172,7 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
     for (; j < m; ++j) {
       const float v = vb[j];
 #pragma unroll
-      for (int f = 0; f < F; ++f) {
-        const int col_f = lane + 64 * f;
-        if (col_f < d) a[f] = __builtin_fmaf(v, xb[j * d + col_f], a[f]);
-      }
+      for (int f = 0; f < F; ++f) a[f] = __builtin_fmaf(v, xb[j * d + fcol[f]], a[f]);
     }
   };
 
@@ -319,15 +324,20 @@ extern "C" int gnnrec_spmm_csr_split_f32(const int64_t* row_ptr, const int32_t* 
   if (split && n_heavy > 0) {
     GNNREC_REQUIRE(n_heavy < (int64_t)INT32_MAX, "spmm: too many heavy rows");
     const dim3 grid((unsigned)n_heavy), block(kHeavyThreads);
-    if (d <= 64)
-      hipLaunchKernelGGL(spmm_heavy_kernel<1>, grid, block, kHeavyLds, s, A, heavy_rows, x, ldx, y,
-                         ldy, d, epi, self, ld_self, acc, ld_acc, acc_div);
-    else if (d <= 128)
-      hipLaunchKernelGGL(spmm_heavy_kernel<2>, grid, block, kHeavyLds, s, A, heavy_rows, x, ldx, y,
-                         ldy, d, epi, self, ld_self, acc, ld_acc, acc_div);
-    else
-      hipLaunchKernelGGL(spmm_heavy_kernel<4>, grid, block, kHeavyLds, s, A, heavy_rows, x, ldx, y,
-                         ldy, d, epi, self, ld_self, acc, ld_acc, acc_div);
+#define GNNREC_HEAVY(F, DC)                                                                      \
+  hipLaunchKernelGGL((spmm_heavy_kernel<F, DC>), grid, block, kHeavyLds, s, A, heavy_rows, x, ldx, \
+                     y, ldy, d, epi, self, ld_self, acc, ld_acc, acc_div)
+    switch (d) {
+      case 32: GNNREC_HEAVY(1, 32); break;
+      case 64: GNNREC_HEAVY(1, 64); break;
+      case 128: GNNREC_HEAVY(2, 128); break;
+      case 256: GNNREC_HEAVY(4, 256); break;
+      default:
+        if (d <= 64) GNNREC_HEAVY(1, 0);
+        else if (d <= 128) GNNREC_HEAVY(2, 0);
+        else GNNREC_HEAVY(4, 0);
+    }
+#undef GNNREC_HEAVY
     return check_launch("spmm_heavy");
   }
   return GNNREC_OK;
