@@ -58,11 +58,11 @@ __global__ __launch_bounds__(kBlock) void spmm_generic_kernel(
 // one sequential fmaf chain per feature, so a long row cannot be split; what is parallelised
 // is the GATHER: all 8 waves fetch neighbour rows into an LDS double buffer (a chunk =
 // kHeavyChunkFloats fp32 = 64 KB of neighbour rows) while wave 0 runs the chain over the
-// other half. Loads are software-pipelined two chunks deep: in round c the workgroup issues
-// the (col, val) loads of chunk c+3 and the row gathers of chunk c+2 (whose columns arrived in
-// round c-1), wave 0 consumes chunk c from LDS, and chunk c+1 (gathered since round c-1) is
-// parked in the free LDS half. A row gather therefore has two rounds to land and never waits
-// behind its own column load.
+// other half. Loads are software-pipelined: in round c the workgroup issues the row gathers
+// of chunk c+2 (whose columns arrived in round c-1) and the (col, val) loads of chunk c+3,
+// wave 0 consumes chunk c from LDS, and chunk c+1 (gathered in round c-1) is parked in the
+// free LDS half. A row gather never waits behind its own column load, and every load has the
+// consumer's whole round to land.
 constexpr int kHeavyThreads = 512;
 constexpr int kHeavyChunkFloats = 16384;                 // per LDS buffer
 constexpr int kHeavyPieces = kHeavyChunkFloats / 4 / kHeavyThreads;  // float4 per thread
@@ -190,8 +190,8 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
   // Unrolled by two so the register sets alternate statically.
   auto round = [&](int64_t c, HeavyCols& cols_c2, HeavyCols& cols_c3, HeavyStage& st_c1,
                    HeavyStage& st_c2) {
-    load_cols(c + 3, cols_c3);               // issued first: next round waits on these alone
     gather(cols_c2, st_c2);                  // columns of c+2 arrived during round c-1
+    load_cols(c + 3, cols_c3);
     if (wave == 0) consume(c);
     if (c + 1 < n_chunks) park(st_c1, (int)((c + 1) & 1));
     __syncthreads();

@@ -128,8 +128,8 @@ __global__ __launch_bounds__(kHeavyThreads) void xheavy(
   // Unrolled by two so the register sets alternate statically.
   auto round = [&](int64_t c, HeavyCols& cols_c2, HeavyCols& cols_c3, HeavyStage& st_c1,
                    HeavyStage& st_c2) {
-    if (MODE != 2) load_cols(c + 3, cols_c3);               // issued first: next round waits on these alone
     if (MODE != 2) gather(cols_c2, st_c2);                  // columns of c+2 arrived during round c-1
+    if (MODE != 2) load_cols(c + 3, cols_c3);
     if (wave == 0 && MODE != 1) consume(c);
     if (MODE != 3 && c + 1 < n_chunks) park(st_c1, (int)((c + 1) & 1));
     __syncthreads();
