@@ -148,28 +148,53 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
   int fcol[F];
 #pragma unroll
   for (int f = 0; f < F; ++f) fcol[f] = min(lane + 64 * f, d - 1);
+  // The chain is latency-bound (one dependent fmaf per neighbour), so the LDS reads of step
+  // s+1 are issued before the FMAs of step s (two register sets, unrolled by two).
+  struct Step {
+    float v[STEP];
+    float x[STEP][F];
+  };
+  auto fetch = [&](const float* xb, const float* vb, int j, Step& st) {
+#pragma unroll
+    for (int t = 0; t < STEP; t += 4) {   // vals: one 16-B broadcast read per 4 neighbours
+      const float4 v4 = *reinterpret_cast<const float4*>(vb + j + t);
+      st.v[t] = v4.x; st.v[t + 1] = v4.y; st.v[t + 2] = v4.z; st.v[t + 3] = v4.w;
+    }
+#pragma unroll
+    for (int t = 0; t < STEP; ++t)
+#pragma unroll
+      for (int f = 0; f < F; ++f) st.x[t][f] = xb[(j + t) * d + fcol[f]];
+  };
+  auto apply = [&](const Step& st) {
+#pragma unroll
+    for (int t = 0; t < STEP; ++t)
+#pragma unroll
+      for (int f = 0; f < F; ++f) a[f] = __builtin_fmaf(st.v[t], st.x[t][f], a[f]);
+  };
   auto consume = [&](int64_t c) {
     const float* xb = buf + (c & 1) * kHeavyChunkFloats;
     const float* vb = vbuf + (c & 1) * kHeavyMaxChunkRows;
     const int m = (int)min<int64_t>(chk, end - (beg + c * chk));
-    int j = 0;
-    for (; j + STEP <= m; j += STEP) {  // all LDS reads of a step before its ordered FMAs
-      float vv[STEP], xx[STEP][F];
-#pragma unroll
-      for (int t = 0; t < STEP; t += 4) {   // vals: one 16-B broadcast read per 4 neighbours
-        const float4 v4 = *reinterpret_cast<const float4*>(vb + j + t);
-        vv[t] = v4.x; vv[t + 1] = v4.y; vv[t + 2] = v4.z; vv[t + 3] = v4.w;
+    const int steps = m / STEP;
+    if constexpr (DC != 0) {
+      Step s0, s1;
+      if (steps > 0) fetch(xb, vb, 0, s0);
+      int q = 0;
+      for (; q + 2 <= steps; q += 2) {
+        fetch(xb, vb, (q + 1) * STEP, s1);
+        apply(s0);
+        if (q + 2 < steps) fetch(xb, vb, (q + 2) * STEP, s0);
+        apply(s1);
       }
-#pragma unroll
-      for (int t = 0; t < STEP; ++t)
-#pragma unroll
-        for (int f = 0; f < F; ++f) xx[t][f] = xb[(j + t) * d + fcol[f]];
-#pragma unroll
-      for (int t = 0; t < STEP; ++t)
-#pragma unroll
-        for (int f = 0; f < F; ++f) a[f] = __builtin_fmaf(vv[t], xx[t][f], a[f]);
+      if (q < steps) apply(s0);
+    } else {  // runtime d: no immediate offsets, one register set (no spills)
+      for (int q = 0; q < steps; ++q) {
+        Step s0;
+        fetch(xb, vb, q * STEP, s0);
+        apply(s0);
+      }
     }
-    for (; j < m; ++j) {
+    for (int j = steps * STEP; j < m; ++j) {
       const float v = vb[j];
 #pragma unroll
       for (int f = 0; f < F; ++f) a[f] = __builtin_fmaf(v, xb[j * d + fcol[f]], a[f]);
