@@ -41,9 +41,10 @@ def _csr_args(adj: CsrGraph):
 
 
 # Rows longer than this go to the workgroup-per-row kernel (bit-exact, LDS-pipelined gather);
-# 0 disables the split. The light kernel's per-row latency grows with the row, the heavy
-# kernel's is ~1.5 us per 64 KB of neighbour rows.
-SPMM_HEAVY_THRESHOLD = 1024
+# 0 disables the split. Sweep (tools/exp_heavy.py, profiles/r01/heavy_split_sweep.jsonl):
+# ML-1M-shaped LightGCN K=3 0.90 ms unsplit -> 0.30 ms at 128, power-law 2M x 2M 123 -> 29 ms;
+# uniform graphs (G100M, max degree ~150) have no rows above it.
+SPMM_HEAVY_THRESHOLD = 256
 
 
 def _heavy_args(adj: CsrGraph, x: torch.Tensor, heavy_threshold: int):
