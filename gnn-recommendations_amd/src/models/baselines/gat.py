@@ -2,8 +2,9 @@
 
 The reference materialises, per head and layer, a dense [N, N] score matrix masked by the
 adjacency pattern (gat.py:99-141): O(N^2) memory, infeasible beyond N ~ 2e4. On a ROCm
-operand each layer here is one dense projection h = x W^T for all heads (a plain library
-GEMM) plus ONE native sparse kernel that does the edge softmax and the aggregation for all
+operand each layer here is one dense projection for all heads (a plain library GEMM whose
+weight also carries a_self^T W_h and a_neigh^T W_h, so h and both attention halves come out
+of it together) plus ONE native sparse kernel that does the edge softmax and the aggregation for all
 heads over the CSR pattern, with the head mean (last layer), F.elu and the layer mean
 fused into its epilogue (gnnrec_gat_aggregate_f32). Parameters keep the reference's names
 and creation order. Semantics difference, documented: an isolated node yields a NaN row
@@ -42,14 +43,31 @@ class GATLayer(nn.Module):
                 and self.out_dim % 4 == 0 and (not self.training or self.dropout == 0.0)
                 and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())))
 
+    def fused_weight(self) -> torch.Tensor:
+        """[H*o + 2H, in]: the stacked head projections W_h, then a_self_h^T W_h and
+        a_neigh_h^T W_h, so ONE GEMM x @ W^T yields h and both attention halves (the
+        reference computes mm(W_h x, a), gat.py:113-118: the same value reassociated).
+        Cached until a parameter changes (inference only)."""
+        from ..orthogonal_bundle.group_shuffle_layer import param_key
+        params = list(self.W.parameters()) + list(self.a_self) + list(self.a_neigh)
+        grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        key = None if grad else param_key(params)
+        if key is not None and getattr(self, "_fused_key", None) == key:
+            return self._fused_w
+        Wcat = torch.cat([w.weight for w in self.W], dim=0)               # [H*o, in]
+        ws = torch.stack([a[:, 0] @ w.weight for a, w in zip(self.a_self, self.W)])
+        wn = torch.stack([a[:, 0] @ w.weight for a, w in zip(self.a_neigh, self.W)])
+        out = torch.cat([Wcat, ws, wn], dim=0)
+        if key is not None:
+            self._fused_w, self._fused_key = out.detach(), key
+        return out
+
     def projections(self, x: torch.Tensor):
-        """h = [W_0 x | ... | W_H x] and the per-head attention halves s_self, s_neigh."""
-        Wcat = torch.cat([w.weight for w in self.W], dim=0)          # [H*o, in]
-        h = x @ Wcat.t()                                              # [N, H*o]
-        hv = h.view(-1, self.n_heads, self.out_dim)
-        a_s = torch.stack([a[:, 0] for a in self.a_self])            # [H, o]
-        a_n = torch.stack([a[:, 0] for a in self.a_neigh])
-        return h, (hv * a_s).sum(-1), (hv * a_n).sum(-1)
+        """h = [W_0 x | ... | W_H x] and the per-head attention halves s_self, s_neigh, all
+        from one GEMM (h is a strided view of its output)."""
+        ho = self.n_heads * self.out_dim
+        out = x @ self.fused_weight().t()                                  # [N, H*o + 2H]
+        return out[:, :ho], out[:, ho:ho + self.n_heads], out[:, ho + self.n_heads:]
 
     def forward(self, x: torch.Tensor, adj_matrix, *, apply_elu: bool = False, epi: int = 0,
                 self_rows=None, acc=None, acc_div: float = 1.0) -> torch.Tensor:
