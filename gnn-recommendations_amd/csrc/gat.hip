@@ -7,7 +7,10 @@
 // (flash-style rescaling), accumulating p_j * h[j] for every head at the same time.
 // Row mapping as the SpMM (gather.h): F = heads*o_dim features per row, GROUP = F/4 lanes
 // per row, 4 features (one head) per lane; a neighbour costs one F*4-byte row gather plus
-// one 4-byte score gather per lane.
+// one 4-byte score gather per lane. With head_stride = 0 every head aggregates the same
+// o_dim-wide row (the layer input x itself): the last, head-averaged layer then gathers x
+// once per neighbour instead of the 4x wider h, and W_h is applied after the aggregation
+// (sum_j a_hj W_h x_j = W_h sum_j a_hj x_j).
 // Fused epilogue: mean over heads (last layer, gat.py:149), F.elu (gat.py:283) and the
 // layer-mean accumulator (gat.py:287-288, GNNREC_EPI_* flags).
 #include <math.h>
@@ -20,6 +23,8 @@ struct GatParams {
   Csr A;
   const float* h;
   int64_t ldh;
+  int64_t head_stride;  // h[j] of head q starts at h + j*ldh + q*head_stride (o_dim: [N, H*o]
+                        // head-major; 0: every head reads the same o_dim-wide row)
   const float* s_self;
   const float* s_neigh;
   int heads, o_dim;
@@ -87,7 +92,7 @@ __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, in
 #pragma unroll
     for (int t = 0; t < kChunk; ++t) {
       const int c = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
-      xv[t] = ld4(p.h + (int64_t)c * p.ldh + 4 * gl);
+      xv[t] = ld4(p.h + (int64_t)c * p.ldh + head * p.head_stride + 4 * (gl - head * hl));
       sn[t] = p.s_neigh[(int64_t)c * p.heads + head];
     }
 #pragma unroll
@@ -190,8 +195,9 @@ __global__ __launch_bounds__(kBlock) void gat_merge_kernel(GatParams p, GatSplit
 using namespace gnnrec;
 
 extern "C" int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* col, int64_t n_rows,
-                                        const float* hfeat, int64_t ldh, const float* s_self,
-                                        const float* s_neigh, int32_t heads, int32_t o_dim,
+                                        const float* hfeat, int64_t ldh, int64_t head_stride,
+                                        const float* s_self, const float* s_neigh, int32_t heads,
+                                        int32_t o_dim,
                                         float slope, int32_t mean_heads, int32_t apply_elu,
                                         float* out, int64_t ldo, int32_t epi, const float* self,
                                         int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
@@ -201,7 +207,9 @@ extern "C" int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* c
   const int F = heads * o_dim;
   const int width = mean_heads ? o_dim : F;
   GNNREC_REQUIRE(row_ptr && col && hfeat && s_self && s_neigh, "gat: null operand");
-  GNNREC_REQUIRE(aligned16(hfeat) && !(ldh & 3) && ldh >= F, "gat: hfeat must be 16-B aligned, ld %% 4 == 0, ld >= heads*o_dim");
+  GNNREC_REQUIRE(head_stride >= 0 && !(head_stride & 3), "gat: head_stride must be >= 0 and %% 4 == 0");
+  GNNREC_REQUIRE(aligned16(hfeat) && !(ldh & 3) && ldh >= (heads - 1) * head_stride + o_dim,
+                 "gat: hfeat must be 16-B aligned, ld %% 4 == 0, ld >= (heads-1)*head_stride + o_dim");
   GNNREC_REQUIRE((epi & GNNREC_EPI_NO_Y) || (out && aligned16(out) && !(ldo & 3) && ldo >= width),
                  "gat: bad out");
   GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_INIT) || (self && aligned16(self) && !(ld_self & 3) && ld_self >= width),
@@ -209,7 +217,7 @@ extern "C" int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* c
   GNNREC_REQUIRE(!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) ||
                      (acc && aligned16(acc) && !(ld_acc & 3) && ld_acc >= width),
                  "gat: ACC needs 16-B aligned acc");
-  GatParams p{Csr{row_ptr, col, nullptr, n_rows}, hfeat, ldh, s_self, s_neigh, heads, o_dim, slope,
+  GatParams p{Csr{row_ptr, col, nullptr, n_rows}, hfeat, ldh, head_stride, s_self, s_neigh, heads, o_dim, slope,
               mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, max_row_len};
   hipStream_t s = as_hip(stream);
   auto grid = [&](int f) { return dim3((unsigned)ceil_div(n_rows, (64 / (f / 4)) * (kBlock / 64))); };
@@ -228,7 +236,7 @@ extern "C" int gnnrec_gat_heavy_f32(const int32_t* col, const int64_t* seg_row,
                                     const int64_t* seg_beg, const int64_t* seg_end, int64_t n_seg,
                                     const int64_t* heavy_rows, const int64_t* heavy_seg_ptr,
                                     int64_t n_heavy, float* work, const float* hfeat, int64_t ldh,
-                                    const float* s_self, const float* s_neigh, int32_t heads,
+                                    int64_t head_stride, const float* s_self, const float* s_neigh, int32_t heads,
                                     int32_t o_dim, float slope, int32_t mean_heads,
                                     int32_t apply_elu, float* out, int64_t ldo, int32_t epi,
                                     const float* self, int64_t ld_self, float* acc, int64_t ld_acc,
@@ -237,10 +245,11 @@ extern "C" int gnnrec_gat_heavy_f32(const int32_t* col, const int64_t* seg_row,
                  "gat_heavy: bad sizes");
   if (n_heavy == 0) return GNNREC_OK;
   GNNREC_REQUIRE(col && seg_row && seg_beg && seg_end && heavy_rows && heavy_seg_ptr && work &&
-                     hfeat && s_self && s_neigh && aligned16(work) && aligned16(hfeat) && !(ldh & 3),
+                     hfeat && s_self && s_neigh && aligned16(work) && aligned16(hfeat) && !(ldh & 3) &&
+                     head_stride >= 0 && !(head_stride & 3),
                  "gat_heavy: null or misaligned operand");
   const int F = heads * o_dim;
-  GatParams p{Csr{nullptr, col, nullptr, 0}, hfeat, ldh, s_self, s_neigh, heads, o_dim, slope,
+  GatParams p{Csr{nullptr, col, nullptr, 0}, hfeat, ldh, head_stride, s_self, s_neigh, heads, o_dim, slope,
               mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, 0};
   GatSplit sp{seg_row, seg_beg, seg_end, n_seg, heavy_rows, heavy_seg_ptr, n_heavy, work};
   hipStream_t s = as_hip(stream);

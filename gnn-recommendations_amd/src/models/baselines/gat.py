@@ -69,14 +69,52 @@ class GATLayer(nn.Module):
         out = x @ self.fused_weight().t()                                  # [N, H*o + 2H]
         return out[:, :ho], out[:, ho:ho + self.n_heads], out[:, ho + self.n_heads:]
 
+    def shares_input(self) -> bool:
+        """Head-averaged layer: aggregate x itself per head and apply W_h afterwards,
+        mean_h sum_j a_hj W_h x_j = (1/H) sum_h W_h (sum_j a_hj x_j), so a neighbour costs an
+        in_dim-wide gather instead of the H*out_dim-wide h (4x fewer bytes for the last GAT
+        layer). Same value reassociated (fp32 tolerance, like the rest of GAT)."""
+        return (not self.concat_heads and self.in_dim % 4 == 0
+                and self.n_heads * self.in_dim in (16, 32, 64, 128, 256))
+
+    def head_mean_weight(self) -> torch.Tensor:
+        """[H*in, out] = vstack(W_h^T) / H: z (per-head aggregates of x) @ this = the head mean."""
+        return torch.cat([w.weight.t() for w in self.W], dim=0) / self.n_heads
+
+    def native_inputs(self, x: torch.Tensor):
+        """(table gathered per neighbour, s_self, s_neigh) for the rows of x."""
+        if self.shares_input():
+            H = self.n_heads
+            s = x @ self.fused_weight()[H * self.out_dim:].t()            # [N, 2H]
+            return x, s[:, :H], s[:, H:]
+        return self.projections(x)
+
+    def native_forward(self, a, feat, s_self, s_neigh, *, apply_elu: bool = False, epi: int = 0,
+                       self_rows=None, acc=None, acc_div: float = 1.0) -> torch.Tensor:
+        """The native layer given native_inputs (feat may be a gathered/exchanged table)."""
+        if not self.shares_input():
+            return ops.gat_aggregate(a, feat, s_self, s_neigh, self.n_heads, self.out_dim,
+                                     self.alpha, mean_heads=not self.concat_heads,
+                                     apply_elu=apply_elu, epi=epi, self_rows=self_rows, acc=acc,
+                                     acc_div=acc_div)
+        z = ops.gat_aggregate(a, feat, s_self, s_neigh, self.n_heads, self.in_dim, self.alpha,
+                              mean_heads=False, apply_elu=False, shared_rows=True)
+        y = z @ self.head_mean_weight()
+        if apply_elu:
+            y = F.elu(y)
+        if epi & (EPI_ACC_INIT | EPI_ACC_ADD):      # the kernel epilogue's order
+            b = (self_rows if epi & EPI_ACC_INIT else acc) + y
+            if epi & EPI_ACC_DIV:
+                b = b / acc_div
+            acc.copy_(b)
+        return y
+
     def forward(self, x: torch.Tensor, adj_matrix, *, apply_elu: bool = False, epi: int = 0,
                 self_rows=None, acc=None, acc_div: float = 1.0) -> torch.Tensor:
         a = ops.as_operand(adj_matrix)
         if self.native_ok(a, x):
-            h, ss, sn = self.projections(x)
-            return ops.gat_aggregate(a, h, ss, sn, self.n_heads, self.out_dim, self.alpha,
-                                     mean_heads=not self.concat_heads, apply_elu=apply_elu,
-                                     epi=epi, self_rows=self_rows, acc=acc, acc_div=acc_div)
+            return self.native_forward(a, *self.native_inputs(x), apply_elu=apply_elu, epi=epi,
+                                       self_rows=self_rows, acc=acc, acc_div=acc_div)
         out = self._dense_forward(x, a)
         return F.elu(out) if apply_elu else out
 

@@ -307,35 +307,34 @@ def ngcf_forward_dist(dg: DistributedGraph, model, x0_pad: torch.Tensor, *,
     return gather_rows(dg, local) if gather_output else local
 
 
-def _native_gat_layer(shard, h, s_self, s_neigh, layer, *, apply_elu, epi, self_rows, acc,
+def _native_gat_layer(shard, feat, s_self, s_neigh, layer, *, apply_elu, epi, self_rows, acc,
                       acc_div):
-    from .functional import gat_aggregate
-    return gat_aggregate(shard, h, s_self, s_neigh, layer.n_heads, layer.out_dim, layer.alpha,
-                         mean_heads=not layer.concat_heads, apply_elu=apply_elu, epi=epi,
-                         self_rows=self_rows, acc=acc, acc_div=acc_div)
+    return layer.native_forward(shard, feat, s_self, s_neigh, apply_elu=apply_elu, epi=epi,
+                                self_rows=self_rows, acc=acc, acc_div=acc_div)
 
 
 def gat_forward_dist(dg: DistributedGraph, model, x0_pad: torch.Tensor, *,
                      gather_output: bool = False, layer_fn: Optional[Callable] = None
                      ) -> torch.Tensor:
     """GAT eval forward over a row-sharded operand (SURVEY §8e "GAT: all-gather h and the
-    per-node attention scalars instead"). Per layer each rank projects only its own rows
-    (h = x W^T for all heads, s_self, s_neigh), exchanges h and s_neigh (the only per-node
+    per-node attention scalars instead"). Per layer each rank computes the per-node values
+    of its own rows only (GATLayer.native_inputs: h = x W^T for all heads, or x itself for the
+    head-averaged layer, plus s_self and s_neigh), exchanges that table and s_neigh (the
     values a neighbour reads), and runs the sparse edge-softmax aggregation over its shard
-    with ELU and the layer mean fused (gnnrec_gat_aggregate_f32 + heavy-row split). x itself
-    never moves. Returns this rank's rows of the layer mean (or the full table)."""
+    with ELU and the layer mean fused (gnnrec_gat_aggregate_f32 + heavy-row split). Returns
+    this rank's rows of the layer mean (or the full table)."""
     from ._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT
     layer_fn = layer_fn or _native_gat_layer
     x_local = dg.local_slice(x0_pad)
     acc = torch.empty_like(x_local)
     L = len(model.layers)
     for k, layer in enumerate(model.layers, start=1):
-        h, ss, sn = layer.projections(x_local)
-        hp, snp = _exchanged(dg, h), _exchanged(dg, sn.contiguous())
+        feat, ss, sn = layer.native_inputs(x_local)
+        featp, snp = _exchanged(dg, feat), _exchanged(dg, sn.contiguous())
         epi = EPI_ACC_INIT if k == 1 else EPI_ACC_ADD
         if k == L:
             epi |= EPI_ACC_DIV
-        x_local = layer_fn(dg.shard, hp, ss, snp, layer, apply_elu=True, epi=epi,
+        x_local = layer_fn(dg.shard, featp, ss, snp, layer, apply_elu=True, epi=epi,
                            self_rows=x_local, acc=acc, acc_div=float(L + 1))
     return gather_rows(dg, acc) if gather_output else acc
 

@@ -265,20 +265,25 @@ def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh:
                   heads: int, o_dim: int, slope: float = 0.2, mean_heads: bool = False,
                   apply_elu: bool = False, *, out: Optional[torch.Tensor] = None, epi: int = 0,
                   self_rows: Optional[torch.Tensor] = None, acc: Optional[torch.Tensor] = None,
-                  acc_div: float = 1.0,
-                  heavy_threshold: int = GAT_HEAVY_THRESHOLD) -> Optional[torch.Tensor]:
+                  acc_div: float = 1.0, heavy_threshold: int = GAT_HEAVY_THRESHOLD,
+                  shared_rows: bool = False) -> Optional[torch.Tensor]:
     """Sparse edge-softmax aggregation of one GAT layer, all heads (gnnrec_gat_aggregate_f32),
-    with rows longer than `heavy_threshold` split into segments (gnnrec_gat_heavy_f32)."""
+    with rows longer than `heavy_threshold` split into segments (gnnrec_gat_heavy_f32).
+    shared_rows: `h` is ONE [N, o_dim] table every head aggregates (head_stride 0), e.g. the
+    layer input x when W_h is applied after the aggregation."""
     h = _rowmajor(h)
     s_self = s_self.contiguous()
     s_neigh = s_neigh.contiguous()
     _require_device(adj, h, self_rows, acc)
+    if h.shape[1] < (o_dim if shared_rows else heads * o_dim):
+        raise ValueError("h is narrower than the aggregated rows")
+    head_stride = 0 if shared_rows else o_dim
     width = o_dim if mean_heads else heads * o_dim
     if out is None and not (epi & EPI_NO_Y):
         out = torch.empty((adj.n_rows, width), dtype=torch.float32, device=h.device)
     plan = adj.heavy_plan(heavy_threshold, GAT_SEGMENT) if heavy_threshold > 0 else None
-    common = (ptr(h), h.stride(0), ptr(s_self), ptr(s_neigh), int(heads), int(o_dim),
-              float(slope), int(mean_heads), int(apply_elu), ptr(out),
+    common = (ptr(h), h.stride(0), head_stride, ptr(s_self), ptr(s_neigh), int(heads),
+              int(o_dim), float(slope), int(mean_heads), int(apply_elu), ptr(out),
               out.stride(0) if out is not None else width, int(epi), ptr(self_rows),
               self_rows.stride(0) if self_rows is not None else width, ptr(acc),
               acc.stride(0) if acc is not None else width, float(acc_div))

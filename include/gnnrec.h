@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GNNREC_ABI_VERSION 1
+#define GNNREC_ABI_VERSION 2
 
 typedef struct ihipStream_t* gnnrec_stream_t;
 
@@ -161,8 +161,12 @@ int gnnrec_spmm_dense_f32(const int64_t* row_ptr, const int32_t* col, const floa
  * for every head h and destination row r with neighbours j (CSR pattern; values ignored):
  *   e_j = LeakyReLU_slope(s_self[r, h] + s_neigh[j, h]);  a = softmax_j(e)
  *   o[r, h, :] = sum_j a_j * hfeat[j, h, :]
- * (single pass, online max/sum rescaling, fp32). hfeat: [N, heads*o_dim] head-major columns
- * (= cat of the per-head W_h x); s_self / s_neigh: [N, heads] (ld = heads).
+ * (single pass, online max/sum rescaling, fp32). hfeat[j, h, :] starts at
+ * hfeat + j*ldh + h*head_stride: head_stride = o_dim for the head-major [N, heads*o_dim]
+ * table of the per-head W_h x; head_stride = 0 lets every head aggregate the same row (the
+ * layer input x, with W_h applied by the caller afterwards: sum_j a_j W_h x_j =
+ * W_h sum_j a_j x_j — the head-averaged last layer then gathers o_dim instead of heads*o_dim
+ * floats per neighbour). s_self / s_neigh: [N, heads] (ld = heads).
  * mean_heads = 0: out[r] = cat_h o[r,h,:] ([n_rows, heads*o_dim]); 1: out[r] = mean_h
  * o[r,h,:] ([n_rows, o_dim]). apply_elu: out = ELU(out) (alpha 1). epi: the ACC_* flags of
  * gnnrec_spmm_csr_f32 applied to the (ELU'd) output with `self` = the layer input rows.
@@ -171,7 +175,8 @@ int gnnrec_spmm_dense_f32(const int64_t* row_ptr, const int32_t* col, const floa
  * max_row_len > 0: rows with more neighbours are skipped here and must be finished by
  * gnnrec_gat_heavy_f32 (power-law degree buckets; 0 = every row here). */
 int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* col, int64_t n_rows,
-                             const float* hfeat, int64_t ldh, const float* s_self,
+                             const float* hfeat, int64_t ldh, int64_t head_stride,
+                             const float* s_self,
                              const float* s_neigh, int32_t heads, int32_t o_dim, float slope,
                              int32_t mean_heads, int32_t apply_elu, float* out, int64_t ldo,
                              int32_t epi, const float* self, int64_t ld_self, float* acc,
@@ -186,11 +191,12 @@ int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* col, int64_t
 int gnnrec_gat_heavy_f32(const int32_t* col, const int64_t* seg_row, const int64_t* seg_beg,
                          const int64_t* seg_end, int64_t n_seg, const int64_t* heavy_rows,
                          const int64_t* heavy_seg_ptr, int64_t n_heavy, float* work,
-                         const float* hfeat, int64_t ldh, const float* s_self,
-                         const float* s_neigh, int32_t heads, int32_t o_dim, float slope,
-                         int32_t mean_heads, int32_t apply_elu, float* out, int64_t ldo,
-                         int32_t epi, const float* self, int64_t ld_self, float* acc,
-                         int64_t ld_acc, float acc_div, gnnrec_stream_t stream);
+                         const float* hfeat, int64_t ldh, int64_t head_stride,
+                         const float* s_self, const float* s_neigh, int32_t heads,
+                         int32_t o_dim, float slope, int32_t mean_heads, int32_t apply_elu,
+                         float* out, int64_t ldo, int32_t epi, const float* self,
+                         int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
+                         gnnrec_stream_t stream);
 
 /* ---- a13: scoring + seen-item mask + top-K ------------------------------------------
  * Replaces evaluator.py:96-105 / trainer.py:327-336 for one batch of users:

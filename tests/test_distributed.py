@@ -102,9 +102,12 @@ def cpu_ngcf_layer(shard, x_in, x_self, layer, gs, out):
     out.copy_(gs(o) if gs is not None else o)
 
 
-def cpu_gat_layer(shard, h, s_self, s_neigh, layer, *, apply_elu, epi, self_rows, acc, acc_div):
-    """CPU stand-in for gnnrec_gat_aggregate_f32: edge softmax over the shard's CSR pattern."""
-    n, H, o = shard.n_rows, layer.n_heads, layer.out_dim
+def cpu_gat_layer(shard, feat, s_self, s_neigh, layer, *, apply_elu, epi, self_rows, acc,
+                  acc_div):
+    """CPU stand-in for GATLayer.native_forward: edge softmax over the shard's CSR pattern."""
+    n, H = shard.n_rows, layer.n_heads
+    shared = layer.shares_input()
+    o = layer.in_dim if shared else layer.out_dim
     rp = shard.row_ptr
     rows = torch.repeat_interleave(torch.arange(n), rp[1:] - rp[:-1])
     col = shard.col.long()
@@ -113,9 +116,13 @@ def cpu_gat_layer(shard, h, s_self, s_neigh, layer, *, apply_elu, epi, self_rows
                                                          "amax")
     p = torch.exp(e - m[rows])
     s = torch.zeros(n, H).index_add_(0, rows, p)
-    agg = torch.zeros(n, H, o).index_add_(0, rows, p[..., None] * h.view(-1, H, o)[col])
+    g = feat[col].unsqueeze(1).expand(-1, H, -1) if shared else feat.view(-1, H, o)[col]
+    agg = torch.zeros(n, H, o).index_add_(0, rows, p[..., None] * g)
     agg = agg / s[..., None]
-    out = agg.reshape(n, H * o) if layer.concat_heads else agg.mean(1)
+    if shared:
+        out = agg.reshape(n, H * o) @ layer.head_mean_weight()
+    else:
+        out = agg.reshape(n, H * o) if layer.concat_heads else agg.mean(1)
     if apply_elu:
         out = torch.nn.functional.elu(out)
     if epi & EPI_ACC_INIT:

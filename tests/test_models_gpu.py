@@ -182,3 +182,20 @@ def test_gat_heavy_row_split_matches_unsplit(cuda, threshold):
         torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
     finally:
         F.GAT_SEGMENT = old
+
+
+@pytest.mark.parametrize("heavy", [0, 64])
+def test_gat_shared_rows_equals_replicated_table(cuda, heavy):
+    """head_stride 0 (every head aggregates the same x row) == the head-major table holding
+    x once per head, bit for bit, on the normal and the heavy-row split path."""
+    from src.ops import functional as F
+    rng = np.random.default_rng(9)
+    u = rng.integers(0, 300, 6000)
+    i = np.minimum(rng.zipf(1.3, 6000) - 1, 199)
+    g = CsrGraph.from_interactions(u, i, 300, 200).to(cuda)
+    n, H, o = g.shape[0], 4, 64
+    x = torch.randn(n, o, device=cuda) * 0.1
+    ss, sn = torch.randn(n, H, device=cuda), torch.randn(n, H, device=cuda)
+    z = F.gat_aggregate(g, x, ss, sn, H, o, 0.2, shared_rows=True, heavy_threshold=heavy)
+    zr = F.gat_aggregate(g, x.repeat(1, H), ss, sn, H, o, 0.2, heavy_threshold=heavy)
+    assert torch.equal(z, zr)
