@@ -52,3 +52,13 @@ class EdgeSpecificBundleConnection(nn.Module):
         for t, layer in enumerate(self.connection_layers):
             W[edge_type == t] = layer().unsqueeze(0)
         return W
+
+    def type_matrices(self) -> torch.Tensor:
+        """[n_edge_types, d, d]: the per-type connection matrices forward() broadcasts."""
+        return torch.stack([layer() for layer in self.connection_layers])
+
+    def transport(self, x, edge_index, edge_type):
+        """parallel_transport_along_edges(x, edge_index, self(edge_index, edge_type)) without
+        the [E, d, d] tensor (parallel_transport_typed: one native launch per edge type)."""
+        from .parallel_transport import parallel_transport_typed
+        return parallel_transport_typed(x, edge_index, edge_type, self.type_matrices())

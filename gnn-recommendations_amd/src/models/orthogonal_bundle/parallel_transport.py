@@ -16,18 +16,46 @@ from ...ops.graph import CsrGraph
 _EDGE_CACHE: dict = {}
 
 
-def edge_index_operand(edge_index: torch.Tensor, num_nodes: int) -> CsrGraph:
-    """CsrGraph of B[dst, src] = multiplicity of (src -> dst), on edge_index's device."""
-    key = (edge_index.data_ptr(), edge_index.shape[1], num_nodes, edge_index.device)
+def edge_index_operand(edge_index: torch.Tensor, num_nodes: int,
+                       mask: torch.Tensor = None, tag=None) -> CsrGraph:
+    """CsrGraph of B[dst, src] = multiplicity of (src -> dst), on edge_index's device (only
+    the edges where `mask` holds, when given; `tag` names the subset in the cache key)."""
+    key = (edge_index.data_ptr(), edge_index.shape[1], num_nodes, edge_index.device, tag)
     g = _EDGE_CACHE.get(key)
     if g is None:
         src, dst = edge_index[0].long(), edge_index[1].long()
+        if mask is not None:
+            src, dst = src[mask], dst[mask]
         vals = torch.ones(src.numel(), dtype=torch.float32, device=edge_index.device)
         coo = torch.sparse_coo_tensor(torch.stack([dst, src]), vals, (num_nodes, num_nodes))
         g = CsrGraph.from_torch_sparse(coo, symmetric=False)
-        _EDGE_CACHE.clear()
+        if len(_EDGE_CACHE) > 16:
+            _EDGE_CACHE.clear()
         _EDGE_CACHE[key] = g
     return g
+
+
+def parallel_transport_typed(x: torch.Tensor, edge_index: torch.Tensor, edge_type: torch.Tensor,
+                             W_types: torch.Tensor) -> torch.Tensor:
+    """out[j] = sum over edges e = (i -> j) of W_types[edge_type[e]] @ x[i] — what
+    parallel_transport_along_edges computes with the [E, d, d] tensor that
+    EdgeSpecificBundleConnection.forward assembles (bundle_layer.py:106-149 feeding
+    parallel_transport.py:37-43), without materialising it (16 KB per edge at d = 64): per
+    type t the sum commutes with W_t, so out = sum_t (B_t x) W_t^T with B_t the type-t edge
+    counts — one native SpMM + MFMA-transform launch per type, accumulated in place."""
+    T = W_types.shape[0]
+    if (x.is_cuda and x.dim() == 2 and x.shape[1] in (32, 64, 128)
+            and not (torch.is_grad_enabled() and (x.requires_grad or W_types.requires_grad))):
+        out = torch.zeros_like(x)
+        for t in range(T):
+            B = edge_index_operand(edge_index, x.size(0), edge_type == t,
+                                   ("type", t, edge_type.data_ptr(), edge_type.numel()))
+            if B.nnz == 0:
+                continue
+            ops.dense_layer(B, x, W_types[t].t(), 1.0, None, 0.0, acc=out, acc_mode=2,
+                            w_out=1.0, store_y=False)
+        return out
+    return parallel_transport_along_edges(x, edge_index, W_types[edge_type.long()])
 
 
 def parallel_transport_along_edges(x, edge_index, W_connection):

@@ -143,3 +143,25 @@ def test_cpu_csrgraph_operand_is_rejected():
     m = LightGCN(2, 2, embedding_dim=8, n_layers=1)
     with pytest.raises(ValueError, match="ROCm"):
         m(g)
+
+
+def _typed_edges(seed=0, n=200, e=3000):
+    g = torch.Generator().manual_seed(seed)
+    ei = torch.randint(0, n, (2, e), generator=g)
+    et = torch.randint(0, 2, (e,), generator=g)
+    x = torch.randn(n, 64, generator=g) * 0.1
+    return ei, et, x
+
+
+def test_edge_specific_transport_cpu_matches_reference_formula():
+    """§8f4: EdgeSpecificBundleConnection.transport == parallel_transport_along_edges with the
+    [E, d, d] tensor its forward() builds (the reference's composition)."""
+    from src.models.orthogonal_bundle import EdgeSpecificBundleConnection
+    from src.models.orthogonal_bundle.parallel_transport import parallel_transport_along_edges
+    torch.manual_seed(4)
+    esbc = EdgeSpecificBundleConnection(64, 8)
+    ei, et, x = _typed_edges()
+    with torch.no_grad():
+        ref = parallel_transport_along_edges(x, ei, esbc(ei, et))
+        out = esbc.transport(x, ei, et)
+    torch.testing.assert_close(out, ref, rtol=0, atol=1e-6)

@@ -200,3 +200,19 @@ def test_gat_shared_rows_equals_replicated_table(cuda, heavy):
     zr = F.gat_aggregate(g, x.repeat(1, H), ss, sn, H, o, 0.2, heavy_threshold=heavy)
     assert torch.isnan(z).any()                      # never-drawn items: empty rows -> NaN
     np.testing.assert_array_equal(z.cpu().numpy().view(np.uint32), zr.cpu().numpy().view(np.uint32))
+
+
+def test_edge_specific_transport_native(cuda):
+    """§8f4 on the GPU: per-type CSR + SpMM/MFMA transform, no [E, d, d] tensor."""
+    from test_models import _typed_edges
+    from src.models.orthogonal_bundle import EdgeSpecificBundleConnection
+    from src.models.orthogonal_bundle.parallel_transport import parallel_transport_along_edges
+    torch.manual_seed(4)
+    esbc = EdgeSpecificBundleConnection(64, 8)
+    ei, et, x = _typed_edges(1)
+    with torch.no_grad():
+        ref = parallel_transport_along_edges(x, ei, esbc(ei, et))
+        esbc = esbc.to(cuda)
+        out = esbc.transport(x.to(cuda), ei.to(cuda), et.to(cuda))
+    assert out.is_cuda
+    torch.testing.assert_close(out.cpu(), ref, rtol=0, atol=2e-6)
