@@ -34,6 +34,8 @@ struct TopkParams {
   int k;
   int64_t* out_idx;
   float* out_score;
+  int n_split;           // item ranges (blockIdx.y); > 1: partial lists go to out_* with
+                         // row stride n_split*k at offset split*k, merged by topk_merge_kernel
 };
 
 // a strictly precedes b in the output order
@@ -77,10 +79,11 @@ __device__ __forceinline__ int find_worst(const float* ls, const int* li, int la
 template <int D, int KM>
 __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
   constexpr int STEPS = D / 4;
-  constexpr int TI = 64;       // items per LDS tile
+  constexpr int TI = D <= 128 ? 64 : 32;  // items per LDS tile
   constexpr int LDV = D + 2;
   constexpr int UPB = 64;      // users per workgroup
-  __shared__ __attribute__((aligned(16))) float v_lds[TI * LDV];
+  constexpr int PIECES = TI * (D / 4) / kBlock;  // float4 per thread per tile
+  __shared__ __attribute__((aligned(16))) float v_lds[2][TI * LDV];
   __shared__ float l_score[UPB][KM];
   __shared__ int l_item[UPB][KM];
   __shared__ float l_worst_s[UPB];
@@ -90,6 +93,10 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i16 = lane & 15, k4 = lane >> 4;
   const int64_t ub = (int64_t)blockIdx.x * UPB;
+  // this workgroup's item range (a multiple of TI, so tiles never straddle two ranges)
+  const int64_t per = ((p.n_items + p.n_split - 1) / p.n_split + TI - 1) / TI * TI;
+  const int64_t i_beg = (int64_t)blockIdx.y * per;
+  const int64_t i_end = min<int64_t>(p.n_items, i_beg + per);
   // A fragments: this wave's 16 users, k = 4s + k4 (ascending k per MFMA chain)
   float af[STEPS];
   {
@@ -106,23 +113,37 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
     l_worst_i[e] = INT_MAX;
     l_worst_p[e] = 0;
   }
-  __syncthreads();
 
-  for (int64_t t0 = 0; t0 < p.n_items; t0 += TI) {
-    // stage 64 item rows (zero rows past the end)
-    for (int e = threadIdx.x; e < TI * (D / 4); e += kBlock) {
-      const int r = e / (D / 4), c4 = e % (D / 4);
+  // item tiles are double-buffered: the global loads of tile t+1 are in flight while the
+  // MFMAs and the list updates of tile t run
+  float4 stage[PIECES];
+  auto load_tile = [&](int64_t t0) {
+#pragma unroll
+    for (int q = 0; q < PIECES; ++q) {
+      const int e = threadIdx.x + q * kBlock, r = e / (D / 4), c4 = e % (D / 4);
       const int64_t item = t0 + r;
-      const float4 q = item < p.n_items ? ld4(p.v + item * p.ldv + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
-      float* dst = &v_lds[r * LDV + 4 * c4];
-      dst[0] = q.x; dst[1] = q.y; dst[2] = q.z; dst[3] = q.w;
+      stage[q] = item < i_end ? ld4(p.v + item * p.ldv + 4 * c4) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+  };
+  auto park_tile = [&](int b) {
+#pragma unroll
+    for (int q = 0; q < PIECES; ++q) {
+      const int e = threadIdx.x + q * kBlock, r = e / (D / 4), c4 = e % (D / 4);
+      float* dst = &v_lds[b][r * LDV + 4 * c4];
+      dst[0] = stage[q].x; dst[1] = stage[q].y; dst[2] = stage[q].z; dst[3] = stage[q].w;
+    }
+  };
+  if (i_beg < i_end) load_tile(i_beg);
+  int buf = 0;
+  for (int64_t t0 = i_beg; t0 < i_end; t0 += TI, buf ^= 1) {
+    park_tile(buf);
     __syncthreads();
+    if (t0 + TI < i_end) load_tile(t0 + TI);
     floatx4_t acc[TI / 16];
 #pragma unroll
     for (int nt = 0; nt < TI / 16; ++nt) {
       floatx4_t c = {0.f, 0.f, 0.f, 0.f};
-      const float* brow = &v_lds[(16 * nt + i16) * LDV + k4];
+      const float* brow = &v_lds[buf][(16 * nt + i16) * LDV + k4];
 #pragma unroll
       for (int s = 0; s < STEPS; ++s) c = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], brow[4 * s], c, 0, 0, 0);
       acc[nt] = c;
@@ -138,7 +159,7 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
         float s = acc[nt][q];
         if (s != s) s = -INFINITY;  // NaN scores rank last
         const int item = (int)item64;
-        bool cand = user < p.nb && item64 < p.n_items &&
+        bool cand = user < p.nb && item64 < i_end &&
                     better(s, item, l_worst_s[ul], l_worst_i[ul]);
         // serialize the (rare) insertions of this wave, one candidate at a time
         unsigned long long m = __ballot(cand);
@@ -169,8 +190,8 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
         }
       }
     }
-    __syncthreads();
   }
+  __syncthreads();
   // emit each user's list sorted by (score desc, item asc): rank by counting
   for (int ul = 16 * wave; ul < 16 * wave + 16; ++ul) {
     const int64_t user = ub + ul;
@@ -185,9 +206,43 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
         rank += (better(sf, jf, s, i) || (sf == s && jf == i && f < e)) ? 1 : 0;
       }
       if (rank < p.k) {
-        p.out_idx[user * p.k + rank] = i == INT_MAX ? -1 : (int64_t)i;
-        p.out_score[user * p.k + rank] = s;
+        const int64_t o = user * ((int64_t)p.n_split * p.k) + (int64_t)blockIdx.y * p.k + rank;
+        p.out_idx[o] = i == INT_MAX ? -1 : (int64_t)i;
+        p.out_score[o] = s;
       }
+    }
+  }
+}
+
+
+// Merge the n_split partial lists of each user (one wave per user): rank every candidate
+// by counting the candidates that precede it under (score desc, item asc; -1 = empty slot
+// last, empty slots ordered by position) and keep ranks < k. Exact: each partial list is the
+// exact top-k of its item range.
+__global__ __launch_bounds__(kBlock) void topk_merge_kernel(const int64_t* __restrict__ pidx,
+                                                            const float* __restrict__ pscore,
+                                                            int64_t nb, int n_split, int k,
+                                                            int64_t* __restrict__ out_idx,
+                                                            float* __restrict__ out_score) {
+  const int lane = threadIdx.x & 63;
+  const int64_t user = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (user >= nb) return;
+  const int C = n_split * k;
+  const int64_t* ci = pidx + user * C;
+  const float* cs = pscore + user * C;
+  for (int e = lane; e < C; e += 64) {
+    const float s = cs[e];
+    const int64_t i = ci[e];
+    const int64_t ie = i < 0 ? INT64_MAX : i;
+    int rank = 0;
+    for (int f = 0; f < C; ++f) {
+      const float sf = cs[f];
+      const int64_t jf = ci[f] < 0 ? INT64_MAX : ci[f];
+      rank += (sf > s || (sf == s && (jf < ie || (jf == ie && f < e)))) ? 1 : 0;
+    }
+    if (rank < k) {
+      out_idx[user * k + rank] = i;
+      out_score[user * k + rank] = s;
     }
   }
 }
@@ -199,7 +254,8 @@ using namespace gnnrec;
 namespace {
 template <int D, int KM>
 void launch_topk(const TopkParams& p, hipStream_t s) {
-  hipLaunchKernelGGL((score_topk_kernel<D, KM>), dim3((unsigned)ceil_div(p.nb, 64)), dim3(kBlock), 0, s, p);
+  hipLaunchKernelGGL((score_topk_kernel<D, KM>), dim3((unsigned)ceil_div(p.nb, 64), (unsigned)p.n_split),
+                     dim3(kBlock), 0, s, p);
 }
 template <int D>
 int dispatch_k(const TopkParams& p, hipStream_t s) {
@@ -210,24 +266,44 @@ int dispatch_k(const TopkParams& p, hipStream_t s) {
 }
 }  // namespace
 
+extern "C" int gnnrec_score_topk_split_f32(const float* u, int64_t ldu, int64_t n_users_batch,
+                                           const float* v, int64_t ldv, int64_t n_items, int32_t d,
+                                           const int64_t* seen_ptr, const int32_t* seen_col,
+                                           int32_t k, int32_t n_split, int64_t* work_idx,
+                                           float* work_score, int64_t* out_idx, float* out_score,
+                                           gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(n_users_batch >= 0 && n_items >= 0 && k >= 1 && k <= 128, "score_topk: need 1 <= k <= 128");
+  GNNREC_REQUIRE(n_split >= 1 && n_split <= 65535, "score_topk: n_split must be in [1, 65535]");
+  if (n_users_batch == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(n_items < (int64_t)INT32_MAX, "score_topk: n_items must fit int32");
+  GNNREC_REQUIRE(u && v && out_idx && out_score, "score_topk: null operand");
+  GNNREC_REQUIRE(n_split == 1 || (work_idx && work_score), "score_topk: n_split > 1 needs work buffers");
+  GNNREC_REQUIRE(ldu >= d && ldv >= d && aligned16(v) && !(ldv & 3), "score_topk: v must be 16-B aligned rows");
+  GNNREC_REQUIRE(!seen_ptr || seen_col || n_users_batch == 0, "score_topk: seen_ptr without seen_col");
+  const bool split = n_split > 1;
+  const TopkParams p{u, ldu, n_users_batch, v, ldv, n_items, seen_ptr, seen_col, k,
+                     split ? work_idx : out_idx, split ? work_score : out_score, n_split};
+  hipStream_t s = as_hip(stream);
+  int rc;
+  switch (d) {
+    case 16: rc = dispatch_k<16>(p, s); break;
+    case 32: rc = dispatch_k<32>(p, s); break;
+    case 64: rc = dispatch_k<64>(p, s); break;
+    case 128: rc = dispatch_k<128>(p, s); break;
+    case 256: rc = dispatch_k<256>(p, s); break;
+    default: set_error("score_topk: d=%d unsupported (16, 32, 64, 128, 256)", d); return GNNREC_EUNSUPPORTED;
+  }
+  if (rc != GNNREC_OK || !split) return rc;
+  hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)ceil_div(n_users_batch, kBlock / 64)),
+                     dim3(kBlock), 0, s, work_idx, work_score, n_users_batch, n_split, k, out_idx,
+                     out_score);
+  return check_launch("topk_merge");
+}
+
 extern "C" int gnnrec_score_topk_f32(const float* u, int64_t ldu, int64_t n_users_batch,
                                      const float* v, int64_t ldv, int64_t n_items, int32_t d,
                                      const int64_t* seen_ptr, const int32_t* seen_col, int32_t k,
                                      int64_t* out_idx, float* out_score, gnnrec_stream_t stream) {
-  GNNREC_REQUIRE(n_users_batch >= 0 && n_items >= 0 && k >= 1 && k <= 128, "score_topk: need 1 <= k <= 128");
-  if (n_users_batch == 0) return GNNREC_OK;
-  GNNREC_REQUIRE(n_items < (int64_t)INT32_MAX, "score_topk: n_items must fit int32");
-  GNNREC_REQUIRE(u && v && out_idx && out_score, "score_topk: null operand");
-  GNNREC_REQUIRE(ldu >= d && ldv >= d && aligned16(v) && !(ldv & 3), "score_topk: v must be 16-B aligned rows");
-  GNNREC_REQUIRE(!seen_ptr || seen_col || n_users_batch == 0, "score_topk: seen_ptr without seen_col");
-  const TopkParams p{u, ldu, n_users_batch, v, ldv, n_items, seen_ptr, seen_col, k, out_idx, out_score};
-  hipStream_t s = as_hip(stream);
-  switch (d) {
-    case 16: return dispatch_k<16>(p, s);
-    case 32: return dispatch_k<32>(p, s);
-    case 64: return dispatch_k<64>(p, s);
-    case 128: return dispatch_k<128>(p, s);
-    case 256: return dispatch_k<256>(p, s);
-    default: set_error("score_topk: d=%d unsupported (16, 32, 64, 128, 256)", d); return GNNREC_EUNSUPPORTED;
-  }
+  return gnnrec_score_topk_split_f32(u, ldu, n_users_batch, v, ldv, n_items, d, seen_ptr, seen_col,
+                                     k, 1, nullptr, nullptr, out_idx, out_score, stream);
 }

@@ -55,16 +55,21 @@ class Evaluator:
         self.k_values = list(k_values)
         self.device = device or torch.device("cuda" if torch.cuda.is_available() else "cpu")
 
-    def topk(self, user_emb, item_emb, users, k, seen_ptr, seen_col, batch_size=2048):
-        """[len(users), k] int64 top-k item ids (fixed tie order)."""
+    def topk(self, user_emb, item_emb, users, k, seen_ptr, seen_col, batch_size=None):
+        """[len(users), k] int64 top-k item ids (fixed tie order). On the GPU nothing of size
+        batch x n_items is materialised, so the batch is large (16384 users) and the kernel's
+        item split fills the chip; the CPU path keeps the reference's 2048."""
+        if batch_size is None:
+            batch_size = 16384 if user_emb.is_cuda else 2048
         rows = []
         for s in range(0, len(users), batch_size):
             b = torch.as_tensor(users[s:s + batch_size], dtype=torch.long, device=user_emb.device)
             bp = seen_ptr[b.cpu().numpy()]
             counts = seen_ptr[b.cpu().numpy() + 1] - bp
             sub_ptr = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
-            sub_col = np.concatenate([seen_col[p:p + c] for p, c in zip(bp, counts)]) \
-                if counts.sum() else np.zeros(0, np.int32)
+            # gather the batch's seen lists without a per-user loop
+            src = np.repeat(bp - sub_ptr[:-1], counts) + np.arange(int(sub_ptr[-1]))
+            sub_col = seen_col[src] if src.size else np.zeros(0, np.int32)
             if user_emb.is_cuda:
                 idx, _ = score_topk(user_emb[b], item_emb, k, torch.from_numpy(sub_ptr),
                                     torch.from_numpy(sub_col.astype(np.int32)))

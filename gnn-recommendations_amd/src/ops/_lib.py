@@ -54,6 +54,8 @@ _SIGNATURES = {
                              _i32, _i32, _f32, _i32, _i32, _p, _i64, _i32, _p, _i64, _p, _i64,
                              _f32, _p],
     "gnnrec_score_topk_f32": [_p, _i64, _i64, _p, _i64, _i64, _i32, _p, _p, _i32, _p, _p, _p],
+    "gnnrec_score_topk_split_f32": [_p, _i64, _i64, _p, _i64, _i64, _i32, _p, _p, _i32, _i32,
+                                    _p, _p, _p, _p, _p],
     "gnnrec_build_bipartite_csr": [_p, _p, _i64, _i64, _i64, _i32, _p, _p, _p, _p, _p, _i32],
     "gnnrec_normalize_values": [_p, _p, _p, _i64, _p, _i32, _p, _i32],
     "gnnrec_build_bipartite_csr_device": [_p, _p, _i64, _i64, _i64, _i32, _p, _p, _p, _p, _p,

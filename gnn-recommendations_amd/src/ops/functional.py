@@ -305,7 +305,8 @@ def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh:
 
 def score_topk(user_emb: torch.Tensor, item_emb: torch.Tensor, k: int,
                seen_ptr: Optional[torch.Tensor] = None,
-               seen_col: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+               seen_col: Optional[torch.Tensor] = None,
+               n_split: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Top-k items per user by score = sequential-fmaf dot product, seen items excluded,
     order (score desc, item index asc) (gnnrec_score_topk_f32; evaluator.py:96-105).
     seen_ptr [B+1] int64 / seen_col int32: per-user sorted seen item lists (CSR)."""
@@ -328,8 +329,22 @@ def score_topk(user_emb: torch.Tensor, item_emb: torch.Tensor, k: int,
     if seen_ptr is not None:
         seen_ptr = seen_ptr.to(u.device, torch.int64).contiguous()
         seen_col = seen_col.to(u.device, torch.int32).contiguous()
-    check(_lib.lib().gnnrec_score_topk_f32(ptr(u), u.stride(0), B, ptr(v), v.stride(0),
-                                           v.shape[0], d, ptr(seen_ptr), ptr(seen_col), int(k),
-                                           ptr(idx), ptr(sc), _lib.stream_of(u.device)),
-          "gnnrec_score_topk_f32")
+    n_split = topk_splits(B, v.shape[0], d) if n_split is None else int(n_split)
+    wi = ws = None
+    if n_split > 1:
+        wi = torch.empty((B, n_split, k), dtype=torch.int64, device=u.device)
+        ws = torch.empty((B, n_split, k), dtype=torch.float32, device=u.device)
+    check(_lib.lib().gnnrec_score_topk_split_f32(ptr(u), u.stride(0), B, ptr(v), v.stride(0),
+                                                 v.shape[0], d, ptr(seen_ptr), ptr(seen_col),
+                                                 int(k), n_split, ptr(wi), ptr(ws), ptr(idx),
+                                                 ptr(sc), _lib.stream_of(u.device)),
+          "gnnrec_score_topk_split_f32")
     return idx, sc
+
+
+def topk_splits(n_users: int, n_items: int, d: int, target_wg: int = 1024) -> int:
+    """Item ranges for gnnrec_score_topk_split_f32: enough workgroups (64 users each) to fill
+    the 256 CUs a few times over, each range at least 16 tiles long."""
+    wg = max(1, -(-n_users // 64))
+    tile = 64 if d <= 128 else 32
+    return int(max(1, min(-(-target_wg // wg), n_items // (16 * tile), 65535)))

@@ -209,6 +209,17 @@ int gnnrec_score_topk_f32(const float* u, int64_t ldu, int64_t n_users_batch,
                           const int64_t* seen_ptr, const int32_t* seen_col, int32_t k,
                           int64_t* out_idx, float* out_score, gnnrec_stream_t stream);
 
+/* Item-split form (same results, bit for bit): the catalogue is cut into n_split ranges
+ * (grid.y), each range's exact top-k per user goes to work_idx/work_score
+ * ([n_users_batch, n_split, k]), and a merge kernel ranks the n_split*k candidates of each
+ * user into out_*. Small user batches (the reference evaluates 2048 users at a time) then
+ * still fill the chip. n_split == 1 is gnnrec_score_topk_f32 (work buffers unused). */
+int gnnrec_score_topk_split_f32(const float* u, int64_t ldu, int64_t n_users_batch,
+                                const float* v, int64_t ldv, int64_t n_items, int32_t d,
+                                const int64_t* seen_ptr, const int32_t* seen_col, int32_t k,
+                                int32_t n_split, int64_t* work_idx, float* work_score,
+                                int64_t* out_idx, float* out_score, gnnrec_stream_t stream);
+
 /* ---- a1-a3: host-side operand construction (native, no GPU) -------------------------
  * build_bipartite_graph + normalize_adjacency_matrix (data/graph_builder.py:16-144):
  * CSR over N = n_users + n_items rows of A = [[0, R], [R^T, 0]] with columns ascending,

@@ -85,3 +85,24 @@ def test_run_all_on_gpu(cuda, model, tmp_path):
     res = json.loads(out.read_text())
     assert rc == 0, res
     assert res[0]["status"] == "success"
+
+
+@pytest.mark.parametrize("n_split", [1, 2, 3, 7, 40])
+@pytest.mark.parametrize("k,d", [(20, 64), (128, 32), (5, 256)])
+def test_topk_item_split_is_exact(cuda, n_split, k, d):
+    """The item-range split + merge (gnnrec_score_topk_split_f32) returns the same bits as the
+    oracle, with exact ties across range boundaries, masks and fewer items than k in a range."""
+    rng = np.random.default_rng(n_split * 7 + k)
+    nb, n_items = 130, 2600
+    U = (rng.standard_normal((nb, d)) * 0.1).astype(np.float32)
+    I = (rng.standard_normal((n_items, d)) * 0.1).astype(np.float32)
+    I[1000:1300] = I[5]                    # ties spanning several ranges
+    lists = [np.unique(rng.integers(0, n_items, rng.integers(0, 80))) for _ in range(nb)]
+    lists[3] = np.arange(n_items - 2)
+    seen_ptr = np.cumsum([0] + [len(l) for l in lists]).astype(np.int64)
+    seen_col = np.concatenate(lists).astype(np.int32)
+    idx, sc = score_topk(torch.from_numpy(U).to(cuda), torch.from_numpy(I).to(cuda), k,
+                         torch.from_numpy(seen_ptr), torch.from_numpy(seen_col), n_split=n_split)
+    oi, osc = oracle.score_topk(U, I, k, seen_ptr, seen_col)
+    np.testing.assert_array_equal(idx.cpu().numpy(), oi)
+    np.testing.assert_array_equal(sc.cpu().numpy().view(np.uint32), osc.view(np.uint32))

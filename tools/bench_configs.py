@@ -219,20 +219,27 @@ def main(argv=None):
             del m, g1, opt, samp
         if 8 in a.configs and world == 1:
             from src.ops import score_topk
-            nb, ni, dd = 16384, 1_000_000, 64
-            gen = torch.Generator(device=device).manual_seed(0)
-            U = torch.randn(nb, dd, device=device, generator=gen) * 0.1
-            V = torch.randn(ni, dd, device=device, generator=gen) * 0.1
-            seen = torch.sort(torch.randint(0, ni, (nb, 100), device=device, generator=gen), 1).values
-            seen_ptr = torch.arange(0, nb * 100 + 1, 100, dtype=torch.int64)
-            seen_col = seen.flatten().to(torch.int32).cpu()
-            f = lambda: score_topk(U, V, 20, seen_ptr, seen_col)
-            t, _ = timed(f, max(2, a.steps // 5), 1, 1, device)
-            flops = 2.0 * nb * ni * dd
-            emit({"config": 8, "workload": f"score + mask + top-20: {nb} users x {ni} items, d={dd}",
-                  "ms": t, "tflops": flops / (t * 1e-3) / 1e12,
-                  "mfma_f32_peak_tflops": 157.3, "frac": flops / (t * 1e-3) / 157.3e12,
-                  "users_per_s": nb / (t * 1e-3)})
+            from src.ops.functional import topk_splits
+            ni, dd = 1_000_000, 64
+            for nb in (16384, 2048):
+                gen = torch.Generator(device=device).manual_seed(0)
+                U = torch.randn(nb, dd, device=device, generator=gen) * 0.1
+                V = torch.randn(ni, dd, device=device, generator=gen) * 0.1
+                seen = torch.sort(torch.randint(0, ni, (nb, 100), device=device, generator=gen), 1).values
+                seen_ptr = torch.arange(0, nb * 100 + 1, 100, dtype=torch.int64)
+                seen_col = seen.flatten().to(torch.int32).cpu()
+                res = {}
+                for ns in sorted({1, topk_splits(nb, ni, dd)}):
+                    f = lambda: score_topk(U, V, 20, seen_ptr, seen_col, n_split=ns)
+                    t, _ = timed(f, max(2, a.steps // 5), 1, 1, device)
+                    res[ns] = t
+                ns = min(res, key=res.get)
+                t = res[ns]
+                flops = 2.0 * nb * ni * dd
+                emit({"config": 8, "workload": f"score + mask + top-20: {nb} users x {ni} items, d={dd}",
+                      "ms": t, "n_split": ns, "ms_by_split": res,
+                      "tflops": flops / (t * 1e-3) / 1e12, "mfma_f32_peak_tflops": 157.3,
+                      "frac": flops / (t * 1e-3) / 157.3e12, "users_per_s": nb / (t * 1e-3)})
         if 7 in a.configs and world == 1:
             rng = np.random.default_rng(0)
             u = rng.integers(0, 1_000_000, 100_000_000, dtype=np.int64)
