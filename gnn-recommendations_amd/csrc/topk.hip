@@ -139,15 +139,23 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
     park_tile(buf);
     __syncthreads();
     if (t0 + TI < i_end) load_tile(t0 + TI);
+    // all B fragments of the tile first (LDS latency paid once), then the MFMAs with the
+    // TI/16 independent accumulator chains interleaved; each chain still runs k ascending
     floatx4_t acc[TI / 16];
+    float bf[TI / 16][STEPS];
 #pragma unroll
     for (int nt = 0; nt < TI / 16; ++nt) {
-      floatx4_t c = {0.f, 0.f, 0.f, 0.f};
       const float* brow = &v_lds[buf][(16 * nt + i16) * LDV + k4];
 #pragma unroll
-      for (int s = 0; s < STEPS; ++s) c = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], brow[4 * s], c, 0, 0, 0);
-      acc[nt] = c;
+      for (int s = 0; s < STEPS; ++s) bf[nt][s] = brow[4 * s];
+      acc[nt] = floatx4_t{0.f, 0.f, 0.f, 0.f};
     }
+    __builtin_amdgcn_sched_barrier(0);  // keep every LDS read ahead of the MFMA stream
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s)
+#pragma unroll
+      for (int nt = 0; nt < TI / 16; ++nt)
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], bf[nt][s], acc[nt], 0, 0, 0);
     // candidates: lane holds users 16*wave + 4*k4 + q (q = reg) x items t0 + 16*nt + i16
 #pragma unroll
     for (int nt = 0; nt < TI / 16; ++nt) {
