@@ -1,25 +1,7 @@
-// Scoring GEMM + seen-item mask + per-user top-K (evaluator.py:96-105, trainer.py:327-336).
-//
-// The reference computes scores = U[b] @ I^T with MKL sgemm, sets the train/valid items of
-// each user to -inf in a Python loop, calls torch.topk (tie order unspecified) and copies
-// the indices to the host. Here one kernel does all of it on the device:
-//   * scores on the matrix cores: v_mfma_f32_16x16x4_f32 is an exact k-ordered fmaf chain,
-//     and the k-steps are issued in ascending k, so score[b,i] is bit-identical to
-//     `acc = 0; for f in 0..d-1: acc = fmaf(u[b,f], v[i,f], acc)` (the oracle's definition);
-//   * a per-user top-K list lives in LDS; a candidate enters only if it beats the list's
-//     current worst entry under the fixed order (score desc, item index asc), so after the
-//     first tiles almost no lane does more than one compare per score;
-//   * seen items are masked lazily: only a candidate that would enter the list is looked up
-//     (binary search in the user's sorted seen list) and, if seen, re-scored as -inf.
-// Workgroup = 4 waves = 64 users (16 per wave); item tiles of 64 rows are staged in LDS
-// ([64][d+2]: d+2 == 2 mod 32 makes the B-fragment reads conflict-free) and reused by the
-// four waves.
+// Diagnostic variants of score_topk_kernel (NOT part of libgnnrec).
 #include <math.h>
-
-#include "gather.h"
-
+#include "../gnn-recommendations_amd/csrc/gather.h"
 namespace gnnrec {
-
 typedef float floatx4_t __attribute__((ext_vector_type(4)));
 
 struct TopkParams {
@@ -76,8 +58,8 @@ __device__ __forceinline__ int find_worst(const float* ls, const int* li, int la
   return __shfl(wp, 0, 64);
 }
 
-template <int D, int KM>
-__global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
+template <int D, int KM, int MODE>
+__global__ __launch_bounds__(kBlock) void xtopk(TopkParams p) {
   constexpr int STEPS = D / 4;
   constexpr int TI = D <= 128 ? 64 : 32;  // items per LDS tile
   constexpr int LDV = D + 2;
@@ -138,7 +120,7 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
   for (int64_t t0 = i_beg; t0 < i_end; t0 += TI, buf ^= 1) {
     park_tile(buf);
     __syncthreads();
-    if (t0 + TI < i_end) load_tile(t0 + TI);
+    if (MODE != 3 && t0 + TI < i_end) load_tile(t0 + TI);
     // all B fragments of the tile first (LDS latency paid once), then the MFMAs with the
     // TI/16 independent accumulator chains interleaved; each chain still runs k ascending
     floatx4_t acc[TI / 16];
@@ -155,7 +137,8 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
     for (int s = 0; s < STEPS; ++s)
 #pragma unroll
       for (int nt = 0; nt < TI / 16; ++nt)
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], bf[nt][s], acc[nt], 0, 0, 0);
+        if (MODE != 2) acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], bf[nt][s], acc[nt], 0, 0, 0);
+    if (MODE == 1) { if (acc[0][0] == 12345.f) p.out_score[0] = acc[1][1] + acc[2][2] + acc[3][3]; continue; }
     // candidates: lane holds users 16*wave + 4*k4 + q (q = reg) x items t0 + 16*nt + i16.
     // Fast filter against register copies of the four users' current worst entries (a list's
     // worst only rises, so a score that fails the copy fails the list); the wave leaves the
@@ -244,95 +227,19 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
 }
 
 
-// Merge the n_split partial lists of each user (one wave per user): rank every candidate
-// by counting the candidates that precede it under (score desc, item asc; -1 = empty slot
-// last, empty slots ordered by position) and keep ranks < k. Exact: each partial list is the
-// exact top-k of its item range.
-__global__ __launch_bounds__(kBlock) void topk_merge_kernel(const int64_t* __restrict__ pidx,
-                                                            const float* __restrict__ pscore,
-                                                            int64_t nb, int n_split, int k,
-                                                            int64_t* __restrict__ out_idx,
-                                                            float* __restrict__ out_score) {
-  const int lane = threadIdx.x & 63;
-  const int64_t user = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-  if (user >= nb) return;
-  const int C = n_split * k;
-  const int64_t* ci = pidx + user * C;
-  const float* cs = pscore + user * C;
-  for (int e = lane; e < C; e += 64) {
-    const float s = cs[e];
-    const int64_t i = ci[e];
-    const int64_t ie = i < 0 ? INT64_MAX : i;
-    int rank = 0;
-    for (int f = 0; f < C; ++f) {
-      const float sf = cs[f];
-      const int64_t jf = ci[f] < 0 ? INT64_MAX : ci[f];
-      rank += (sf > s || (sf == s && (jf < ie || (jf == ie && f < e)))) ? 1 : 0;
-    }
-    if (rank < k) {
-      out_idx[user * k + rank] = i;
-      out_score[user * k + rank] = s;
-    }
-  }
-}
-
 }  // namespace gnnrec
-
 using namespace gnnrec;
-
-namespace {
-template <int D, int KM>
-void launch_topk(const TopkParams& p, hipStream_t s) {
-  hipLaunchKernelGGL((score_topk_kernel<D, KM>), dim3((unsigned)ceil_div(p.nb, 64), (unsigned)p.n_split),
-                     dim3(kBlock), 0, s, p);
-}
-template <int D>
-int dispatch_k(const TopkParams& p, hipStream_t s) {
-  if (p.k <= 32) launch_topk<D, 32>(p, s);
-  else if (p.k <= 64) launch_topk<D, 64>(p, s);
-  else launch_topk<D, 128>(p, s);
-  return check_launch("score_topk");
-}
-}  // namespace
-
-extern "C" int gnnrec_score_topk_split_f32(const float* u, int64_t ldu, int64_t n_users_batch,
-                                           const float* v, int64_t ldv, int64_t n_items, int32_t d,
-                                           const int64_t* seen_ptr, const int32_t* seen_col,
-                                           int32_t k, int32_t n_split, int64_t* work_idx,
-                                           float* work_score, int64_t* out_idx, float* out_score,
-                                           gnnrec_stream_t stream) {
-  GNNREC_REQUIRE(n_users_batch >= 0 && n_items >= 0 && k >= 1 && k <= 128, "score_topk: need 1 <= k <= 128");
-  GNNREC_REQUIRE(n_split >= 1 && n_split <= 65535, "score_topk: n_split must be in [1, 65535]");
-  if (n_users_batch == 0) return GNNREC_OK;
-  GNNREC_REQUIRE(n_items < (int64_t)INT32_MAX, "score_topk: n_items must fit int32");
-  GNNREC_REQUIRE(u && v && out_idx && out_score, "score_topk: null operand");
-  GNNREC_REQUIRE(n_split == 1 || (work_idx && work_score), "score_topk: n_split > 1 needs work buffers");
-  GNNREC_REQUIRE(ldu >= d && ldv >= d && aligned16(v) && !(ldv & 3), "score_topk: v must be 16-B aligned rows");
-  GNNREC_REQUIRE(!seen_ptr || seen_col || n_users_batch == 0, "score_topk: seen_ptr without seen_col");
-  const bool split = n_split > 1;
-  const TopkParams p{u, ldu, n_users_batch, v, ldv, n_items, seen_ptr, seen_col, k,
-                     split ? work_idx : out_idx, split ? work_score : out_score, n_split};
-  hipStream_t s = as_hip(stream);
-  int rc;
-  switch (d) {
-    case 16: rc = dispatch_k<16>(p, s); break;
-    case 32: rc = dispatch_k<32>(p, s); break;
-    case 64: rc = dispatch_k<64>(p, s); break;
-    case 128: rc = dispatch_k<128>(p, s); break;
-    case 256: rc = dispatch_k<256>(p, s); break;
-    default: set_error("score_topk: d=%d unsupported (16, 32, 64, 128, 256)", d); return GNNREC_EUNSUPPORTED;
+extern "C" int xtopk_run(int mode, const float* u, int64_t nb, const float* v, int64_t ni,
+                         const int64_t* sp, const int32_t* sc, int64_t* oi, float* os, int n_split,
+                         hipStream_t s) {
+  TopkParams p{u, 64, nb, v, 64, ni, sp, sc, 20, oi, os, n_split};
+  const dim3 g((unsigned)((nb + 63) / 64), (unsigned)n_split), b(kBlock);
+  switch (mode) {
+    case 0: hipLaunchKernelGGL((xtopk<64, 32, 0>), g, b, 0, s, p); break;
+    case 1: hipLaunchKernelGGL((xtopk<64, 32, 1>), g, b, 0, s, p); break;
+    case 2: hipLaunchKernelGGL((xtopk<64, 32, 2>), g, b, 0, s, p); break;
+    case 3: hipLaunchKernelGGL((xtopk<64, 32, 3>), g, b, 0, s, p); break;
+    default: return -1;
   }
-  if (rc != GNNREC_OK || !split) return rc;
-  hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)ceil_div(n_users_batch, kBlock / 64)),
-                     dim3(kBlock), 0, s, work_idx, work_score, n_users_batch, n_split, k, out_idx,
-                     out_score);
-  return check_launch("topk_merge");
-}
-
-extern "C" int gnnrec_score_topk_f32(const float* u, int64_t ldu, int64_t n_users_batch,
-                                     const float* v, int64_t ldv, int64_t n_items, int32_t d,
-                                     const int64_t* seen_ptr, const int32_t* seen_col, int32_t k,
-                                     int64_t* out_idx, float* out_score, gnnrec_stream_t stream) {
-  return gnnrec_score_topk_split_f32(u, ldu, n_users_batch, v, ldv, n_items, d, seen_ptr, seen_col,
-                                     k, 1, nullptr, nullptr, out_idx, out_score, stream);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
 }
