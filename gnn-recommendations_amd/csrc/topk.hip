@@ -6,9 +6,9 @@
 //   * scores on the matrix cores: v_mfma_f32_16x16x4_f32 is an exact k-ordered fmaf chain,
 //     and the k-steps are issued in ascending k, so score[b,i] is bit-identical to
 //     `acc = 0; for f in 0..d-1: acc = fmaf(u[b,f], v[i,f], acc)` (the oracle's definition);
-//   * a per-user top-K list lives in LDS; a candidate enters only if it beats the list's
-//     current worst entry under the fixed order (score desc, item index asc), so after the
-//     first tiles almost no lane does more than one compare per score;
+//   * a per-user top-K list lives in LDS as a heap rooted at its worst entry under the fixed
+//     order (score desc, item index asc); a candidate enters only if it beats the root, so
+//     after the first tiles a tile costs one register compare per score and one ballot;
 //   * seen items are masked lazily: only a candidate that would enter the list is looked up
 //     (binary search in the user's sorted seen list) and, if seen, re-scored as -inf.
 // Workgroup = 4 waves = 64 users (16 per wave); item tiles of 64 rows are staged in LDS
@@ -55,25 +55,31 @@ __device__ __forceinline__ bool is_seen(const TopkParams& p, int64_t user, int i
   return false;
 }
 
-// Wave-wide: position of the worst entry of one user's list (entries [0, KM)).
+// One user's list is a binary heap over KM slots whose root is the list's WORST entry under
+// the output order (score desc, item asc). Replacing the root by a better candidate and
+// sifting it down keeps that invariant in log2(KM) steps of one lane (the previous design
+// re-scanned the whole list with wave shuffles after every insertion).
 template <int KM>
-__device__ __forceinline__ int find_worst(const float* ls, const int* li, int lane) {
-  float ws = INFINITY;
-  int wi = -1, wp = 0;
-  for (int e = lane; e < KM; e += 64) {
-    const float s = ls[e];
-    const int i = li[e];
-    if (wi == -1 || better(ws, wi, s, i)) { ws = s; wi = i; wp = e; }
+__device__ __forceinline__ void heap_replace_root(float* hs, int* hi, float cs, int ci) {
+  int pos = 0;
+  while (true) {
+    const int l = 2 * pos + 1, r = l + 1;
+    if (l >= KM) break;
+    int w = l;                        // the worse child
+    float wsc = hs[l];
+    int wit = hi[l];
+    if (r < KM) {
+      const float rs = hs[r];
+      const int ri = hi[r];
+      if (better(wsc, wit, rs, ri)) { w = r; wsc = rs; wit = ri; }
+    }
+    if (!better(cs, ci, wsc, wit)) break;  // the worse child is not worse than the candidate
+    hs[pos] = wsc;
+    hi[pos] = wit;
+    pos = w;
   }
-  for (int off = 32; off >= 1; off >>= 1) {
-    const float os = __shfl_xor(ws, off, 64);
-    const int oi = __shfl_xor(wi, off, 64);
-    const int op = __shfl_xor(wp, off, 64);
-    const bool take = (wi == -1) || (oi != -1 && better(ws, wi, os, oi)) ||
-                      (oi != -1 && ws == os && wi == oi && op < wp);
-    if (take) { ws = os; wi = oi; wp = op; }
-  }
-  return __shfl(wp, 0, 64);
+  hs[pos] = cs;
+  hi[pos] = ci;
 }
 
 template <int D, int KM>
@@ -86,9 +92,6 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
   __shared__ __attribute__((aligned(16))) float v_lds[2][TI * LDV];
   __shared__ float l_score[UPB][KM];
   __shared__ int l_item[UPB][KM];
-  __shared__ float l_worst_s[UPB];
-  __shared__ int l_worst_i[UPB];
-  __shared__ int l_worst_p[UPB];
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i16 = lane & 15, k4 = lane >> 4;
@@ -107,11 +110,6 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
   for (int e = threadIdx.x; e < UPB * KM; e += kBlock) {
     l_score[e / KM][e % KM] = -INFINITY;
     l_item[e / KM][e % KM] = INT_MAX;  // sentinel: loses to every real item
-  }
-  for (int e = threadIdx.x; e < UPB; e += kBlock) {
-    l_worst_s[e] = -INFINITY;
-    l_worst_i[e] = INT_MAX;
-    l_worst_p[e] = 0;
   }
 
   // item tiles are double-buffered: the global loads of tile t+1 are in flight while the
@@ -165,8 +163,8 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
     bool any = false;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      ws[q] = l_worst_s[16 * wave + 4 * k4 + q];
-      wi[q] = l_worst_i[16 * wave + 4 * k4 + q];
+      ws[q] = l_score[16 * wave + 4 * k4 + q][0];   // heap roots = current worst
+      wi[q] = l_item[16 * wave + 4 * k4 + q][0];
     }
 #pragma unroll
     for (int nt = 0; nt < TI / 16; ++nt)
@@ -189,33 +187,26 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
         const float s = acc[nt][q];
         const int item = (int)item64;
         bool cand = user < p.nb && item64 < i_end &&
-                    better(s, item, l_worst_s[ul], l_worst_i[ul]);
-        // serialize the (rare) insertions of this wave, one candidate at a time
-        unsigned long long m = __ballot(cand);
-        while (m) {
-          const int src = __ffsll((long long)m) - 1;
-          m &= m - 1;
-          const int cu = __shfl(ul, src, 64);
-          const int ci = __shfl(item, src, 64);
-          float cs = __shfl(s, src, 64);
-          if (is_seen(p, ub + cu, ci)) cs = -INFINITY;
-          if (better(cs, ci, l_worst_s[cu], l_worst_i[cu])) {
-            if (lane == 0) {
-              const int wp = l_worst_p[cu];
-              l_score[cu][wp] = cs;
-              l_item[cu][wp] = ci;
-            }
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            __builtin_amdgcn_wave_barrier();
-            const int wp = find_worst<KM>(&l_score[cu][0], &l_item[cu][0], lane);
-            if (lane == 0) {
-              l_worst_s[cu] = l_score[cu][wp];
-              l_worst_i[cu] = l_item[cu][wp];
-              l_worst_p[cu] = wp;
-            }
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            __builtin_amdgcn_wave_barrier();
+                    better(s, item, l_score[ul][0], l_item[ul][0]);
+        const unsigned long long m = __ballot(cand);
+        if (m == 0) continue;
+        // the 16 lanes of group k4 share user ul; group leader (i16 == 0) inserts the group's
+        // candidates into that user's heap one by one — the four groups work in parallel
+        unsigned grp = (unsigned)(m >> (16 * k4)) & 0xffffu;
+        while (__ballot(grp != 0)) {
+          const bool has = grp != 0;
+          const int src = has ? __ffs(grp) - 1 : 0;
+          grp &= grp - 1;
+          const int src_lane = 16 * k4 + src;
+          float cs = __shfl(s, src_lane, 64);
+          const int ci = __shfl(item, src_lane, 64);
+          if (i16 == 0 && has) {
+            if (is_seen(p, user, ci)) cs = -INFINITY;
+            if (better(cs, ci, l_score[ul][0], l_item[ul][0]))
+              heap_replace_root<KM>(&l_score[ul][0], &l_item[ul][0], cs, ci);
           }
+          __builtin_amdgcn_s_waitcnt(0xc07f);
+          __builtin_amdgcn_wave_barrier();
         }
       }
     }
