@@ -143,7 +143,7 @@ __global__ __launch_bounds__(kBlock) void xtopk(TopkParams p) {
     // tile after one ballot unless some lane has a candidate.
     float ws[4];
     int wi[4];
-    bool any = false;
+    unsigned cmask = 0;   // bit 4*nt + q: (item, user q) passes the register filter
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       ws[q] = l_score[16 * wave + 4 * k4 + q][0];   // heap roots = current worst
@@ -157,9 +157,11 @@ __global__ __launch_bounds__(kBlock) void xtopk(TopkParams p) {
         if (sc != sc) sc = -INFINITY;  // NaN scores rank last
         acc[nt][q] = sc;
         const int64_t item64 = t0 + 16 * nt + i16;
-        any |= item64 < i_end && better(sc, (int)item64, ws[q], wi[q]);
+        if (item64 < i_end && ub + 16 * wave + 4 * k4 + q < p.nb &&
+            better(sc, (int)item64, ws[q], wi[q]))
+          cmask |= 1u << (4 * nt + q);
       }
-    if (__ballot(any && ub + 16 * wave + 4 * k4 < p.nb) == 0) continue;
+    if (__ballot(cmask != 0) == 0) continue;
 #pragma unroll
     for (int nt = 0; nt < TI / 16; ++nt) {
 #pragma unroll
@@ -169,9 +171,8 @@ __global__ __launch_bounds__(kBlock) void xtopk(TopkParams p) {
         const int64_t item64 = t0 + 16 * nt + i16;
         const float s = acc[nt][q];
         const int item = (int)item64;
-        bool cand = user < p.nb && item64 < i_end &&
-                    better(s, item, l_score[ul][0], l_item[ul][0]);
-        const unsigned long long m = __ballot(cand);
+        // (the leader re-checks each candidate against the heap root, which only rises)
+        const unsigned long long m = __ballot((cmask >> (4 * nt + q)) & 1u);
         if (m == 0) continue;
         // the 16 lanes of group k4 share user ul; group leader (i16 == 0) inserts the group's
         // candidates into that user's heap one by one — the four groups work in parallel
