@@ -174,8 +174,9 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
         if (sc != sc) sc = -INFINITY;  // NaN scores rank last
         acc[nt][q] = sc;
         const int64_t item64 = t0 + 16 * nt + i16;
-        if (item64 < i_end && ub + 16 * wave + 4 * k4 + q < p.nb &&
-            better(sc, (int)item64, ws[q], wi[q]))
+        // >= : a superset of better() (ties are settled by the leader's exact check)
+        if (sc >= ws[q] && item64 < i_end && ub + 16 * wave + 4 * k4 + q < p.nb &&
+            (sc > ws[q] || (int)item64 < wi[q]))
           cmask |= 1u << (4 * nt + q);
       }
     if (__ballot(cmask != 0) == 0) continue;
@@ -201,7 +202,9 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
           const int src_lane = 16 * k4 + src;
           float cs = __shfl(s, src_lane, 64);
           const int ci = __shfl(item, src_lane, 64);
-          if (i16 == 0 && has) {
+          if (i16 == 0 && has && better(cs, ci, l_score[ul][0], l_item[ul][0])) {
+            // the seen lookup (a binary search in HBM) only for a candidate that would enter;
+            // a masked item scores -inf and still enters if the root is an empty slot
             if (is_seen(p, user, ci)) cs = -INFINITY;
             if (better(cs, ci, l_score[ul][0], l_item[ul][0]))
               heap_replace_root<KM>(&l_score[ul][0], &l_item[ul][0], cs, ci);
