@@ -9,8 +9,9 @@
 //   * a per-user top-K list lives in LDS as a heap rooted at its worst entry under the fixed
 //     order (score desc, item index asc); a candidate enters only if it beats the root, so
 //     after the first tiles a tile costs one register compare per score and one ballot;
-//   * seen items are masked lazily: only a candidate that would enter the list is looked up
-//     (binary search in the user's sorted seen list) and, if seen, re-scored as -inf.
+//   * seen items are masked lazily: only a candidate that would enter the list is looked up,
+//     through a per-user cursor into its sorted seen list that only moves forward (the
+//     candidates of a user arrive in ascending item order), and, if seen, re-scored as -inf.
 // Workgroup = 4 waves = 64 users (16 per wave); item tiles of 64 rows are staged in LDS
 // ([64][d+2]: d+2 == 2 mod 32 makes the B-fragment reads conflict-free) and reused by the
 // four waves.
@@ -43,17 +44,6 @@ __device__ __forceinline__ bool better(float sa, int ia, float sb, int ib) {
   return sa > sb || (sa == sb && ia < ib);
 }
 
-__device__ __forceinline__ bool is_seen(const TopkParams& p, int64_t user, int item) {
-  if (!p.seen_ptr) return false;
-  int64_t lo = p.seen_ptr[user], hi = p.seen_ptr[user + 1];
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    const int c = p.seen_col[mid];
-    if (c == item) return true;
-    if (c < item) lo = mid + 1; else hi = mid;
-  }
-  return false;
-}
 
 // One user's list is a binary heap over KM slots whose root is the list's WORST entry under
 // the output order (score desc, item asc). Replacing the root by a better candidate and
@@ -92,6 +82,8 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
   __shared__ __attribute__((aligned(16))) float v_lds[2][TI * LDV];
   __shared__ float l_score[UPB][KM];
   __shared__ int l_item[UPB][KM];
+  __shared__ int64_t s_cur[UPB];   // per user: cursor into its sorted seen list ...
+  __shared__ int s_val[UPB];       // ... and the item there (INT_MAX when exhausted)
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i16 = lane & 15, k4 = lane >> 4;
@@ -110,6 +102,24 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
   for (int e = threadIdx.x; e < UPB * KM; e += kBlock) {
     l_score[e / KM][e % KM] = -INFINITY;
     l_item[e / KM][e % KM] = INT_MAX;  // sentinel: loses to every real item
+  }
+  // A user's candidates reach its list in ascending item order (tiles ascend, and inside a
+  // tile nt then i16 ascend), so the seen test is a cursor that only moves forward: set it
+  // to the first seen item >= this workgroup's range start.
+  for (int e = threadIdx.x; e < UPB; e += kBlock) {
+    int64_t lo = 0, hi = 0;
+    if (p.seen_ptr && ub + e < p.nb) {
+      lo = p.seen_ptr[ub + e];
+      hi = p.seen_ptr[ub + e + 1];
+      const int64_t last = hi;
+      while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (p.seen_col[mid] < i_beg) lo = mid + 1; else hi = mid;
+      }
+      hi = last;
+    }
+    s_cur[e] = lo;
+    s_val[e] = lo < hi ? p.seen_col[lo] : INT_MAX;
   }
 
   // item tiles are double-buffered: the global loads of tile t+1 are in flight while the
@@ -205,7 +215,18 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
           if (i16 == 0 && has && better(cs, ci, l_score[ul][0], l_item[ul][0])) {
             // the seen lookup (a binary search in HBM) only for a candidate that would enter;
             // a masked item scores -inf and still enters if the root is an empty slot
-            if (is_seen(p, user, ci)) cs = -INFINITY;
+            int64_t cur = s_cur[ul];
+            int sv = s_val[ul];
+            if (sv < ci) {
+              const int64_t end = p.seen_ptr[user + 1];
+              do {
+                ++cur;
+                sv = cur < end ? p.seen_col[cur] : INT_MAX;
+              } while (sv < ci);
+              s_cur[ul] = cur;
+              s_val[ul] = sv;
+            }
+            if (sv == ci) cs = -INFINITY;
             if (better(cs, ci, l_score[ul][0], l_item[ul][0]))
               heap_replace_root<KM>(&l_score[ul][0], &l_item[ul][0], cs, ci);
           }
