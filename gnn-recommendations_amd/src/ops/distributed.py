@@ -261,7 +261,7 @@ def gather_rows(dg: DistributedGraph, local: torch.Tensor) -> torch.Tensor:
 
 def _exchanged(dg: DistributedGraph, local: torch.Tensor) -> torch.Tensor:
     """This rank's [n_local, w] rows -> the padded gather table [world*rows_pad, w] holding
-    every row this rank's shard references (one exchange)."""
+    every row this rank's shard references plus its own rows (one exchange)."""
     if dg.world == 1:
         return local
     piece = torch.zeros((dg.rows_pad, local.shape[1]), dtype=local.dtype, device=local.device)
@@ -269,7 +269,8 @@ def _exchanged(dg: DistributedGraph, local: torch.Tensor) -> torch.Tensor:
     table = torch.zeros((dg.world * dg.rows_pad, local.shape[1]), dtype=local.dtype,
                         device=local.device)
     dg.exchange(table, piece)
-    return table
+    dg.local_slice(table).copy_(local)   # own rows too (the point-to-point form skips them
+    return table                         # when the shard does not reference them)
 
 
 def _native_ngcf_layer(shard, x_in, x_self, layer, gs, out):

@@ -1,6 +1,7 @@
 from .losses import BCELoss, BPRLoss, RegularizedLoss
 from .sampler import DeviceSampler, ReferenceSampler
 from .trainer import Trainer, bpr_scores, train_step
+from .distributed import lightgcn_train_step_dist
 
 __all__ = ["BPRLoss", "BCELoss", "RegularizedLoss", "DeviceSampler", "ReferenceSampler",
-           "Trainer", "bpr_scores", "train_step"]
+           "Trainer", "bpr_scores", "train_step", "lightgcn_train_step_dist"]

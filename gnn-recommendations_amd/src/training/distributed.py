@@ -1,0 +1,89 @@
+"""Row-sharded LightGCN BPR training step (SURVEY §8e "Training (next)" + §8f1).
+
+The embedding table x0 = cat(user_embedding, item_embedding) is split by destination rows
+exactly like the operand (DistributedGraph): rank p owns rows [b_p, b_{p+1}) of x0 as its
+own parameter shard and its Adam state. One step (the body of trainer.py:248-279):
+
+  forward   x0 rows exchanged once (each rank receives the rows its shard references), then
+            the K-hop propagation with its per-hop exchanges (lightgcn_propagate_dist);
+  loss      the batch (identical on every rank: same sampler seed) needs the output rows of
+            its users / positives / negatives; every rank writes the rows it owns into a
+            [3B, d] buffer of zeros and one all_reduce(SUM) completes it (x + 0 = x: exact);
+            every rank then evaluates the same BPR loss ([B, B] broadcast kept) and its
+            gradient with respect to those rows;
+  backward  each rank scatters the gradient rows it owns into dY, and the gradient of x0 is
+            the SAME propagation applied to dY (A^T = A): mean_k A^k dY, sharded the same way;
+  update    clip_grad_norm_ over the global norm (one all_reduce of the squared norm), then
+            Adam on the local shard (element-wise, so identical to the single-device update
+            of those rows).
+
+No all-reduce of the embedding gradient is needed: the table is row-sharded, not replicated.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops.distributed import DistributedGraph, _exchanged, lightgcn_propagate_dist
+from .losses import BPRLoss
+
+
+def _all_reduce(t: torch.Tensor, dg: DistributedGraph) -> torch.Tensor:
+    if dg.world == 1:
+        return t
+    if t.is_cuda and dist.get_backend(dg.group) == "gloo":   # 1-GPU test harness
+        h = t.cpu()
+        dist.all_reduce(h, group=dg.group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, group=dg.group)
+    return t
+
+
+def lightgcn_train_step_dist(dg: DistributedGraph, emb_local: torch.nn.Parameter, n_layers: int,
+                             n_users: int, users: torch.Tensor, pos_items: torch.Tensor,
+                             neg_items: torch.Tensor, optimizer: torch.optim.Optimizer,
+                             loss_fn: Optional[torch.nn.Module] = None,
+                             max_grad_norm: float = 1.0,
+                             hop_fn: Optional[Callable] = None) -> torch.Tensor:
+    """One BPR step on this rank's shard; returns the (replicated) loss as a 0-d tensor.
+    emb_local: this rank's rows [row_begin, row_end) of x0 (a leaf Parameter the optimizer
+    owns). users / pos_items / neg_items: the same batch on every rank (global ids; items
+    counted from 0 as in the reference). hop_fn: the local hop (default: the native SpMM)."""
+    loss_fn = loss_fn or BPRLoss()
+    dev = emb_local.device
+    b0, b1 = dg.row_begin, dg.row_end
+    with torch.no_grad():
+        x0_pad = _exchanged(dg, emb_local.detach())
+        out_local = lightgcn_propagate_dist(dg, x0_pad, n_layers, hop_fn=hop_fn)
+        B = users.numel()
+        neg2 = neg_items.view(B, -1)
+        ids = torch.cat([users.view(-1), n_users + pos_items.view(-1),
+                         n_users + neg2.reshape(-1)]).to(dev)
+        mine = (ids >= b0) & (ids < b1)
+        rows = torch.zeros((ids.numel(), emb_local.shape[1]), dtype=emb_local.dtype, device=dev)
+        rows[mine] = out_local[ids[mine] - b0]
+        _all_reduce(rows, dg)
+    rb = rows.requires_grad_(True)
+    u, p, n = rb[:B], rb[B:2 * B], rb[2 * B:].view(B, neg2.shape[1], -1)
+    pos_s = (u * p).sum(dim=1)
+    neg_s = (u.unsqueeze(1) * n).sum(dim=2)
+    if neg_items.dim() == 1:
+        neg_s = neg_s.view(B)
+    loss = loss_fn(pos_s, neg_s)
+    loss.backward()
+    with torch.no_grad():
+        dy = torch.zeros_like(emb_local)
+        dy.index_add_(0, ids[mine] - b0, rb.grad[mine])
+        grad = lightgcn_propagate_dist(dg, _exchanged(dg, dy), n_layers, hop_fn=hop_fn)
+        if max_grad_norm > 0:
+            sq = (grad.double() ** 2).sum().view(1)
+            _all_reduce(sq, dg)
+            coef = torch.clamp(max_grad_norm / (sq.sqrt() + 1e-6), max=1.0).to(grad.dtype)
+            grad.mul_(coef)
+    optimizer.zero_grad()
+    emb_local.grad = grad
+    optimizer.step()
+    return loss.detach()

@@ -15,7 +15,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import oracle
-from conftest import golden_csr
+from conftest import golden_csr, load_golden
 
 from src.ops import CsrGraph
 from src.ops._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT, EPI_NO_Y
@@ -186,3 +186,55 @@ def test_sharded_model_forward_matches_single_device(kind, world):
     np.testing.assert_allclose(whole, single, rtol=0, atol=1e-6)
     # and the stand-in layers reproduce the model's own (reference) forward
     np.testing.assert_allclose(single, ref, rtol=0, atol=2e-6)
+
+
+# ---- row-sharded BPR training step (§8e training + §8f1) ---------------------------------
+def _train_worker(rank, world, port, q):
+    from src.models import LightGCN
+    from src.ops.distributed import gather_rows
+    from src.training import lightgcn_train_step_dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        f = load_golden("bpr_train_K3_d64")
+        rp, col, val, nu, ni = golden_csr("g_small")
+        full = CsrGraph(torch.from_numpy(rp), torch.from_numpy(col), torch.from_numpy(val),
+                        (rp.size - 1, rp.size - 1), nu, ni, True)
+        torch.manual_seed(56)
+        m = LightGCN(nu, ni, embedding_dim=64, n_layers=3, init_scale=0.1)
+        x0 = torch.cat([m.user_embedding.weight, m.item_embedding.weight]).detach()
+        dg = DistributedGraph(full, rank, world, "cpu")
+        emb = torch.nn.Parameter(x0[dg.row_begin:dg.row_end].clone())
+        opt = torch.optim.Adam([emb], lr=1e-2, weight_decay=1e-4)
+        losses = []
+        for b in range(3):
+            args = [torch.from_numpy(f[k][b]) for k in ("users", "pos", "neg")]
+            losses.append(float(lightgcn_train_step_dist(dg, emb, 3, nu, *args, opt,
+                                                         hop_fn=cpu_hop)))
+        table = gather_rows(dg, emb.detach())
+        if rank == 0:
+            q.put((np.array(losses), table[:nu].numpy(), table[nu:].numpy()))
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_sharded_training_matches_reference_trainer(world):
+    """Three Adam steps of the row-sharded step reproduce the reference trainer's golden
+    (tests/golden/bpr_train_K3_d64.npz, made by running its own code) at every world size."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_train_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    losses, uw, iw = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    f = load_golden("bpr_train_K3_d64")
+    np.testing.assert_allclose(losses, f["losses"], rtol=1e-6)
+    np.testing.assert_allclose(uw, f["user_w"], atol=1e-6)
+    np.testing.assert_allclose(iw, f["item_w"], atol=1e-6)

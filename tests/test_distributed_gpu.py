@@ -35,7 +35,7 @@ def _graph():
 def _model(kind, nu, ni, dev):
     from src.models import GAT, LightGCN, NGCFGroupShuffle
     torch.manual_seed(7)
-    if kind == "lightgcn":
+    if kind in ("lightgcn", "train"):
         m = LightGCN(nu, ni, 64, 3, 0.1)
     elif kind == "ngcf_gs":
         m = NGCFGroupShuffle(nu, ni, 64, [64, 64, 64], 0.1, 0.1, 8, 0.3)
@@ -60,6 +60,25 @@ def _worker(rank, world, port, kind, exchange, q):
         with torch.no_grad():
             dg = DistributedGraph(full, rank, world, dev, exchange=exchange)
             x0p = dg.pad_table(m._initial_table())
+            if kind == "train":   # one BPR step on the shard, then the updated rows
+                from src.training import lightgcn_train_step_dist
+                emb = torch.nn.Parameter(dg.local_slice(x0p).clone())
+                opt = torch.optim.Adam([emb], lr=1e-2)
+                gen = torch.Generator().manual_seed(3)
+                bu = torch.randint(0, nu, (256,), generator=gen)
+                bp = torch.randint(0, ni, (256,), generator=gen)
+                bn = torch.randint(0, ni, (256, 1), generator=gen)
+                with torch.enable_grad():
+                    lightgcn_train_step_dist(dg, emb, 3, nu, bu, bp, bn, opt)
+                mine = emb.detach()
+                one = DistributedGraph(full, 0, 1, dev)
+                emb1 = torch.nn.Parameter(m._initial_table().clone())
+                opt1 = torch.optim.Adam([emb1], lr=1e-2)
+                with torch.enable_grad():
+                    lightgcn_train_step_dist(one, emb1, 3, nu, bu, bp, bn, opt1)
+                q.put((rank, mine.cpu().numpy(), emb1.detach()[dg.row_begin:dg.row_end].cpu().numpy(),
+                       dg.exchange_mode))
+                return
             if kind == "lightgcn":
                 mine = lightgcn_propagate_dist(dg, x0p, 3, overlap_chunks=3)
             elif kind == "ngcf_gs":
@@ -74,7 +93,8 @@ def _worker(rank, world, port, kind, exchange, q):
 
 
 @pytest.mark.parametrize("kind,exchange", [("lightgcn", "p2p"), ("lightgcn", "allgather"),
-                                           ("ngcf_gs", "auto"), ("gat", "auto")])
+                                           ("ngcf_gs", "auto"), ("gat", "auto"),
+                                           ("train", "auto")])
 def test_two_ranks_native_match_single_device(cuda, kind, exchange):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -89,7 +109,7 @@ def test_two_ranks_native_match_single_device(cuda, kind, exchange):
     for rank, mine, ref, mode in res:
         assert mine.shape == ref.shape and mine.shape[0] > 0
         assert np.isfinite(mine).all()
-        if kind == "gat":
+        if kind in ("gat", "train"):   # train: the clip norm is summed across ranks
             np.testing.assert_allclose(mine, ref, rtol=0, atol=1e-5)
         else:
             np.testing.assert_array_equal(mine.view(np.uint32), ref.view(np.uint32))

@@ -44,3 +44,26 @@ def test_trainer_native(cuda):
     res = t.train()
     assert res["train_losses"][-1] < res["train_losses"][0]
     assert res["valid_metrics"][0]["recall@10"] >= 0.0
+
+
+def test_sharded_step_world1_native_matches_reference(cuda):
+    """lightgcn_train_step_dist on one device (native hops) vs the reference trainer golden."""
+    from conftest import load_golden
+    from src.models import LightGCN
+    from src.ops.distributed import DistributedGraph
+    from src.training import lightgcn_train_step_dist
+    f = load_golden("bpr_train_K3_d64")
+    g, nu, ni = _golden_graph()
+    torch.manual_seed(56)
+    m = LightGCN(nu, ni, embedding_dim=64, n_layers=3, init_scale=0.1)
+    x0 = torch.cat([m.user_embedding.weight, m.item_embedding.weight]).detach()
+    dg = DistributedGraph(g, 0, 1, cuda)
+    emb = torch.nn.Parameter(x0.to(cuda).clone())
+    opt = torch.optim.Adam([emb], lr=1e-2, weight_decay=1e-4)
+    losses = [float(lightgcn_train_step_dist(dg, emb, 3, nu,
+                                             *[torch.from_numpy(f[k][b]).to(cuda)
+                                               for k in ("users", "pos", "neg")], opt))
+              for b in range(3)]
+    np.testing.assert_allclose(losses, f["losses"], rtol=1e-5)
+    np.testing.assert_allclose(emb.detach()[:nu].cpu().numpy(), f["user_w"], atol=2e-5)
+    np.testing.assert_allclose(emb.detach()[nu:].cpu().numpy(), f["item_w"], atol=2e-5)

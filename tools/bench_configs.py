@@ -16,6 +16,8 @@
      resident in HBM -> normalised CSR in HBM) vs the native host builder (1 GPU)
   8  full-catalogue scoring + seen mask + top-20 (1 GPU): 16 384 G100M users x
      1M items, d = 64, ~100 seen items per user; MFMA fp32 (exact k-ordered chain) TFLOP/s
+  9  G100M LightGCN K=3 d=64 BPR training step, row-sharded (src/training/distributed.py):
+     any N; the embedding table and its Adam state split by destination rows
   5  power-law bipartite graph, GAT d=64 4 heads K=3: by default a 2M x 2M, 50M-pair slice;
      --g1b: the full 10M x 10M, 1B-pair configuration (Zipf exponent 0.9, seed 0, every node
      degree >= 1)
@@ -159,7 +161,7 @@ def main(argv=None):
                   "nnz": g.nnz, "n_nodes": g.shape[0], "ms": t,
                   "edges_per_s": 3 * g.nnz / (t * 1e-3)})
         g100 = None
-        if 3 in a.configs or 4 in a.configs or (6 in a.configs and world == 1):
+        if 3 in a.configs or 4 in a.configs or 9 in a.configs or (6 in a.configs and world == 1):
             g100 = bench.build_graph(1_000_000, 1_000_000, 100_000_000, 0, threads)
         if 3 in a.configs:
             torch.manual_seed(0)
@@ -199,6 +201,29 @@ def main(argv=None):
                 del g1, u, i
             emit(rec)
             del m, dg, x0p, work, mine
+        if 9 in a.configs:
+            from src.training import lightgcn_train_step_dist
+            torch.manual_seed(0)
+            m = LightGCN(1_000_000, 1_000_000, 64, 3, 0.1)
+            dg = DistributedGraph(g100, rank, world, device)
+            x0 = m._initial_table().detach()
+            emb = torch.nn.Parameter(x0[dg.row_begin:dg.row_end].to(device).clone())
+            del m, x0
+            opt = torch.optim.Adam([emb], lr=1e-3, weight_decay=1e-4)
+            gen = torch.Generator().manual_seed(0)      # the same batches on every rank
+
+            def step9():
+                bu = torch.randint(0, 1_000_000, (2048,), generator=gen)
+                bp = torch.randint(0, 1_000_000, (2048,), generator=gen)
+                bn = torch.randint(0, 1_000_000, (2048, 1), generator=gen)
+                return lightgcn_train_step_dist(dg, emb, 3, 1_000_000, bu, bp, bn, opt)
+            with torch.enable_grad():
+                t, loss = timed(step9, a.steps, a.warmup, world, device)
+            emit({"config": 9, "workload": "G100M LightGCN K=3 d=64 BPR train step, row-sharded "
+                  "(batch 2048, fwd + bwd propagation with per-hop exchanges, sharded Adam)",
+                  "nnz": g100.nnz, "ms": t, "edges_per_s": 2 * 3 * g100.nnz / (t * 1e-3),
+                  "loss": float(loss), "exchange": dg.exchange_mode if world > 1 else None})
+            del dg, emb, opt
         if 6 in a.configs and world == 1:
             from src.training import BPRLoss, DeviceSampler, train_step
             torch.manual_seed(0)
