@@ -195,10 +195,12 @@ def main(argv=None) -> int:
     device = torch.device("cuda", local_rank % torch.cuda.device_count())
     torch.cuda.set_device(device)
     if world > 1:
+        from datetime import timedelta
+        # a stuck collective fails the run after 10 minutes instead of holding the node
         if a.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
+            dist.init_process_group("nccl", device_id=device, timeout=timedelta(minutes=10))
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timedelta(minutes=10))
 
     threads = max(1, host_threads() // max(1, world))
     t0 = time.perf_counter()

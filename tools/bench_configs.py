@@ -98,13 +98,6 @@ def timed(fn, steps, warmup, world, device):
     return float(t.item()), out
 
 
-def total(v, world, device):
-    t = torch.tensor([float(v)], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(t)
-    return float(t.item())
-
-
 def rank_max(v, world, device):
     t = torch.tensor([float(v)], dtype=torch.float64, device=device)
     if world > 1:
