@@ -12,8 +12,10 @@ LightGCN.forward (lightgcn.py:76-95), eval mode.
 
 One step = one full propagation (K SpMM hops with the layer mean fused into their
 epilogues) with the operand and x0 already resident in HBM. value = K * nnz / t_step
-(edges/s, every stored nonzero one directed message). N > 1: destination-row shards with
-one RCCL all-gather per hop over the SAME graph (strong scaling); t_step = max over ranks.
+(edges/s, every stored nonzero one directed message). N > 1: destination-row shards over the
+SAME graph (strong scaling) with one RCCL exchange per hop — all-gather, or bipartite
+point-to-point with 1/4/8 overlap chunks, whichever whole steps time fastest before the
+timed region (src/ops/distributed.py); t_step = max over ranks.
 
 Also reported: roofline of the dominant kernel (the SpMM hop) from HIP events around every
 hop launch inside the timed region, the PMC-measured HBM traffic per launch when a
