@@ -139,7 +139,26 @@ def cpu_baseline(g: CsrGraph, x0: torch.Tensor, n_users: int, reps: int = 2) -> 
         torch.sparse.mm(A, xc)
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
+    # the reference's graph build (scipy, graph_builder.py:16-174) on a 10M-pair sample
+    rng = np.random.default_rng(1)
+    su = rng.integers(0, n_users, 10_000_000)
+    si = rng.integers(0, g.shape[0] - n_users, 10_000_000)
+    t0 = time.perf_counter()
+    tr.scipy_operand(su, si, n_users, g.shape[0] - n_users)
+    t_build = time.perf_counter() - t0
+    cpu_model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {"value": nnz / t, "unit": "edges/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model,
+            "graph_build": {"pairs": 10_000_000, "seconds": t_build,
+                            "what": "scipy COO -> tocsr -> D^-1/2 A D^-1/2 -> torch COO "
+                                    "(oracle/torch_ref.scipy_operand)"},
             "sample": f"1 hop of torch.sparse.mm on the reference-layout uncoalesced COO "
                       f"(graph_builder.py:163-172) over the {n_users} user rows of A "
                       f"({nnz} nnz, half the operand) x full x0 [{g.shape[1]}, {x0.shape[1]}]; "

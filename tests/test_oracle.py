@@ -105,3 +105,17 @@ def test_gat_matches_reference():
     out = gat_forward_oracle(f, rp, col)
     np.testing.assert_allclose(out[:nu], f["user_out"], rtol=0, atol=2e-5)
     np.testing.assert_allclose(out[nu:], f["item_out"], rtol=0, atol=2e-5)
+
+
+def test_scipy_operand_restatement_matches_golden():
+    """oracle/torch_ref.scipy_operand (the CPU graph-build baseline) reproduces the reference's
+    normalised operand values on the golden graph."""
+    import oracle.torch_ref as tr
+    g = load_golden("graph_g_small")
+    t = tr.scipy_operand(g["users"], g["items"], int(g["n_users"]), int(g["n_items"]))
+    idx, val = t._indices().numpy(), t._values().numpy()
+    order = np.lexsort((idx[1], idx[0]))
+    ref = np.lexsort((g["col"], g["row"]))
+    np.testing.assert_array_equal(idx[0][order], g["row"][ref])
+    np.testing.assert_array_equal(idx[1][order], g["col"][ref])
+    np.testing.assert_array_equal(val[order].view(np.uint32), g["val"][ref].view(np.uint32))
