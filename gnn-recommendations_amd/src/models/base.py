@@ -50,3 +50,25 @@ class BaseRecommender(nn.Module):
 
     def _score_pairs(self, user_emb, item_emb, users, items) -> torch.Tensor:
         return (user_emb[users] * item_emb[items]).sum(dim=1)
+
+    def _serving_embeddings(self, *operands) -> Tuple[torch.Tensor, torch.Tensor]:
+        """get_all_embeddings(*operands) for predict(). The reference re-propagates the whole
+        graph on every predict call; in eval mode without autograd the result
+        depends only on the parameters and the operand, so it is cached until a parameter
+        changes in place (optimizer step) or another operand is passed — same values, and a
+        serving predict() costs a gather instead of K full hops."""
+        if self.training or torch.is_grad_enabled():
+            return self.get_all_embeddings(*operands)
+        from .orthogonal_bundle.group_shuffle_layer import param_key
+
+        def ident(o):
+            if o is None:
+                return None
+            rp = getattr(o, "row_ptr", None)
+            return (id(o), rp.data_ptr() if rp is not None else None,
+                    getattr(o, "nnz", None) if rp is not None else o.shape)
+        key = (param_key(list(self.parameters())), tuple(ident(o) for o in operands))
+        if getattr(self, "_serving_key", None) != key:
+            self._serving_cache = self.get_all_embeddings(*operands)
+            self._serving_key = key
+        return self._serving_cache

@@ -52,7 +52,7 @@ class LightGCN(BaseRecommender):
                 adj_matrix: Optional[torch.Tensor] = None) -> torch.Tensor:
         if adj_matrix is None:
             raise ValueError("adj_matrix must be given for LightGCN")
-        user_emb, item_emb = self.get_all_embeddings(adj_matrix)
+        user_emb, item_emb = self._serving_embeddings(adj_matrix)
         return self._score_pairs(user_emb, item_emb, users, items)
 
     def get_all_embeddings(self, adj_matrix=None) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -88,7 +88,7 @@ class NGCF(BaseRecommender):
     def predict(self, users, items, adj_matrix=None) -> torch.Tensor:
         if adj_matrix is None:
             raise ValueError("adj_matrix must be given for NGCF")
-        user_emb, item_emb = self.get_all_embeddings(adj_matrix)
+        user_emb, item_emb = self._serving_embeddings(adj_matrix)
         return self._score_pairs(user_emb, item_emb, users, items)
 
     def get_all_embeddings(self, adj_matrix=None) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -132,7 +132,7 @@ class OrthogonalBundleGNN(BaseRecommender):
         return out
 
     def predict(self, users, items, adj_matrix=None, edge_index=None) -> torch.Tensor:
-        user_emb, item_emb = self.get_all_embeddings(adj_matrix, edge_index)
+        user_emb, item_emb = self._serving_embeddings(adj_matrix, edge_index)
         return self._score_pairs(user_emb, item_emb, users, items)
 
     def get_all_embeddings(self, adj_matrix=None, edge_index=None):

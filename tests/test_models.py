@@ -165,3 +165,23 @@ def test_edge_specific_transport_cpu_matches_reference_formula():
         ref = parallel_transport_along_edges(x, ei, esbc(ei, et))
         out = esbc.transport(x, ei, et)
     torch.testing.assert_close(out, ref, rtol=0, atol=1e-6)
+
+
+def test_predict_serving_cache_tracks_parameters():
+    """predict() in eval/no-grad reuses the propagated tables until a parameter changes."""
+    rp, col, val, nu, ni = golden_csr("g_small")
+    g = CsrGraph(torch.from_numpy(rp), torch.from_numpy(col), torch.from_numpy(val),
+                 (rp.size - 1, rp.size - 1), nu, ni, True)
+    adj = g.to_torch_sparse_coo()
+    torch.manual_seed(0)
+    m = LightGCN(nu, ni, 32, 2, 0.1).eval()
+    users, items = torch.tensor([0, 5, 7]), torch.tensor([1, 2, 3])
+    with torch.no_grad():
+        a = m.predict(users, items, adj)
+        assert m._serving_cache is not None
+        b = m.predict(users, items, adj)
+        assert torch.equal(a, b)
+        m.user_embedding.weight.add_(0.5)          # in-place update: cache must refresh
+        c = m.predict(users, items, adj)
+        ue, ie = m.get_all_embeddings(adj)
+    assert torch.equal(c, (ue[users] * ie[items]).sum(1)) and not torch.equal(a, c)
