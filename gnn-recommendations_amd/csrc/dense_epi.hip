@@ -311,3 +311,53 @@ extern "C" int gnnrec_spmm_dense_f32(const int64_t* row_ptr, const int32_t* col,
   GNNREC_REQUIRE(!work || aligned16(work), "spmm_dense: work must be 16-B aligned");
   return run_dense<1>(p, d, work, as_hip(stream));
 }
+
+// Transform-only forms: the caller already holds n = A x (e.g. from gnnrec_spmm_csr_split_f32,
+// whose heavy-row kernel keeps power-law operands fast); the streaming MFMA kernel applies
+// the rest exactly as the split form of the two calls above.
+extern "C" int gnnrec_ngcf_transform_f32(int64_t n_rows, const float* n, int64_t ldn,
+                                         const float* x_self, int64_t ld_self, float* y,
+                                         int64_t ldy, int32_t d, const float* W1, const float* b1,
+                                         const float* W2, const float* b2, float slope,
+                                         const float* gas_blocks, const int32_t* gas_perm,
+                                         int32_t gas_bs, gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(n_rows >= 0, "ngcf_transform: n_rows < 0");
+  if (n_rows == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(W1 && b1 && W2 && b2, "ngcf_transform: null weights");
+  GNNREC_REQUIRE(ldn >= d && ld_self >= d && ldy >= d, "ngcf_transform: leading dimension < d");
+  GNNREC_REQUIRE(rows_ok(n, ldn) && rows_ok(x_self, ld_self) && rows_ok(y, ldy),
+                 "ngcf_transform: n/x_self/y must be 16-B aligned with ld %% 4 == 0");
+  if (gas_blocks) {
+    GNNREC_REQUIRE(gas_perm && gas_bs >= 1 && gas_bs <= 32 && d % gas_bs == 0,
+                   "ngcf_transform: bad GAS block size %d", gas_bs);
+  }
+  DenseParams p{};
+  p.A = Csr{nullptr, nullptr, nullptr, n_rows};
+  p.x = n; p.ldx = ldn; p.x_self = x_self; p.ld_self = ld_self; p.y = y; p.ldy = ldy;
+  p.W1 = W1; p.b1 = b1; p.W2 = W2; p.b2 = b2; p.slope = slope;
+  p.gas_blocks = gas_blocks; p.gas_perm = gas_perm; p.gas_bs = gas_bs;
+  return launch_dense<0, false>(p, d, as_hip(stream));
+}
+
+extern "C" int gnnrec_dense_transform_f32(int64_t n_rows, const float* n, int64_t ldn, float* y,
+                                          int64_t ldy, int32_t d, const float* M, float c_out,
+                                          const float* resid, int64_t ld_resid, float c_res,
+                                          float* acc, int64_t ld_acc, int32_t acc_mode,
+                                          float w_out, float w_res, gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(n_rows >= 0, "dense_transform: n_rows < 0");
+  if (n_rows == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(M, "dense_transform: null M");
+  GNNREC_REQUIRE(acc_mode >= 0 && acc_mode <= 2, "dense_transform: acc_mode must be 0, 1 or 2");
+  GNNREC_REQUIRE(y || acc_mode, "dense_transform: nothing to write");
+  GNNREC_REQUIRE(rows_ok(n, ldn) && ldn >= d, "dense_transform: n must be 16-B aligned, ld %% 4 == 0, ld >= d");
+  GNNREC_REQUIRE(resid ? (rows_ok(resid, ld_resid) && ld_resid >= d) : acc_mode != 1,
+                 "dense_transform: resid must be 16-B aligned with ld >= d (required by acc_mode 1)");
+  GNNREC_REQUIRE(!y || (rows_ok(y, ldy) && ldy >= d), "dense_transform: bad y");
+  GNNREC_REQUIRE(!acc_mode || (rows_ok(acc, ld_acc) && ld_acc >= d), "dense_transform: bad acc");
+  DenseParams p{};
+  p.A = Csr{nullptr, nullptr, nullptr, n_rows};
+  p.x = n; p.ldx = ldn; p.y = y; p.ldy = ldy;
+  p.M = M; p.c_out = c_out; p.c_res = c_res; p.resid = resid; p.ld_resid = ld_resid;
+  p.acc = acc; p.ld_acc = ld_acc; p.acc_mode = acc_mode; p.w_out = w_out; p.w_res = w_res;
+  return launch_dense<1, false>(p, d, as_hip(stream));
+}

@@ -221,12 +221,20 @@ def ngcf_layer(adj: CsrGraph, x: torch.Tensor, W1: torch.Tensor, b1: torch.Tenso
         gb = gas_blocks.detach().to(dev, torch.float32).contiguous()
         gp = gas_perm.to(dev, torch.int32).contiguous()
         bs = gb.shape[1]
-    work = None if fused else torch.empty((adj.n_rows, d), dtype=torch.float32, device=x.device)
-    check(_lib.lib().gnnrec_spmm_ngcf_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(x_self),
-                                          x_self.stride(0), ptr(y), d, d, ptr(w1), ptr(bb1),
-                                          ptr(w2), ptr(bb2), float(slope), ptr(gb), ptr(gp), bs,
-                                          ptr(work), _lib.stream_of(adj.device)),
-          "gnnrec_spmm_ngcf_f32")
+    stream = _lib.stream_of(adj.device)
+    if fused:
+        check(_lib.lib().gnnrec_spmm_ngcf_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(x_self),
+                                              x_self.stride(0), ptr(y), y.stride(0), d, ptr(w1),
+                                              ptr(bb1), ptr(w2), ptr(bb2), float(slope), ptr(gb),
+                                              ptr(gp), bs, None, stream), "gnnrec_spmm_ngcf_f32")
+        return y
+    # split form: the hop (heavy-row aware) into a scratch table, then the streaming transform
+    work = torch.empty((adj.n_rows, d), dtype=torch.float32, device=x.device)
+    spmm_into(adj, x, work)
+    check(_lib.lib().gnnrec_ngcf_transform_f32(adj.n_rows, ptr(work), d, ptr(x_self),
+                                               x_self.stride(0), ptr(y), y.stride(0), d, ptr(w1),
+                                               ptr(bb1), ptr(w2), ptr(bb2), float(slope), ptr(gb),
+                                               ptr(gp), bs, stream), "gnnrec_ngcf_transform_f32")
     return y
 
 
@@ -243,17 +251,18 @@ def dense_layer(adj: CsrGraph, x: torch.Tensor, M: torch.Tensor, c_out: float,
     if store_y and y is None:
         y = torch.empty((adj.n_rows, d), dtype=torch.float32, device=x.device)
     m = M.detach().to(x.device, torch.float32).contiguous()
-    check(_lib.lib().gnnrec_spmm_dense_f32(*_csr_args(adj), ptr(x), x.stride(0),
-                                           ptr(y if store_y else None), d, d, ptr(m),
-                                           float(c_out), ptr(resid),
-                                           resid.stride(0) if resid is not None else d,
-                                           float(c_res), ptr(acc),
-                                           acc.stride(0) if acc is not None else d,
-                                           int(acc_mode), float(w_out), float(w_res),
-                                           ptr(None if fused else torch.empty(
-                                               (adj.n_rows, d), dtype=torch.float32,
-                                               device=x.device)),
-                                           _lib.stream_of(adj.device)), "gnnrec_spmm_dense_f32")
+    tail = (ptr(y if store_y else None), y.stride(0) if store_y else d, d, ptr(m), float(c_out),
+            ptr(resid), resid.stride(0) if resid is not None else d, float(c_res), ptr(acc),
+            acc.stride(0) if acc is not None else d, int(acc_mode), float(w_out), float(w_res))
+    stream = _lib.stream_of(adj.device)
+    if fused:
+        check(_lib.lib().gnnrec_spmm_dense_f32(*_csr_args(adj), ptr(x), x.stride(0), *tail, None,
+                                               stream), "gnnrec_spmm_dense_f32")
+    else:  # split form: heavy-row aware hop into a scratch table, then the transform
+        work = torch.empty((adj.n_rows, d), dtype=torch.float32, device=x.device)
+        spmm_into(adj, x, work)
+        check(_lib.lib().gnnrec_dense_transform_f32(adj.n_rows, ptr(work), d, *tail, stream),
+              "gnnrec_dense_transform_f32")
     return y if store_y else None
 
 

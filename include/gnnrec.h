@@ -155,6 +155,20 @@ int gnnrec_spmm_dense_f32(const int64_t* row_ptr, const int32_t* col, const floa
                           int32_t acc_mode, float w_out, float w_res, float* work,
                           gnnrec_stream_t stream);
 
+/* Transform-only halves of the two calls above: `n` already holds A x (for instance from
+ * gnnrec_spmm_csr_split_f32, whose heavy-row kernel keeps power-law operands fast); the
+ * rest is applied exactly as in their split form. n: [n_rows, ldn]. */
+int gnnrec_ngcf_transform_f32(int64_t n_rows, const float* n, int64_t ldn, const float* x_self,
+                              int64_t ld_self, float* y, int64_t ldy, int32_t d, const float* W1,
+                              const float* b1, const float* W2, const float* b2, float slope,
+                              const float* gas_blocks, const int32_t* gas_perm, int32_t gas_bs,
+                              gnnrec_stream_t stream);
+
+int gnnrec_dense_transform_f32(int64_t n_rows, const float* n, int64_t ldn, float* y, int64_t ldy,
+                               int32_t d, const float* M, float c_out, const float* resid,
+                               int64_t ld_resid, float c_res, float* acc, int64_t ld_acc,
+                               int32_t acc_mode, float w_out, float w_res, gnnrec_stream_t stream);
+
 /* ---- a11: GAT sparse edge-softmax aggregation ---------------------------------------
  * Replaces the dense masked softmax + mm of GATLayer.forward (baselines/gat.py:99-149)
  * plus the F.elu between layers (gat.py:283) and the layer mean (gat.py:287-288):

@@ -293,3 +293,26 @@ def test_lightgcn_hipgraph_capture_replay(cuda):
     assert g.heavy_rows(256) is not None
     np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(ref2.cpu().numpy()))
     assert not torch.equal(ref, ref2)
+
+
+def test_ngcf_and_dense_split_forms_on_powerlaw_equal_fused(cuda):
+    """Split forms (heavy-row aware hop + transform-only kernel) == the fused kernels, bit for
+    bit, on an operand with rows far above the heavy threshold."""
+    g, _ = powerlaw_graph(21, cuda)
+    assert g.heavy_rows(256) is not None
+    torch.manual_seed(0)
+    n, d = g.shape[0], 64
+    x = torch.randn(n, d, device=cuda) * 0.1
+    W1, W2 = torch.randn(d, d, device=cuda) * 0.1, torch.randn(d, d, device=cuda) * 0.1
+    b1, b2 = torch.randn(d, device=cuda) * 0.01, torch.randn(d, device=cuda) * 0.01
+    blocks = torch.linalg.qr(torch.randn(8, 8, 8, device=cuda))[0]
+    perm = torch.randperm(d, device=cuda)
+    a = F.ngcf_layer(g, x, W1, b1, W2, b2, 0.2, gas_blocks=blocks, gas_perm=perm, fused=False)
+    b = F.ngcf_layer(g, x, W1, b1, W2, b2, 0.2, gas_blocks=blocks, gas_perm=perm, fused=True)
+    np.testing.assert_array_equal(bits(a.cpu().numpy()), bits(b.cpu().numpy()))
+    M = torch.randn(d, d, device=cuda) * 0.1
+    acc1, acc2 = torch.zeros_like(x), torch.zeros_like(x)
+    y1 = F.dense_layer(g, x, M, 0.9, x, 0.1, acc=acc1, acc_mode=1, w_out=0.3, w_res=0.2)
+    y2 = F.dense_layer(g, x, M, 0.9, x, 0.1, acc=acc2, acc_mode=1, w_out=0.3, w_res=0.2, fused=True)
+    np.testing.assert_array_equal(bits(y1.cpu().numpy()), bits(y2.cpu().numpy()))
+    np.testing.assert_array_equal(bits(acc1.cpu().numpy()), bits(acc2.cpu().numpy()))
