@@ -367,6 +367,11 @@ def main(argv=None) -> int:
                 "kernel": f"spmm_vec_kernel<{d}> (one launch per hop)",
                 "launch_ms": launch_ms,
                 "algorithmic_bytes_per_launch": launch_bytes,
+                # the same launch priced by its MEASURED memory-side traffic (PMC): how close
+                # the random row gather runs to the fabric/HBM rate
+                "traffic_gbps": (traffic / (launch_ms * 1e-3) / 1e9) if traffic else None,
+                "traffic_frac": (traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS)
+                if traffic else None,
             },
             "cpu_baseline": cpu,
             "edges_per_s_per_interaction": value / 2.0,
