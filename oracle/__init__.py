@@ -22,7 +22,7 @@ import numpy as np
 HERE = Path(__file__).resolve().parent
 SRC = HERE / "oracle.c"
 SO = HERE / "_build" / "liboracle.so"
-CFLAGS = ["-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared"]
+CFLAGS = ["-O2", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-shared", "-fopenmp"]
 
 _lib = None
 
