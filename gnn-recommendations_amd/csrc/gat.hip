@@ -131,6 +131,79 @@ __global__ __launch_bounds__(kBlock) void gat_kernel(GatParams p) {
   gat_finish<GROUP>(p, r, make_float4(a.x / l, a.y / l, a.z / l, a.w / l), gl);
 }
 
+// Shared-row mode (head_stride 0, no epilogue: the caller applies W_h afterwards): every
+// head aggregates the same O-wide row, so a row is owned by O/4 lanes that each load ONE
+// float4 of x per neighbour and keep H heads' online-softmax state for it (the generic
+// kernel would spread the heads over H times as many lanes that all load the same bytes).
+// Per (row, head, feature) the arithmetic is the generic kernel's, step for step.
+template <int O, int H, int CH>
+__global__ __launch_bounds__(kBlock) void gat_shared_kernel(GatParams p) {
+  constexpr int GROUP = O / 4;
+  constexpr int RPW = 64 / GROUP;
+  const int lane = threadIdx.x & 63;
+  const int gl = lane % GROUP;
+  const int64_t r = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
+  if (r >= p.A.n_rows) return;
+  const int64_t beg = p.A.row_ptr[r], end = p.A.row_ptr[r + 1];
+  if (p.max_row_len > 0 && end - beg > p.max_row_len) return;  // heavy row: split path
+  float ss[H], m[H], l[H];
+  float4 a[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    ss[h] = p.s_self[r * H + h];
+    m[h] = -INFINITY;
+    l[h] = 0.f;
+    a[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  for (int64_t k0 = beg; k0 < end; k0 += CH) {
+    constexpr int PER = (GROUP >= CH) ? 1 : CH / GROUP;
+    int cm[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      int64_t k = k0 + gl + (int64_t)q * GROUP;
+      k = k < end ? k : end - 1;
+      cm[q] = p.A.col[k];
+    }
+    float4 xv[CH];
+    float sn[CH][H];
+#pragma unroll
+    for (int t = 0; t < CH; ++t) {
+      const int c = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
+      xv[t] = ld4(p.h + (int64_t)c * p.ldh + 4 * gl);
+      if constexpr (H == 4) {
+        const float4 s4 = ld4(p.s_neigh + (int64_t)c * 4);
+        sn[t][0] = s4.x; sn[t][1] = s4.y; sn[t][2] = s4.z; sn[t][3] = s4.w;
+      } else {
+#pragma unroll
+        for (int h = 0; h < H; ++h) sn[t][h] = p.s_neigh[(int64_t)c * H + h];
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < CH; ++t) {
+      if (k0 + t < end) {
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+          float e = ss[h] + sn[t][h];
+          e = e > 0.f ? e : e * p.slope;
+          const float mn = fmaxf(m[h], e);
+          const float sc = expf(m[h] - mn);
+          const float pe = expf(e - mn);
+          l[h] = l[h] * sc + pe;
+          a[h].x = __builtin_fmaf(pe, xv[t].x, a[h].x * sc);
+          a[h].y = __builtin_fmaf(pe, xv[t].y, a[h].y * sc);
+          a[h].z = __builtin_fmaf(pe, xv[t].z, a[h].z * sc);
+          a[h].w = __builtin_fmaf(pe, xv[t].w, a[h].w * sc);
+          m[h] = mn;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h)
+    st4(p.out + r * p.ldo + h * O + 4 * gl,
+        make_float4(a[h].x / l[h], a[h].y / l[h], a[h].z / l[h], a[h].w / l[h]));
+}
+
 // Heavy rows, pass 1: one row group per segment -> partial (acc[F], m[H], l[H]).
 struct GatSplit {
   const int64_t* seg_row;
@@ -221,6 +294,17 @@ extern "C" int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* c
               mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, max_row_len};
   hipStream_t s = as_hip(stream);
   auto grid = [&](int f) { return dim3((unsigned)ceil_div(n_rows, (64 / (f / 4)) * (kBlock / 64))); };
+  const bool shared_fast = head_stride == 0 && heads == 4 && !mean_heads && !apply_elu && epi == 0 &&
+                           (o_dim == 16 || o_dim == 32 || o_dim == 64) && aligned16(s_neigh) &&
+                           aligned16(out);
+  if (shared_fast) {
+    switch (o_dim) {
+      case 16: hipLaunchKernelGGL((gat_shared_kernel<16, 4, 8>), grid(16), dim3(kBlock), 0, s, p); break;
+      case 32: hipLaunchKernelGGL((gat_shared_kernel<32, 4, 8>), grid(32), dim3(kBlock), 0, s, p); break;
+      default: hipLaunchKernelGGL((gat_shared_kernel<64, 4, 8>), grid(64), dim3(kBlock), 0, s, p); break;
+    }
+    return check_launch("gat_aggregate (shared rows)");
+  }
   switch (F) {
     case 16: hipLaunchKernelGGL(gat_kernel<16>, grid(16), dim3(kBlock), 0, s, p); break;
     case 32: hipLaunchKernelGGL(gat_kernel<32>, grid(32), dim3(kBlock), 0, s, p); break;
