@@ -115,11 +115,16 @@ __device__ __forceinline__ void stv(float* p, const VecF<N>& a) {
   }
 }
 
-template <int VEC, int GROUP, bool TAIL, int CH, bool NT = false>
+// xmask (optional): one byte per source row, 0 = the row is all zeros. Such a row is not
+// gathered and contributes 0: fmaf(v, +-0, acc) == acc for the finite operand values and the
+// accumulator that starts at +0, so the result is the same bits (sparse inputs, e.g. the
+// BPR gradient entering the backward propagation, skip almost every gather).
+template <int VEC, int GROUP, bool TAIL, int CH, bool NT = false, bool MASKED = false>
 __device__ __forceinline__ void gather_step_v(const int32_t* __restrict__ col,
                                               const float* __restrict__ val, int64_t k0,
                                               int64_t end, const float* __restrict__ x,
-                                              int64_t ldx, int gl, VecF<VEC>& a) {
+                                              int64_t ldx, int gl, VecF<VEC>& a,
+                                              const uint8_t* __restrict__ xmask = nullptr) {
   constexpr int PER = (GROUP >= CH) ? 1 : CH / GROUP;
   int cm[PER];
   float vm[PER];
@@ -140,7 +145,12 @@ __device__ __forceinline__ void gather_step_v(const int32_t* __restrict__ col,
 #pragma unroll
   for (int t = 0; t < CH; ++t) {
     const int c = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
-    xv[t] = ldv<VEC>(x + (int64_t)c * ldx + VEC * gl);
+    if (MASKED && xmask[c] == 0) {
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) xv[t].v[q] = 0.f;
+    } else {
+      xv[t] = ldv<VEC>(x + (int64_t)c * ldx + VEC * gl);
+    }
   }
 #pragma unroll
   for (int t = 0; t < CH; ++t) {
@@ -154,18 +164,20 @@ __device__ __forceinline__ void gather_step_v(const int32_t* __restrict__ col,
   }
 }
 
-template <int VEC, int GROUP, int CH, bool NT = false>
+template <int VEC, int GROUP, int CH, bool NT = false, bool MASKED = false>
 __device__ __forceinline__ VecF<VEC> gather_row_v(const int32_t* __restrict__ col,
                                                   const float* __restrict__ val, int64_t beg,
                                                   int64_t end, const float* __restrict__ x,
-                                                  int64_t ldx, int gl) {
+                                                  int64_t ldx, int gl,
+                                                  const uint8_t* __restrict__ xmask = nullptr) {
   VecF<VEC> a;
 #pragma unroll
   for (int q = 0; q < VEC; ++q) a.v[q] = 0.f;
   int64_t k0 = beg;
   for (; k0 + CH <= end; k0 += CH)
-    gather_step_v<VEC, GROUP, false, CH, NT>(col, val, k0, end, x, ldx, gl, a);
-  if (k0 < end) gather_step_v<VEC, GROUP, true, CH, NT>(col, val, k0, end, x, ldx, gl, a);
+    gather_step_v<VEC, GROUP, false, CH, NT, MASKED>(col, val, k0, end, x, ldx, gl, a, xmask);
+  if (k0 < end)
+    gather_step_v<VEC, GROUP, true, CH, NT, MASKED>(col, val, k0, end, x, ldx, gl, a, xmask);
   return a;
 }
 

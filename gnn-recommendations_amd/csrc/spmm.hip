@@ -11,11 +11,11 @@
 
 namespace gnnrec {
 
-template <int D>
+template <int D, bool MASKED = false>
 __global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
     Csr A, const float* __restrict__ x, int64_t ldx, float* __restrict__ y, int64_t ldy,
     int epi, const float* __restrict__ self, int64_t ld_self, float* __restrict__ acc,
-    int64_t ld_acc, float acc_div, int64_t skip_len) {
+    int64_t ld_acc, float acc_div, int64_t skip_len, const uint8_t* __restrict__ xmask) {
   constexpr int VEC = SpmmCfg<D>::VEC, CH = SpmmCfg<D>::CH;
   constexpr int GROUP = D / VEC;
   constexpr int RPW = 64 / GROUP;
@@ -26,7 +26,8 @@ __global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
   if (r >= A.n_rows) return;  // the whole group leaves together
   const int64_t beg = A.row_ptr[r], end = A.row_ptr[r + 1];
   if (skip_len > 0 && end - beg > skip_len) return;  // a heavy row: spmm_heavy_kernel's
-  const VecF<VEC> a = gather_row_v<VEC, GROUP, CH>(A.col, A.val, beg, end, x, ldx, gl);
+  const VecF<VEC> a = gather_row_v<VEC, GROUP, CH, false, MASKED>(A.col, A.val, beg, end, x, ldx,
+                                                                   gl, xmask);
   if (!(epi & GNNREC_EPI_NO_Y)) stv<VEC>(y + r * ldy + VEC * gl, a);
   acc_epilogue_v<VEC>(epi, a, self + r * ld_self + VEC * gl, acc + r * ld_acc + VEC * gl, acc_div);
 }
@@ -227,6 +228,20 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
   }
 }
 
+// mask[r] = 1 if row r of x has any element != 0 (NaN counts as non-zero), for the masked hop.
+__global__ __launch_bounds__(kBlock) void row_nonzero_kernel(const float* __restrict__ x,
+                                                             int64_t ldx, int64_t n_rows, int d,
+                                                             uint8_t* __restrict__ mask) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t r = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; r < n_rows;
+       r += ((int64_t)gridDim.x * kBlock) >> 6) {
+    bool nz = false;
+    for (int f = lane; f < d; f += 64) nz |= !(x[r * ldx + f] == 0.f);
+    const unsigned long long b = __ballot(nz);
+    if (lane == 0) mask[r] = b != 0 ? 1 : 0;
+  }
+}
+
 // MODE 0: standalone GAS of x rows. MODE 1: GAS(A x) (fused hop epilogue).
 template <int D, int MODE>
 __global__ __launch_bounds__(kBlock) void gas_kernel(Csr A, const float* __restrict__ x,
@@ -270,11 +285,15 @@ namespace {
 template <int D>
 void launch_spmm_vec4(const Csr& A, const float* x, int64_t ldx, float* y, int64_t ldy, int epi,
                       const float* self, int64_t ld_self, float* acc, int64_t ld_acc,
-                      float acc_div, int64_t skip, hipStream_t s) {
+                      float acc_div, int64_t skip, const uint8_t* xmask, hipStream_t s) {
   constexpr int RPB = (64 / (D / SpmmCfg<D>::VEC)) * (kBlock / 64);
   const int64_t grid = ceil_div(A.n_rows, RPB);
-  hipLaunchKernelGGL(spmm_vec_kernel<D>, dim3((unsigned)grid), dim3(kBlock), 0, s, A, x, ldx,
-                     y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip);
+  if (xmask)
+    hipLaunchKernelGGL((spmm_vec_kernel<D, true>), dim3((unsigned)grid), dim3(kBlock), 0, s, A, x,
+                       ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xmask);
+  else
+    hipLaunchKernelGGL((spmm_vec_kernel<D, false>), dim3((unsigned)grid), dim3(kBlock), 0, s, A, x,
+                       ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xmask);
 }
 
 bool vec4_ok(int d, const float* x, int64_t ldx, const float* y, int64_t ldy, int epi,
@@ -290,13 +309,14 @@ bool vec4_ok(int d, const float* x, int64_t ldx, const float* y, int64_t ldy, in
 
 }  // namespace
 
-extern "C" int gnnrec_spmm_csr_split_f32(const int64_t* row_ptr, const int32_t* col,
-                                         const float* val, int64_t n_rows, const float* x,
-                                         int64_t ldx, float* y, int64_t ldy, int32_t d, int32_t epi,
-                                         const float* self, int64_t ld_self, float* acc,
-                                         int64_t ld_acc, float acc_div, const int64_t* heavy_rows,
-                                         int64_t n_heavy, int64_t heavy_threshold,
-                                         gnnrec_stream_t stream) {
+extern "C" int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col,
+                                          const float* val, int64_t n_rows, const float* x,
+                                          int64_t ldx, const uint8_t* x_nonzero, float* y,
+                                          int64_t ldy, int32_t d, int32_t epi, const float* self,
+                                          int64_t ld_self, float* acc, int64_t ld_acc,
+                                          float acc_div, const int64_t* heavy_rows,
+                                          int64_t n_heavy, int64_t heavy_threshold,
+                                          gnnrec_stream_t stream) {
   GNNREC_REQUIRE(n_rows >= 0 && d >= 1, "spmm: bad sizes n_rows=%lld d=%d", (long long)n_rows, d);
   if (n_rows == 0) return GNNREC_OK;
   GNNREC_REQUIRE(row_ptr && x, "spmm: null row_ptr/x");
@@ -318,14 +338,15 @@ extern "C" int gnnrec_spmm_csr_split_f32(const int64_t* row_ptr, const int32_t* 
   const Csr A{row_ptr, col, val, n_rows};
   hipStream_t s = as_hip(stream);
   const int64_t skip = split ? heavy_threshold : 0;
+  const uint8_t* xm = x_nonzero;
   if (vec4_ok(d, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc)) {
     switch (d) {
-      case 8: launch_spmm_vec4<8>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, s); break;
-      case 16: launch_spmm_vec4<16>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, s); break;
-      case 32: launch_spmm_vec4<32>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, s); break;
-      case 64: launch_spmm_vec4<64>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, s); break;
-      case 128: launch_spmm_vec4<128>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, s); break;
-      default: launch_spmm_vec4<256>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, s); break;
+      case 8: launch_spmm_vec4<8>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, s); break;
+      case 16: launch_spmm_vec4<16>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, s); break;
+      case 32: launch_spmm_vec4<32>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, s); break;
+      case 64: launch_spmm_vec4<64>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, s); break;
+      case 128: launch_spmm_vec4<128>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, s); break;
+      default: launch_spmm_vec4<256>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, s); break;
     }
   } else {
     const int64_t grid = ceil_div(n_rows, kBlock / 64);
@@ -353,6 +374,29 @@ extern "C" int gnnrec_spmm_csr_split_f32(const int64_t* row_ptr, const int32_t* 
     return check_launch("spmm_heavy");
   }
   return GNNREC_OK;
+}
+
+extern "C" int gnnrec_row_nonzero_f32(const float* x, int64_t ldx, int64_t n_rows, int32_t d,
+                                      uint8_t* mask, gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(n_rows >= 0 && d >= 1 && ldx >= d, "row_nonzero: bad sizes");
+  if (n_rows == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(x && mask, "row_nonzero: null pointer");
+  const int64_t g = ceil_div(n_rows, kBlock / 64);
+  hipLaunchKernelGGL(row_nonzero_kernel, dim3((unsigned)(g < 65536 ? g : 65536)), dim3(kBlock), 0,
+                     as_hip(stream), x, ldx, n_rows, (int)d, mask);
+  return check_launch("row_nonzero");
+}
+
+extern "C" int gnnrec_spmm_csr_split_f32(const int64_t* row_ptr, const int32_t* col,
+                                         const float* val, int64_t n_rows, const float* x,
+                                         int64_t ldx, float* y, int64_t ldy, int32_t d, int32_t epi,
+                                         const float* self, int64_t ld_self, float* acc,
+                                         int64_t ld_acc, float acc_div, const int64_t* heavy_rows,
+                                         int64_t n_heavy, int64_t heavy_threshold,
+                                         gnnrec_stream_t stream) {
+  return gnnrec_spmm_csr_masked_f32(row_ptr, col, val, n_rows, x, ldx, nullptr, y, ldy, d, epi,
+                                    self, ld_self, acc, ld_acc, acc_div, heavy_rows, n_heavy,
+                                    heavy_threshold, stream);
 }
 
 extern "C" int gnnrec_spmm_csr_f32(const int64_t* row_ptr, const int32_t* col, const float* val,

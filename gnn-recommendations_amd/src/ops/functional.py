@@ -62,21 +62,63 @@ def _heavy_args(adj: CsrGraph, x: torch.Tensor, heavy_threshold: int):
 # ---- raw launches (no autograd) ---------------------------------------------------------
 def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi: int = 0,
               self_rows: Optional[torch.Tensor] = None, acc: Optional[torch.Tensor] = None,
-              acc_div: float = 1.0, heavy_threshold: Optional[int] = None) -> None:
-    """y = A x with an optional fused layer-mean epilogue (gnnrec_spmm_csr_split_f32: rows
-    longer than `heavy_threshold` run on the workgroup-per-row kernel)."""
+              acc_div: float = 1.0, heavy_threshold: Optional[int] = None,
+              x_mask: Optional[torch.Tensor] = None) -> None:
+    """y = A x with an optional fused layer-mean epilogue (gnnrec_spmm_csr_masked_f32: rows
+    longer than `heavy_threshold` run on the workgroup-per-row kernel; rows of x whose
+    `x_mask` byte is 0 are all-zero and are not gathered — same bits)."""
     _require_device(adj, x, y, self_rows, acc)
+    if x_mask is not None and (x_mask.dtype != torch.uint8 or x_mask.device != x.device
+                               or x_mask.numel() < adj.shape[1]):
+        raise ValueError("x_mask must be a uint8 tensor on x's device with a byte per row")
     d = x.shape[1]
     if x.shape[0] < adj.shape[1]:
         raise ValueError(f"x has {x.shape[0]} rows, operand has {adj.shape[1]} columns")
     L = _lib.lib()
     ht = SPMM_HEAVY_THRESHOLD if heavy_threshold is None else heavy_threshold
-    check(L.gnnrec_spmm_csr_split_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(y),
-                                      y.stride(0) if y is not None else d, d, epi, ptr(self_rows),
-                                      self_rows.stride(0) if self_rows is not None else d,
-                                      ptr(acc), acc.stride(0) if acc is not None else d,
-                                      float(acc_div), *_heavy_args(adj, x, ht),
-                                      _lib.stream_of(adj.device)), "gnnrec_spmm_csr_split_f32")
+    check(L.gnnrec_spmm_csr_masked_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(x_mask),
+                                       ptr(y), y.stride(0) if y is not None else d, d, epi,
+                                       ptr(self_rows),
+                                       self_rows.stride(0) if self_rows is not None else d,
+                                       ptr(acc), acc.stride(0) if acc is not None else d,
+                                       float(acc_div), *_heavy_args(adj, x, ht),
+                                       _lib.stream_of(adj.device)), "gnnrec_spmm_csr_masked_f32")
+
+
+def row_nonzero(x: torch.Tensor) -> torch.Tensor:
+    """uint8 [rows]: 1 where the row of x holds any non-zero (NaN included)."""
+    x = _rowmajor(x)
+    m = torch.empty(x.shape[0], dtype=torch.uint8, device=x.device)
+    check(_lib.lib().gnnrec_row_nonzero_f32(ptr(x), x.stride(0), x.shape[0], x.shape[1], ptr(m),
+                                            _lib.stream_of(x.device)), "gnnrec_row_nonzero_f32")
+    return m
+
+
+def lightgcn_backward(adj: CsrGraph, g: torch.Tensor, n_layers: int,
+                      masked_hops: Optional[int] = None) -> torch.Tensor:
+    """d/dx0 of mean_k A^k x0 applied to g: mean_k (A^T)^k g — the same launches and epilogue
+    order as lightgcn_forward over A^T (so the same bits), with the first `masked_hops` hops
+    (default K-1) skipping the all-zero rows of their input: the BPR gradient touches a few
+    thousand rows, so the first hops gather almost nothing."""
+    at = adj.t()
+    g = g.contiguous()
+    _require_device(at, g)
+    K = int(n_layers)
+    masked_hops = K - 1 if masked_hops is None else masked_hops
+    out = torch.empty_like(g)
+    if K == 0:
+        out.copy_(g)
+        return out
+    bufs = [torch.empty_like(g), torch.empty_like(g)] if K > 1 else [None]
+    x_in = g
+    for k in range(1, K + 1):
+        last = k == K
+        epi = (EPI_ACC_INIT if k == 1 else EPI_ACC_ADD) | ((EPI_ACC_DIV | EPI_NO_Y) if last else 0)
+        y = None if last else bufs[k & 1]
+        spmm_into(at, x_in, y, epi=epi, self_rows=g, acc=out, acc_div=float(K + 1),
+                  x_mask=row_nonzero(x_in) if k <= masked_hops else None)
+        x_in = y
+    return out
 
 
 def spmm_forward(adj: CsrGraph, x: torch.Tensor) -> torch.Tensor:
@@ -142,9 +184,9 @@ class _LightGCN(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        # d/dx0 of mean_k A^k x0 is mean_k (A^T)^k g: the same propagation over A^T.
-        gx, _ = lightgcn_forward(ctx.adj.t(), g.contiguous(), ctx.n_layers)
-        return None, gx, None
+        # d/dx0 of mean_k A^k x0 is mean_k (A^T)^k g: the same propagation over A^T, its
+        # first hops skipping the all-zero rows of the (sparse) incoming gradient.
+        return None, lightgcn_backward(ctx.adj, g, ctx.n_layers), None
 
 
 def lightgcn_propagate(adj: CsrGraph, x0: torch.Tensor, n_layers: int) -> torch.Tensor:

@@ -316,3 +316,24 @@ def test_ngcf_and_dense_split_forms_on_powerlaw_equal_fused(cuda):
     y2 = F.dense_layer(g, x, M, 0.9, x, 0.1, acc=acc2, acc_mode=1, w_out=0.3, w_res=0.2, fused=True)
     np.testing.assert_array_equal(bits(y1.cpu().numpy()), bits(y2.cpu().numpy()))
     np.testing.assert_array_equal(bits(acc1.cpu().numpy()), bits(acc2.cpu().numpy()))
+
+
+@pytest.mark.parametrize("K", [1, 2, 3])
+def test_masked_backward_equals_dense(cuda, K):
+    """lightgcn_backward (first hops skip the all-zero rows of a sparse gradient) == the dense
+    propagation over A^T, bit for bit; and a masked hop == an unmasked one."""
+    g, (rp, col, val) = powerlaw_graph(31 + K, cuda)
+    n = g.shape[0]
+    grad = torch.zeros(n, 64, device=cuda)
+    rows = torch.randperm(n, device=cuda)[:50]
+    grad[rows] = torch.randn(50, 64, device=cuda)
+    grad[rows[0], 3] = -0.0                       # signed zeros inside a non-zero row
+    sparse_out = F.lightgcn_backward(g, grad, K)
+    dense_out, _ = F.lightgcn_forward(g.t(), grad, K)
+    np.testing.assert_array_equal(bits(sparse_out.cpu().numpy()), bits(dense_out.cpu().numpy()))
+    m = F.row_nonzero(grad)
+    assert int(m.sum()) == 50
+    y1, y2 = torch.empty_like(grad), torch.empty_like(grad)
+    F.spmm_into(g, grad, y1, x_mask=m)
+    F.spmm_into(g, grad, y2)
+    np.testing.assert_array_equal(bits(y1.cpu().numpy()), bits(y2.cpu().numpy()))
