@@ -142,15 +142,26 @@ __device__ __forceinline__ void gather_step_v(const int32_t* __restrict__ col,
     }
   }
   VecF<VEC> xv[CH];
+  int cc[CH];
 #pragma unroll
-  for (int t = 0; t < CH; ++t) {
-    const int c = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
-    if (MASKED && xmask[c] == 0) {
+  for (int t = 0; t < CH; ++t) cc[t] = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
+  if constexpr (MASKED) {
+    // all CH mask bytes in flight together, then only the non-zero rows are gathered
+    uint8_t mk[CH];
 #pragma unroll
-      for (int q = 0; q < VEC; ++q) xv[t].v[q] = 0.f;
-    } else {
-      xv[t] = ldv<VEC>(x + (int64_t)c * ldx + VEC * gl);
+    for (int t = 0; t < CH; ++t) mk[t] = xmask[cc[t]];
+#pragma unroll
+    for (int t = 0; t < CH; ++t) {
+      if (mk[t]) {
+        xv[t] = ldv<VEC>(x + (int64_t)cc[t] * ldx + VEC * gl);
+      } else {
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) xv[t].v[q] = 0.f;
+      }
     }
+  } else {
+#pragma unroll
+    for (int t = 0; t < CH; ++t) xv[t] = ldv<VEC>(x + (int64_t)cc[t] * ldx + VEC * gl);
   }
 #pragma unroll
   for (int t = 0; t < CH; ++t) {
