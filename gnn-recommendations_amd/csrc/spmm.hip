@@ -15,7 +15,8 @@ template <int D, bool MASKED = false>
 __global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
     Csr A, const float* __restrict__ x, int64_t ldx, float* __restrict__ y, int64_t ldy,
     int epi, const float* __restrict__ self, int64_t ld_self, float* __restrict__ acc,
-    int64_t ld_acc, float acc_div, int64_t skip_len, const uint8_t* __restrict__ xmask) {
+    int64_t ld_acc, float acc_div, int64_t skip_len, const uint8_t* __restrict__ xmask,
+    const uint8_t* __restrict__ y_active) {
   constexpr int VEC = SpmmCfg<D>::VEC, CH = SpmmCfg<D>::CH;
   constexpr int GROUP = D / VEC;
   constexpr int RPW = 64 / GROUP;
@@ -26,8 +27,14 @@ __global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
   if (r >= A.n_rows) return;  // the whole group leaves together
   const int64_t beg = A.row_ptr[r], end = A.row_ptr[r + 1];
   if (skip_len > 0 && end - beg > skip_len) return;  // a heavy row: spmm_heavy_kernel's
-  const VecF<VEC> a = gather_row_v<VEC, GROUP, CH, false, MASKED>(A.col, A.val, beg, end, x, ldx,
-                                                                   gl, xmask);
+  VecF<VEC> a;
+  if (MASKED && y_active != nullptr && y_active[r] == 0) {
+    // no neighbour of this row is non-zero: the chain would add only +-0 terms to +0
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) a.v[q] = 0.f;
+  } else {
+    a = gather_row_v<VEC, GROUP, CH, false, MASKED>(A.col, A.val, beg, end, x, ldx, gl, xmask);
+  }
   if (!(epi & GNNREC_EPI_NO_Y)) stv<VEC>(y + r * ldy + VEC * gl, a);
   acc_epilogue_v<VEC>(epi, a, self + r * ld_self + VEC * gl, acc + r * ld_acc + VEC * gl, acc_div);
 }
@@ -242,6 +249,22 @@ __global__ __launch_bounds__(kBlock) void row_nonzero_kernel(const float* __rest
   }
 }
 
+// y_active[r] = 1 for every destination row r with a neighbour c whose x row is non-zero,
+// scattered from the non-zero sources through the TRANSPOSE's rows (row c lists every r with
+// A[r, c] != 0); y_active must be zeroed first. Benign races: every writer stores 1.
+__global__ __launch_bounds__(kBlock) void mark_active_kernel(const int64_t* __restrict__ rp_t,
+                                                             const int32_t* __restrict__ col_t,
+                                                             int64_t n_src,
+                                                             const uint8_t* __restrict__ x_nonzero,
+                                                             uint8_t* __restrict__ y_active) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t c = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6; c < n_src;
+       c += ((int64_t)gridDim.x * kBlock) >> 6) {
+    if (!x_nonzero[c]) continue;
+    for (int64_t k = rp_t[c] + lane; k < rp_t[c + 1]; k += 64) y_active[col_t[k]] = 1;
+  }
+}
+
 // MODE 0: standalone GAS of x rows. MODE 1: GAS(A x) (fused hop epilogue).
 template <int D, int MODE>
 __global__ __launch_bounds__(kBlock) void gas_kernel(Csr A, const float* __restrict__ x,
@@ -285,15 +308,16 @@ namespace {
 template <int D>
 void launch_spmm_vec4(const Csr& A, const float* x, int64_t ldx, float* y, int64_t ldy, int epi,
                       const float* self, int64_t ld_self, float* acc, int64_t ld_acc,
-                      float acc_div, int64_t skip, const uint8_t* xmask, hipStream_t s) {
+                      float acc_div, int64_t skip, const uint8_t* xmask, const uint8_t* y_active,
+                      hipStream_t s) {
   constexpr int RPB = (64 / (D / SpmmCfg<D>::VEC)) * (kBlock / 64);
   const int64_t grid = ceil_div(A.n_rows, RPB);
   if (xmask)
     hipLaunchKernelGGL((spmm_vec_kernel<D, true>), dim3((unsigned)grid), dim3(kBlock), 0, s, A, x,
-                       ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xmask);
+                       ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xmask, y_active);
   else
     hipLaunchKernelGGL((spmm_vec_kernel<D, false>), dim3((unsigned)grid), dim3(kBlock), 0, s, A, x,
-                       ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xmask);
+                       ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xmask, y_active);
 }
 
 bool vec4_ok(int d, const float* x, int64_t ldx, const float* y, int64_t ldy, int epi,
@@ -311,7 +335,8 @@ bool vec4_ok(int d, const float* x, int64_t ldx, const float* y, int64_t ldy, in
 
 extern "C" int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col,
                                           const float* val, int64_t n_rows, const float* x,
-                                          int64_t ldx, const uint8_t* x_nonzero, float* y,
+                                          int64_t ldx, const uint8_t* x_nonzero,
+                                          const uint8_t* y_active, float* y,
                                           int64_t ldy, int32_t d, int32_t epi, const float* self,
                                           int64_t ld_self, float* acc, int64_t ld_acc,
                                           float acc_div, const int64_t* heavy_rows,
@@ -341,12 +366,12 @@ extern "C" int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t*
   const uint8_t* xm = x_nonzero;
   if (vec4_ok(d, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc)) {
     switch (d) {
-      case 8: launch_spmm_vec4<8>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, s); break;
-      case 16: launch_spmm_vec4<16>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, s); break;
-      case 32: launch_spmm_vec4<32>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, s); break;
-      case 64: launch_spmm_vec4<64>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, s); break;
-      case 128: launch_spmm_vec4<128>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, s); break;
-      default: launch_spmm_vec4<256>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, s); break;
+      case 8: launch_spmm_vec4<8>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, s); break;
+      case 16: launch_spmm_vec4<16>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, s); break;
+      case 32: launch_spmm_vec4<32>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, s); break;
+      case 64: launch_spmm_vec4<64>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, s); break;
+      case 128: launch_spmm_vec4<128>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, s); break;
+      default: launch_spmm_vec4<256>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, s); break;
     }
   } else {
     const int64_t grid = ceil_div(n_rows, kBlock / 64);
@@ -387,6 +412,22 @@ extern "C" int gnnrec_row_nonzero_f32(const float* x, int64_t ldx, int64_t n_row
   return check_launch("row_nonzero");
 }
 
+extern "C" int gnnrec_mark_active_rows(const int64_t* row_ptr_t, const int32_t* col_t,
+                                       int64_t n_src, const uint8_t* x_nonzero, int64_t n_dst,
+                                       uint8_t* y_active, gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(n_src >= 0 && n_dst >= 0, "mark_active_rows: bad sizes");
+  GNNREC_REQUIRE(y_active && (n_src == 0 || (row_ptr_t && col_t && x_nonzero)),
+                 "mark_active_rows: null pointer");
+  hipStream_t s = as_hip(stream);
+  if (n_dst > 0 && hipMemsetAsync(y_active, 0, (size_t)n_dst, s) != hipSuccess)
+    return check_launch("mark_active_rows: memset");
+  if (n_src == 0) return GNNREC_OK;
+  const int64_t g = ceil_div(n_src, kBlock / 64);
+  hipLaunchKernelGGL(mark_active_kernel, dim3((unsigned)(g < 65536 ? g : 65536)), dim3(kBlock), 0,
+                     s, row_ptr_t, col_t, n_src, x_nonzero, y_active);
+  return check_launch("mark_active_rows");
+}
+
 extern "C" int gnnrec_spmm_csr_split_f32(const int64_t* row_ptr, const int32_t* col,
                                          const float* val, int64_t n_rows, const float* x,
                                          int64_t ldx, float* y, int64_t ldy, int32_t d, int32_t epi,
@@ -394,7 +435,7 @@ extern "C" int gnnrec_spmm_csr_split_f32(const int64_t* row_ptr, const int32_t* 
                                          int64_t ld_acc, float acc_div, const int64_t* heavy_rows,
                                          int64_t n_heavy, int64_t heavy_threshold,
                                          gnnrec_stream_t stream) {
-  return gnnrec_spmm_csr_masked_f32(row_ptr, col, val, n_rows, x, ldx, nullptr, y, ldy, d, epi,
+  return gnnrec_spmm_csr_masked_f32(row_ptr, col, val, n_rows, x, ldx, nullptr, nullptr, y, ldy, d, epi,
                                     self, ld_self, acc, ld_acc, acc_div, heavy_rows, n_heavy,
                                     heavy_threshold, stream);
 }

@@ -63,7 +63,8 @@ def _heavy_args(adj: CsrGraph, x: torch.Tensor, heavy_threshold: int):
 def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi: int = 0,
               self_rows: Optional[torch.Tensor] = None, acc: Optional[torch.Tensor] = None,
               acc_div: float = 1.0, heavy_threshold: Optional[int] = None,
-              x_mask: Optional[torch.Tensor] = None) -> None:
+              x_mask: Optional[torch.Tensor] = None,
+              y_active: Optional[torch.Tensor] = None) -> None:
     """y = A x with an optional fused layer-mean epilogue (gnnrec_spmm_csr_masked_f32: rows
     longer than `heavy_threshold` run on the workgroup-per-row kernel; rows of x whose
     `x_mask` byte is 0 are all-zero and are not gathered — same bits)."""
@@ -76,8 +77,11 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
         raise ValueError(f"x has {x.shape[0]} rows, operand has {adj.shape[1]} columns")
     L = _lib.lib()
     ht = SPMM_HEAVY_THRESHOLD if heavy_threshold is None else heavy_threshold
+    if y_active is not None and (x_mask is None or y_active.dtype != torch.uint8
+                                 or y_active.numel() < adj.n_rows):
+        raise ValueError("y_active needs x_mask and a uint8 byte per destination row")
     check(L.gnnrec_spmm_csr_masked_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(x_mask),
-                                       ptr(y), y.stride(0) if y is not None else d, d, epi,
+                                       ptr(y_active), ptr(y), y.stride(0) if y is not None else d, d, epi,
                                        ptr(self_rows),
                                        self_rows.stride(0) if self_rows is not None else d,
                                        ptr(acc), acc.stride(0) if acc is not None else d,
@@ -115,8 +119,17 @@ def lightgcn_backward(adj: CsrGraph, g: torch.Tensor, n_layers: int,
         last = k == K
         epi = (EPI_ACC_INIT if k == 1 else EPI_ACC_ADD) | ((EPI_ACC_DIV | EPI_NO_Y) if last else 0)
         y = None if last else bufs[k & 1]
+        xm = ya = None
+        if k <= masked_hops:
+            xm = row_nonzero(x_in)
+            ya = torch.empty(at.n_rows, dtype=torch.uint8, device=g.device)
+            # rows of A^T that reach a non-zero row: scattered through (A^T)^T = A
+            check(_lib.lib().gnnrec_mark_active_rows(ptr(adj.row_ptr), ptr(adj.col), adj.n_rows,
+                                                     ptr(xm), at.n_rows, ptr(ya),
+                                                     _lib.stream_of(g.device)),
+                  "gnnrec_mark_active_rows")
         spmm_into(at, x_in, y, epi=epi, self_rows=g, acc=out, acc_div=float(K + 1),
-                  x_mask=row_nonzero(x_in) if k <= masked_hops else None)
+                  x_mask=xm, y_active=ya)
         x_in = y
     return out
 

@@ -104,19 +104,28 @@ int gnnrec_lightgcn_split_f32(const int64_t* row_ptr, const int32_t* col, const 
                               int64_t heavy_threshold, gnnrec_stream_t stream);
 
 /* Sparse-input hop: gnnrec_spmm_csr_split_f32 where x_nonzero (device uint8 [rows of x],
- * may be NULL) marks the rows of x that hold any non-zero; the row-parallel kernel does not
- * gather unmarked rows (they contribute fmaf(v, +-0, acc) == acc: same bits). The BPR
- * gradient entering the backward propagation touches a few thousand of 2M rows, so its first
- * hops skip almost every gather. gnnrec_row_nonzero_f32 builds the mask. */
+ * may be NULL) marks the rows of x that hold any non-zero, and y_active (uint8 [n_rows], may
+ * be NULL; used only with x_nonzero) the destination rows with at least one such neighbour.
+ * The row-parallel kernel does not gather unmarked x rows and does not walk inactive rows
+ * at all (their terms are fmaf(v, +-0, acc) == acc from +0: same bits). The BPR gradient
+ * entering the backward propagation touches a few thousand of 2M rows, so its first hops
+ * skip almost everything. gnnrec_row_nonzero_f32 builds x_nonzero and
+ * gnnrec_mark_active_rows builds y_active from the operand's transpose (row_ptr_t/col_t:
+ * row c lists the r with A[r, c] != 0 — the operand itself when it is symmetric). */
 int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
                                int64_t n_rows, const float* x, int64_t ldx,
-                               const uint8_t* x_nonzero, float* y, int64_t ldy, int32_t d,
+                               const uint8_t* x_nonzero, const uint8_t* y_active, float* y,
+                               int64_t ldy, int32_t d,
                                int32_t epi, const float* self, int64_t ld_self, float* acc,
                                int64_t ld_acc, float acc_div, const int64_t* heavy_rows,
                                int64_t n_heavy, int64_t heavy_threshold, gnnrec_stream_t stream);
 
 int gnnrec_row_nonzero_f32(const float* x, int64_t ldx, int64_t n_rows, int32_t d,
                            uint8_t* mask, gnnrec_stream_t stream);
+
+int gnnrec_mark_active_rows(const int64_t* row_ptr_t, const int32_t* col_t, int64_t n_src,
+                            const uint8_t* x_nonzero, int64_t n_dst, uint8_t* y_active,
+                            gnnrec_stream_t stream);
 
 /* ---- a7: Group-and-Shuffle transform -----------------------------------------------
  * Replaces GroupShuffleLayer.forward (orthogonal_bundle/group_shuffle_layer.py:88-94):
