@@ -17,7 +17,10 @@ __global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
     int epi, const float* __restrict__ self, int64_t ld_self, float* __restrict__ acc,
     int64_t ld_acc, float acc_div, int64_t skip_len, const uint8_t* __restrict__ xmask,
     const uint8_t* __restrict__ y_active) {
-  constexpr int VEC = SpmmCfg<D>::VEC, CH = SpmmCfg<D>::CH;
+  constexpr int VEC = SpmmCfg<D>::VEC;
+  // a sparse input gathers few rows per step, so the walk over (col, val, mask) is
+  // latency-bound: take 4x the neighbours per dependent step
+  constexpr int CH = MASKED ? 4 * SpmmCfg<D>::CH : SpmmCfg<D>::CH;
   constexpr int GROUP = D / VEC;
   constexpr int RPW = 64 / GROUP;
   const int lane = threadIdx.x & 63;
