@@ -11,16 +11,17 @@
 
 namespace gnnrec {
 
-template <int D, bool MASKED = false>
+// MASKED: skip the neighbours whose input row is all-zero (xmask). ACTIVE: rows with
+// y_active[r] == 0 are not computed (written as +0 with the epilogue applied) — for rows
+// whose value nobody reads, or that no non-zero input row reaches.
+template <int D, bool MASKED = false, bool ACTIVE = false>
 __global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
     Csr A, const float* __restrict__ x, int64_t ldx, float* __restrict__ y, int64_t ldy,
     int epi, const float* __restrict__ self, int64_t ld_self, float* __restrict__ acc,
     int64_t ld_acc, float acc_div, int64_t skip_len, const uint8_t* __restrict__ xmask,
     const uint8_t* __restrict__ y_active) {
   constexpr int VEC = SpmmCfg<D>::VEC;
-  // a sparse input gathers few rows per step, so the walk over (col, val, mask) is
-  // latency-bound: take 4x the neighbours per dependent step
-  constexpr int CH = MASKED ? 4 * SpmmCfg<D>::CH : SpmmCfg<D>::CH;
+  constexpr int CH = SpmmCfg<D>::CH;
   constexpr int GROUP = D / VEC;
   constexpr int RPW = 64 / GROUP;
   const int lane = threadIdx.x & 63;
@@ -31,8 +32,9 @@ __global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
   const int64_t beg = A.row_ptr[r], end = A.row_ptr[r + 1];
   if (skip_len > 0 && end - beg > skip_len) return;  // a heavy row: spmm_heavy_kernel's
   VecF<VEC> a;
-  if (MASKED && y_active != nullptr && y_active[r] == 0) {
-    // no neighbour of this row is non-zero: the chain would add only +-0 terms to +0
+  if (ACTIVE && y_active[r] == 0) {
+    // no neighbour of this row is non-zero (or the row is not needed): the chain would add
+    // only +-0 terms to +0
 #pragma unroll
     for (int q = 0; q < VEC; ++q) a.v[q] = 0.f;
   } else {
@@ -315,12 +317,14 @@ void launch_spmm_vec4(const Csr& A, const float* x, int64_t ldx, float* y, int64
                       hipStream_t s) {
   constexpr int RPB = (64 / (D / SpmmCfg<D>::VEC)) * (kBlock / 64);
   const int64_t grid = ceil_div(A.n_rows, RPB);
-  if (xmask)
-    hipLaunchKernelGGL((spmm_vec_kernel<D, true>), dim3((unsigned)grid), dim3(kBlock), 0, s, A, x,
-                       ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xmask, y_active);
-  else
-    hipLaunchKernelGGL((spmm_vec_kernel<D, false>), dim3((unsigned)grid), dim3(kBlock), 0, s, A, x,
-                       ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xmask, y_active);
+#define GNNREC_VEC(M, AC)                                                                          \
+  hipLaunchKernelGGL((spmm_vec_kernel<D, M, AC>), dim3((unsigned)grid), dim3(kBlock), 0, s, A, x, \
+                     ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xmask, y_active)
+  if (xmask && y_active) GNNREC_VEC(true, true);
+  else if (xmask) GNNREC_VEC(true, false);
+  else if (y_active) GNNREC_VEC(false, true);
+  else GNNREC_VEC(false, false);
+#undef GNNREC_VEC
 }
 
 bool vec4_ok(int d, const float* x, int64_t ldx, const float* y, int64_t ldy, int epi,

@@ -48,6 +48,18 @@ class LightGCN(BaseRecommender):
         user_emb, item_emb = torch.split(out, [self.n_users, self.n_items], dim=0)
         return user_emb, item_emb
 
+    def forward_rows(self, adj_matrix, need: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """forward() where only the output rows marked in `need` (uint8 [n_users + n_items])
+        are defined — what a training batch reads (ops.lightgcn_forward_rows: the last hops
+        compute only those rows and their neighbourhoods; same bits at the marked rows). On
+        a CPU operand it is forward()."""
+        a = ops.as_operand(adj_matrix)
+        if not isinstance(a, CsrGraph):
+            return self.forward(adj_matrix)
+        out = ops.lightgcn_propagate(a, self._initial_table(), self.n_layers, need=need)
+        user_emb, item_emb = torch.split(out, [self.n_users, self.n_items], dim=0)
+        return user_emb, item_emb
+
     def predict(self, users: torch.Tensor, items: torch.Tensor,
                 adj_matrix: Optional[torch.Tensor] = None) -> torch.Tensor:
         if adj_matrix is None:

@@ -67,7 +67,8 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
               y_active: Optional[torch.Tensor] = None) -> None:
     """y = A x with an optional fused layer-mean epilogue (gnnrec_spmm_csr_masked_f32: rows
     longer than `heavy_threshold` run on the workgroup-per-row kernel; rows of x whose
-    `x_mask` byte is 0 are all-zero and are not gathered — same bits)."""
+    `x_mask` byte is 0 are all-zero and are not gathered — same bits; destination rows whose
+    `y_active` byte is 0 are not computed — y is +0 there, or the true value)."""
     _require_device(adj, x, y, self_rows, acc)
     if x_mask is not None and (x_mask.dtype != torch.uint8 or x_mask.device != x.device
                                or x_mask.numel() < adj.shape[1]):
@@ -77,9 +78,10 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
         raise ValueError(f"x has {x.shape[0]} rows, operand has {adj.shape[1]} columns")
     L = _lib.lib()
     ht = SPMM_HEAVY_THRESHOLD if heavy_threshold is None else heavy_threshold
-    if y_active is not None and (x_mask is None or y_active.dtype != torch.uint8
+    if y_active is not None and (y_active.dtype != torch.uint8 or y_active.device != x.device
                                  or y_active.numel() < adj.n_rows):
-        raise ValueError("y_active needs x_mask and a uint8 byte per destination row")
+        raise ValueError("y_active must be a uint8 tensor on x's device with a byte per "
+                         "destination row")
     check(L.gnnrec_spmm_csr_masked_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(x_mask),
                                        ptr(y_active), ptr(y), y.stride(0) if y is not None else d, d, epi,
                                        ptr(self_rows),
@@ -98,40 +100,83 @@ def row_nonzero(x: torch.Tensor) -> torch.Tensor:
     return m
 
 
+def mark_rows(row_ptr: torch.Tensor, col: torch.Tensor, marked: torch.Tensor,
+              n_out: int) -> torch.Tensor:
+    """uint8 [n_out]: 1 at every column listed in a marked row of (row_ptr, col)
+    (gnnrec_mark_active_rows)."""
+    m = torch.empty(n_out, dtype=torch.uint8, device=marked.device)
+    check(_lib.lib().gnnrec_mark_active_rows(ptr(row_ptr), ptr(col), row_ptr.numel() - 1,
+                                             ptr(marked), n_out, ptr(m),
+                                             _lib.stream_of(marked.device)),
+          "gnnrec_mark_active_rows")
+    return m
+
+
+def _lightgcn_hops(op: CsrGraph, x0: torch.Tensor, K: int, masks) -> torch.Tensor:
+    """mean(x0, op x0, ..., op^K x0) as K spmm_into launches with the layer mean in their
+    epilogues — the launch and rounding order of gnnrec_lightgcn_split_f32. `masks(k, x_in)`
+    gives hop k's (x_mask, y_active), either None."""
+    out = torch.empty_like(x0)
+    if K == 0:
+        out.copy_(x0)
+        return out
+    bufs = [torch.empty_like(x0), torch.empty_like(x0)] if K > 1 else [None]
+    x_in = x0
+    for k in range(1, K + 1):
+        last = k == K
+        epi = (EPI_ACC_INIT if k == 1 else EPI_ACC_ADD) | ((EPI_ACC_DIV | EPI_NO_Y) if last else 0)
+        y = None if last else bufs[k & 1]
+        xm, ya = masks(k, x_in)
+        spmm_into(op, x_in, y, epi=epi, self_rows=x0, acc=out, acc_div=float(K + 1),
+                  x_mask=xm, y_active=ya)
+        x_in = y
+    return out
+
+
 def lightgcn_backward(adj: CsrGraph, g: torch.Tensor, n_layers: int,
-                      masked_hops: Optional[int] = None) -> torch.Tensor:
+                      masked_hops: Optional[int] = None, active_hops: int = 1) -> torch.Tensor:
     """d/dx0 of mean_k A^k x0 applied to g: mean_k (A^T)^k g — the same launches and epilogue
-    order as lightgcn_forward over A^T (so the same bits), with the first `masked_hops` hops
-    (default K-1) skipping the all-zero rows of their input: the BPR gradient touches a few
-    thousand rows, so the first hops gather almost nothing."""
+    order as lightgcn_forward over A^T (so the same bits). The BPR gradient touches a few
+    thousand rows, so the first `masked_hops` hops (default K-1) skip the all-zero rows of
+    their input, and the first `active_hops` also skip the output rows no non-zero row reaches.
+    G100M, batch 2048 (tools/exp_masked.py): hop 1 1.9 ms masked+active vs 7.0 dense; hop 2
+    (a quarter of the rows live) 5.9 ms masked, 6.0 + 0.4 (marking) masked+active."""
     at = adj.t()
     g = g.contiguous()
     _require_device(at, g)
     K = int(n_layers)
     masked_hops = K - 1 if masked_hops is None else masked_hops
-    out = torch.empty_like(g)
-    if K == 0:
-        out.copy_(g)
-        return out
-    bufs = [torch.empty_like(g), torch.empty_like(g)] if K > 1 else [None]
-    x_in = g
-    for k in range(1, K + 1):
-        last = k == K
-        epi = (EPI_ACC_INIT if k == 1 else EPI_ACC_ADD) | ((EPI_ACC_DIV | EPI_NO_Y) if last else 0)
-        y = None if last else bufs[k & 1]
-        xm = ya = None
-        if k <= masked_hops:
-            xm = row_nonzero(x_in)
-            ya = torch.empty(at.n_rows, dtype=torch.uint8, device=g.device)
-            # rows of A^T that reach a non-zero row: scattered through (A^T)^T = A
-            check(_lib.lib().gnnrec_mark_active_rows(ptr(adj.row_ptr), ptr(adj.col), adj.n_rows,
-                                                     ptr(xm), at.n_rows, ptr(ya),
-                                                     _lib.stream_of(g.device)),
-                  "gnnrec_mark_active_rows")
-        spmm_into(at, x_in, y, epi=epi, self_rows=g, acc=out, acc_div=float(K + 1),
-                  x_mask=xm, y_active=ya)
-        x_in = y
-    return out
+
+    def masks(k, x_in):
+        if k > masked_hops:
+            return None, None
+        xm = row_nonzero(x_in)
+        # rows of A^T that reach a non-zero row: listed by (A^T)^T = A's rows
+        ya = mark_rows(adj.row_ptr, adj.col, xm, at.n_rows) if k <= active_hops else None
+        return xm, ya
+
+    return _lightgcn_hops(at, g, K, masks)
+
+
+def lightgcn_forward_rows(adj: CsrGraph, x0: torch.Tensor, n_layers: int, need: torch.Tensor,
+                          restricted_hops: int = 2) -> torch.Tensor:
+    """lightgcn_forward's output at the rows where `need` (uint8 [N]) is 1, with the same
+    bits; the other rows are NOT defined. For a training batch: the BPR loss reads ~6K of 2M
+    output rows, so hop K computes only those (R_K = need) and hop k < K only what hop k+1
+    reads plus the needed rows (R_k = need | columns of R_{k+1}) — for the last
+    `restricted_hops` hops; earlier hops reach nearly every row and run dense."""
+    x0 = x0.contiguous()
+    _require_device(adj, x0)
+    n = x0.shape[0]
+    if adj.n_rows != n or adj.shape[1] != n:
+        raise ValueError("LightGCN propagation needs a square operand matching x0")
+    if need.dtype != torch.uint8 or need.numel() != n or need.device != x0.device:
+        raise ValueError("need must be a uint8 tensor with a byte per row on x0's device")
+    K = int(n_layers)
+    rows = {K: need}
+    for k in range(K - 1, max(K - restricted_hops, 0), -1):
+        rows[k] = mark_rows(adj.row_ptr, adj.col, rows[k + 1], n).bitwise_or_(need)
+    return _lightgcn_hops(adj, x0, K, lambda k, _x: (None, rows.get(k)))
 
 
 def spmm_forward(adj: CsrGraph, x: torch.Tensor) -> torch.Tensor:
@@ -190,8 +235,10 @@ def spmm(adj: CsrGraph, x: torch.Tensor) -> torch.Tensor:
 
 class _LightGCN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, adj: CsrGraph, x0: torch.Tensor, n_layers: int):
+    def forward(ctx, adj: CsrGraph, x0: torch.Tensor, n_layers: int, need=None):
         ctx.adj, ctx.n_layers = adj, n_layers
+        if need is not None:
+            return lightgcn_forward_rows(adj, x0, n_layers, need)
         out, _ = lightgcn_forward(adj, x0, n_layers)
         return out
 
@@ -199,12 +246,15 @@ class _LightGCN(torch.autograd.Function):
     def backward(ctx, g):
         # d/dx0 of mean_k A^k x0 is mean_k (A^T)^k g: the same propagation over A^T, its
         # first hops skipping the all-zero rows of the (sparse) incoming gradient.
-        return None, lightgcn_backward(ctx.adj, g, ctx.n_layers), None
+        return None, lightgcn_backward(ctx.adj, g, ctx.n_layers), None, None
 
 
-def lightgcn_propagate(adj: CsrGraph, x0: torch.Tensor, n_layers: int) -> torch.Tensor:
-    """Fused K-hop LightGCN propagation + layer mean (lightgcn.py:76-95), differentiable."""
-    return _LightGCN.apply(adj, x0, int(n_layers))
+def lightgcn_propagate(adj: CsrGraph, x0: torch.Tensor, n_layers: int,
+                       need: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Fused K-hop LightGCN propagation + layer mean (lightgcn.py:76-95), differentiable.
+    With `need` (uint8 [N]) only those output rows are defined (lightgcn_forward_rows); the
+    gradient must then be zero elsewhere, as it is when only those rows are read."""
+    return _LightGCN.apply(adj, x0, int(n_layers), need)
 
 
 # ---- fused inference kernels ----------------------------------------------------------

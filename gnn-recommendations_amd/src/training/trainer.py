@@ -43,12 +43,28 @@ def bpr_scores(user_emb: torch.Tensor, item_emb: torch.Tensor, users: torch.Tens
     return pos, neg
 
 
+def batch_rows(n_users: int, n_items: int, users, pos_items, neg_items) -> torch.Tensor:
+    """uint8 [n_users + n_items]: 1 at the propagated-table rows a BPR batch reads."""
+    need = torch.zeros(n_users + n_items, dtype=torch.uint8, device=users.device)
+    need[users] = 1
+    need[n_users + pos_items] = 1
+    need[n_users + neg_items.reshape(-1)] = 1
+    return need
+
+
 def train_step(model: nn.Module, adj, users, pos_items, neg_items, optimizer,
-               loss_fn: Optional[nn.Module] = None, max_grad_norm: float = 1.0) -> torch.Tensor:
-    """One batch of trainer.py:248-279: full propagation, BPR loss, backward, clip, Adam.
-    Returns the loss as a 0-d device tensor (no host sync)."""
+               loss_fn: Optional[nn.Module] = None, max_grad_norm: float = 1.0,
+               row_subset: bool = True) -> torch.Tensor:
+    """One batch of trainer.py:248-279: propagation, BPR loss, backward, clip, Adam.
+    Returns the loss as a 0-d device tensor (no host sync). The loss reads only the batch's
+    rows of the propagated table, so with `row_subset` a model with `forward_rows` computes
+    just those (and what they depend on): the same loss and gradient bits as the full
+    propagation the reference runs (trainer.py:251-254)."""
     loss_fn = loss_fn or BPRLoss()
-    if hasattr(model, "get_all_embeddings"):
+    if row_subset and hasattr(model, "forward_rows"):
+        need = batch_rows(model.n_users, model.n_items, users, pos_items, neg_items)
+        user_emb, item_emb = model.forward_rows(adj, need)
+    elif hasattr(model, "get_all_embeddings"):
         user_emb, item_emb = model.get_all_embeddings(adj)
     else:
         user_emb, item_emb = model(adj)

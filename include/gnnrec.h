@@ -103,15 +103,20 @@ int gnnrec_lightgcn_split_f32(const int64_t* row_ptr, const int32_t* col, const 
                               int64_t ld_out, const int64_t* heavy_rows, int64_t n_heavy,
                               int64_t heavy_threshold, gnnrec_stream_t stream);
 
-/* Sparse-input hop: gnnrec_spmm_csr_split_f32 where x_nonzero (device uint8 [rows of x],
- * may be NULL) marks the rows of x that hold any non-zero, and y_active (uint8 [n_rows], may
- * be NULL; used only with x_nonzero) the destination rows with at least one such neighbour.
- * The row-parallel kernel does not gather unmarked x rows and does not walk inactive rows
- * at all (their terms are fmaf(v, +-0, acc) == acc from +0: same bits). The BPR gradient
- * entering the backward propagation touches a few thousand of 2M rows, so its first hops
- * skip almost everything. gnnrec_row_nonzero_f32 builds x_nonzero and
- * gnnrec_mark_active_rows builds y_active from the operand's transpose (row_ptr_t/col_t:
- * row c lists the r with A[r, c] != 0 — the operand itself when it is symmetric). */
+/* Sparse-input / row-subset hop: gnnrec_spmm_csr_split_f32 where x_nonzero (device uint8
+ * [rows of x], may be NULL) marks the rows of x that hold any non-zero, and y_active (uint8
+ * [n_rows], may be NULL) the destination rows to compute. The row-parallel kernel does not
+ * gather unmarked x rows (their terms are fmaf(v, +-0, acc) == acc from +0: same bits) and
+ * does not walk inactive rows: their y is written as +0 (or, for heavy rows and the any-d
+ * path, the true value) and the epilogue applied to it. Two uses:
+ *  - backward: the BPR gradient touches a few thousand of 2M rows, so y_active = rows with a
+ *    non-zero neighbour (gnnrec_mark_active_rows) loses nothing and skips almost everything;
+ *  - training forward: the loss reads a few thousand output rows, so the last hops need only
+ *    those rows and their neighbourhoods (the values of the other rows are then not defined).
+ * gnnrec_row_nonzero_f32 builds x_nonzero; gnnrec_mark_active_rows sets y_active[c] = 1 for
+ * every c listed in a marked row of (row_ptr_t, col_t) and 0 elsewhere — given the operand's
+ * transpose it marks the rows a non-zero input row reaches, given the operand itself the
+ * inputs the marked rows read (the same thing when the operand is symmetric). */
 int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
                                int64_t n_rows, const float* x, int64_t ldx,
                                const uint8_t* x_nonzero, const uint8_t* y_active, float* y,

@@ -328,12 +328,42 @@ def test_masked_backward_equals_dense(cuda, K):
     rows = torch.randperm(n, device=cuda)[:50]
     grad[rows] = torch.randn(50, 64, device=cuda)
     grad[rows[0], 3] = -0.0                       # signed zeros inside a non-zero row
-    sparse_out = F.lightgcn_backward(g, grad, K)
     dense_out, _ = F.lightgcn_forward(g.t(), grad, K)
-    np.testing.assert_array_equal(bits(sparse_out.cpu().numpy()), bits(dense_out.cpu().numpy()))
+    for mh, ah in ((None, 1), (K, K), (1, 0)):     # default, every hop masked+active, one
+        sparse_out = F.lightgcn_backward(g, grad, K, masked_hops=mh, active_hops=ah)
+        np.testing.assert_array_equal(bits(sparse_out.cpu().numpy()),
+                                      bits(dense_out.cpu().numpy()))
     m = F.row_nonzero(grad)
     assert int(m.sum()) == 50
     y1, y2 = torch.empty_like(grad), torch.empty_like(grad)
     F.spmm_into(g, grad, y1, x_mask=m)
     F.spmm_into(g, grad, y2)
     np.testing.assert_array_equal(bits(y1.cpu().numpy()), bits(y2.cpu().numpy()))
+
+
+@pytest.mark.parametrize("K,d", [(1, 64), (2, 64), (3, 64), (3, 32), (3, 128), (4, 16)])
+def test_lightgcn_forward_rows_equal_full(cuda, K, d):
+    """The training forward that computes only the rows a batch reads (and their
+    neighbourhoods) gives the full propagation's bits at those rows, heavy rows included."""
+    g, _ = powerlaw_graph(41 + K, cuda)
+    n = g.shape[0]
+    torch.manual_seed(K)
+    x0 = torch.randn(n, d, device=cuda)
+    full, _ = F.lightgcn_forward(g, x0, K)
+    for n_need in (1, 40, 600):
+        need = torch.zeros(n, dtype=torch.uint8, device=cuda)
+        idx = torch.randperm(n, device=cuda)[:n_need]
+        need[idx] = 1
+        hr = g.heavy_rows(F.SPMM_HEAVY_THRESHOLD)
+        if hr is not None and n_need > 1:
+            need[hr[:2]] = 1
+        out = F.lightgcn_forward_rows(g, x0, K, need)
+        sel = need.bool()
+        np.testing.assert_array_equal(bits(out[sel].cpu().numpy()), bits(full[sel].cpu().numpy()))
+    # a hop restricted by y_active alone: the active rows are exact
+    ya = (torch.rand(n, device=cuda) < 0.3).to(torch.uint8)
+    y1, y2 = torch.empty_like(x0), torch.empty_like(x0)
+    F.spmm_into(g, x0, y1, y_active=ya)
+    F.spmm_into(g, x0, y2)
+    sel = ya.bool()
+    np.testing.assert_array_equal(bits(y1[sel].cpu().numpy()), bits(y2[sel].cpu().numpy()))

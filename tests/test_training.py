@@ -39,7 +39,7 @@ def test_bpr_loss_keeps_the_broadcast():
     assert torch.equal(BPRLoss()(pos, neg), ref)
 
 
-def _run_steps(adj, device):
+def _run_steps(adj, device, row_subset=True):
     f = load_golden("bpr_train_K3_d64")
     _, nu, ni = _golden_graph()
     torch.manual_seed(56)
@@ -50,7 +50,7 @@ def _run_steps(adj, device):
     losses = []
     for b in range(3):
         args = [torch.from_numpy(f[k][b]).to(device) for k in ("users", "pos", "neg")]
-        losses.append(float(train_step(m, adj, *args, opt, BPRLoss(), 1.0)))
+        losses.append(float(train_step(m, adj, *args, opt, BPRLoss(), 1.0, row_subset)))
     return f, m, np.array(losses)
 
 

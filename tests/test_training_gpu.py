@@ -19,6 +19,18 @@ def test_three_adam_steps_native_match_reference(cuda):
     np.testing.assert_allclose(m.item_embedding.weight.detach().cpu().numpy(), f["item_w"], atol=2e-5)
 
 
+def test_row_subset_step_same_bits_as_full_propagation(cuda):
+    """The training forward computes only the batch's rows (and their neighbourhoods): the
+    loss and the updated weights are bit-identical to the full propagation's."""
+    g, _, _ = _golden_graph()
+    gd = g.to(cuda)
+    _, m1, l1 = _run_steps(gd, cuda, row_subset=True)
+    _, m2, l2 = _run_steps(gd, cuda, row_subset=False)
+    np.testing.assert_array_equal(l1, l2)
+    for p1, p2 in zip(m1.parameters(), m2.parameters()):
+        assert torch.equal(p1.detach(), p2.detach())
+
+
 def test_device_sampler_on_gpu(cuda):
     from src.training import DeviceSampler
     rng = np.random.default_rng(1)
