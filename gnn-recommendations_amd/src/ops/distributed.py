@@ -37,9 +37,10 @@ from .graph import CsrGraph
 HopFn = Callable[..., None]
 
 
-def _native_hop(adj, x, y, *, epi, self_rows, acc, acc_div):
+def _native_hop(adj, x, y, *, epi, self_rows, acc, acc_div, x_mask=None, y_active=None):
     from .functional import spmm_into
-    spmm_into(adj, x, y, epi=epi, self_rows=self_rows, acc=acc, acc_div=acc_div)
+    spmm_into(adj, x, y, epi=epi, self_rows=self_rows, acc=acc, acc_div=acc_div,
+              x_mask=x_mask, y_active=y_active)
 
 
 class DistributedGraph:
@@ -186,7 +187,8 @@ class DistributedGraph:
 
 def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers: int, *,
                             gather_output: bool = False, hop_fn: Optional[HopFn] = None,
-                            work: Optional[tuple] = None, overlap_chunks: int = 1) -> torch.Tensor:
+                            work: Optional[tuple] = None, overlap_chunks: int = 1,
+                            masks: Optional[Callable] = None) -> torch.Tensor:
     """LightGCN propagation over a row-sharded operand.
 
     x0_pad: [world*rows_pad, d] padded initial table (identical on every rank).
@@ -196,8 +198,15 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
     overlap_chunks > 1 (point-to-point exchange only): the hop runs in that many row chunks
     and each chunk's transfer is posted as soon as its kernel is queued, so the exchange of
     chunk c overlaps the SpMM of chunk c+1.
+    masks(k, x_in) -> (x_mask [padded rows], y_active [n_local]) or None: the sparse-input /
+    row-subset options of the native hop (spmm_into) for hop k.
     """
     hop = hop_fn or _native_hop
+
+    def mkw(k, x_in):
+        m = masks(k, x_in) if masks is not None else None
+        return {} if m is None else {"x_mask": m[0], "y_active": m[1]}
+
     d = x0_pad.shape[1]
     if work is None:
         work = make_work(dg, d, x0_pad.device)
@@ -216,12 +225,12 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
         if dg.world == 1:  # ping-pong the hop outputs themselves
             y = None if last else (Xa if x_in is not Xa else Xb)
             hop(dg.shard, x_in, None if last else y[:dg.n_local], epi=epi, self_rows=self_rows,
-                acc=acc, acc_div=float(n_layers + 1))
+                acc=acc, acc_div=float(n_layers + 1), **mkw(k, x_in))
             x_in = y
             continue
         if last or not chunked:
             hop(dg.shard, x_in, None if last else Y[:dg.n_local], epi=epi, self_rows=self_rows,
-                acc=acc, acc_div=float(n_layers + 1))
+                acc=acc, acc_div=float(n_layers + 1), **mkw(k, x_in))
             if not last:
                 x_next = Xa if x_in is not Xa else Xb
                 dg.exchange(x_next, Y)
@@ -229,11 +238,15 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
             continue
         x_next = Xa if x_in is not Xa else Xb
         pending = []
+        m = masks(k, x_in) if masks is not None else None
         for c0, c1 in dg.chunk_bounds(overlap_chunks):
             r1 = min(c1, dg.n_local)
             if r1 > c0:
+                kw = {} if m is None else {"x_mask": m[0],
+                                           "y_active": None if m[1] is None else m[1][c0:r1]}
                 hop(dg.shard.row_slice(c0, r1), x_in, Y[c0:r1], epi=epi,
-                    self_rows=self_rows[c0:r1], acc=acc[c0:r1], acc_div=float(n_layers + 1))
+                    self_rows=self_rows[c0:r1], acc=acc[c0:r1], acc_div=float(n_layers + 1),
+                    **kw)
             pending += dg.post_chunk(x_next, Y, c0, c1)
         dg.finish(pending)
         x_in = x_next

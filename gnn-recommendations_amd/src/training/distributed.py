@@ -18,6 +18,12 @@ own parameter shard and its Adam state. One step (the body of trainer.py:248-279
             of those rows).
 
 No all-reduce of the embedding gradient is needed: the table is row-sharded, not replicated.
+
+With the native hops (`hop_fn` None) and `row_subset`, the forward's last two hops compute
+only the rows the batch reads and their neighbourhoods, and the backward's first hops skip
+the all-zero rows of the sparse gradient (as ops.lightgcn_forward_rows / lightgcn_backward
+on one device: the same bits). The row sets are marked on each rank from its own shard's
+rows and OR-ed across ranks (one all_reduce(MAX) of a byte per row per restricted hop).
 """
 from __future__ import annotations
 
@@ -30,16 +36,31 @@ from ..ops.distributed import DistributedGraph, _exchanged, lightgcn_propagate_d
 from .losses import BPRLoss
 
 
-def _all_reduce(t: torch.Tensor, dg: DistributedGraph) -> torch.Tensor:
+def _all_reduce(t: torch.Tensor, dg: DistributedGraph, op=dist.ReduceOp.SUM) -> torch.Tensor:
     if dg.world == 1:
         return t
     if t.is_cuda and dist.get_backend(dg.group) == "gloo":   # 1-GPU test harness
         h = t.cpu()
-        dist.all_reduce(h, group=dg.group)
+        dist.all_reduce(h, op=op, group=dg.group)
         t.copy_(h)
     else:
-        dist.all_reduce(t, group=dg.group)
+        dist.all_reduce(t, op=op, group=dg.group)
     return t
+
+
+def _padded_ids(dg: DistributedGraph, ids: torch.Tensor) -> torch.Tensor:
+    """Global row ids -> positions in the padded layout (on ids' device)."""
+    b = torch.as_tensor(dg.bounds, dtype=torch.int64, device=ids.device)
+    owner = torch.searchsorted(b, ids, right=True) - 1
+    return owner * dg.rows_pad + (ids - b[owner])
+
+
+def _reach(dg: DistributedGraph, local_marked: torch.Tensor) -> torch.Tensor:
+    """Padded uint8 mask of the columns listed by the marked rows of every rank's shard (for
+    a symmetric operand: the rows those rows reach, and the rows they read)."""
+    from ..ops.functional import mark_rows
+    m = mark_rows(dg.shard.row_ptr, dg.shard.col, local_marked, dg.world * dg.rows_pad)
+    return _all_reduce(m, dg, dist.ReduceOp.MAX)
 
 
 def lightgcn_train_step_dist(dg: DistributedGraph, emb_local: torch.nn.Parameter, n_layers: int,
@@ -47,7 +68,8 @@ def lightgcn_train_step_dist(dg: DistributedGraph, emb_local: torch.nn.Parameter
                              neg_items: torch.Tensor, optimizer: torch.optim.Optimizer,
                              loss_fn: Optional[torch.nn.Module] = None,
                              max_grad_norm: float = 1.0,
-                             hop_fn: Optional[Callable] = None) -> torch.Tensor:
+                             hop_fn: Optional[Callable] = None,
+                             row_subset: bool = True) -> torch.Tensor:
     """One BPR step on this rank's shard; returns the (replicated) loss as a 0-d tensor.
     emb_local: this rank's rows [row_begin, row_end) of x0 (a leaf Parameter the optimizer
     owns). users / pos_items / neg_items: the same batch on every rank (global ids; items
@@ -55,13 +77,23 @@ def lightgcn_train_step_dist(dg: DistributedGraph, emb_local: torch.nn.Parameter
     loss_fn = loss_fn or BPRLoss()
     dev = emb_local.device
     b0, b1 = dg.row_begin, dg.row_end
+    K = int(n_layers)
+    native = hop_fn is None and row_subset
     with torch.no_grad():
-        x0_pad = _exchanged(dg, emb_local.detach())
-        out_local = lightgcn_propagate_dist(dg, x0_pad, n_layers, hop_fn=hop_fn)
         B = users.numel()
         neg2 = neg_items.view(B, -1)
         ids = torch.cat([users.view(-1), n_users + pos_items.view(-1),
                          n_users + neg2.reshape(-1)]).to(dev)
+        fwd_masks = None
+        if native:   # R_K = the batch rows, R_k = R_K | rows read by R_{k+1} (last two hops)
+            need = torch.zeros(dg.world * dg.rows_pad, dtype=torch.uint8, device=dev)
+            need[_padded_ids(dg, ids)] = 1
+            R = {K: need}
+            for k in range(K - 1, max(K - 2, 0), -1):
+                R[k] = _reach(dg, dg.local_slice(R[k + 1])).bitwise_or_(need)
+            fwd_masks = lambda k, _x: (None, dg.local_slice(R[k])) if k in R else None  # noqa: E731
+        x0_pad = _exchanged(dg, emb_local.detach())
+        out_local = lightgcn_propagate_dist(dg, x0_pad, K, hop_fn=hop_fn, masks=fwd_masks)
         mine = (ids >= b0) & (ids < b1)
         rows = torch.zeros((ids.numel(), emb_local.shape[1]), dtype=emb_local.dtype, device=dev)
         rows[mine] = out_local[ids[mine] - b0]
@@ -77,7 +109,18 @@ def lightgcn_train_step_dist(dg: DistributedGraph, emb_local: torch.nn.Parameter
     with torch.no_grad():
         dy = torch.zeros_like(emb_local)
         dy.index_add_(0, ids[mine] - b0, rb.grad[mine])
-        grad = lightgcn_propagate_dist(dg, _exchanged(dg, dy), n_layers, hop_fn=hop_fn)
+        bwd_masks = None
+        if native:   # hops 1..K-1 skip the zero rows; hop 1 also the rows none reaches
+            from ..ops.functional import row_nonzero
+
+            def bwd_masks(k, x_in):
+                if k >= K:
+                    return None
+                xm = row_nonzero(x_in)
+                ya = dg.local_slice(_reach(dg, dg.local_slice(xm))) if k == 1 else None
+                return xm, ya
+        grad = lightgcn_propagate_dist(dg, _exchanged(dg, dy), K, hop_fn=hop_fn,
+                                       masks=bwd_masks)
         if max_grad_norm > 0:
             sq = (grad.double() ** 2).sum().view(1)
             _all_reduce(sq, dg)

@@ -79,3 +79,30 @@ def test_sharded_step_world1_native_matches_reference(cuda):
     np.testing.assert_allclose(losses, f["losses"], rtol=1e-5)
     np.testing.assert_allclose(emb.detach()[:nu].cpu().numpy(), f["user_w"], atol=2e-5)
     np.testing.assert_allclose(emb.detach()[nu:].cpu().numpy(), f["item_w"], atol=2e-5)
+
+
+def test_sharded_step_row_subset_same_bits(cuda):
+    """The sharded step's row-subset forward and masked backward (native hops) give the
+    same bits as its full propagation."""
+    from conftest import load_golden
+    from src.models import LightGCN
+    from src.ops.distributed import DistributedGraph
+    from src.training import lightgcn_train_step_dist
+    f = load_golden("bpr_train_K3_d64")
+    g, nu, ni = _golden_graph()
+    torch.manual_seed(56)
+    m = LightGCN(nu, ni, embedding_dim=64, n_layers=3, init_scale=0.1)
+    x0 = torch.cat([m.user_embedding.weight, m.item_embedding.weight]).detach()
+    dg = DistributedGraph(g, 0, 1, cuda)
+    res = []
+    for subset in (True, False):
+        emb = torch.nn.Parameter(x0.to(cuda).clone())
+        opt = torch.optim.Adam([emb], lr=1e-2, weight_decay=1e-4)
+        losses = [float(lightgcn_train_step_dist(dg, emb, 3, nu,
+                                                 *[torch.from_numpy(f[k][b]).to(cuda)
+                                                   for k in ("users", "pos", "neg")], opt,
+                                                 row_subset=subset))
+                  for b in range(3)]
+        res.append((losses, emb.detach().clone()))
+    assert res[0][0] == res[1][0]
+    assert torch.equal(res[0][1], res[1][1])

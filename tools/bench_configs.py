@@ -228,12 +228,19 @@ def main(argv=None):
             samp = DeviceSampler(users, items, 1_000_000, 2048, 1, device, seed=0)
             opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-4)
             loss_fn = BPRLoss()
-            with torch.enable_grad():
-                t, loss = timed(lambda: train_step(m, g1, *samp(), opt, loss_fn, 1.0),
-                                a.steps, a.warmup, 1, device)
+            res = {}
+            for subset in (True, False):
+                with torch.enable_grad():
+                    res[subset] = timed(lambda: train_step(m, g1, *samp(), opt, loss_fn, 1.0,
+                                                           row_subset=subset),
+                                        a.steps, a.warmup, 1, device)
+            t, loss = res[True]
+            # equiv_edges_per_s: the 2*K*nnz edge messages of the reference's full forward +
+            # backward, per step time (the row-subset forward skips most of the forward's)
             emit({"config": 6, "workload": "G100M LightGCN K=3 d=64 BPR train step (batch 2048, "
-                  "fwd + fused bwd propagation, Adam)", "nnz": g1.nnz, "ms": t,
-                  "edges_per_s": 2 * 3 * g1.nnz / (t * 1e-3), "loss": float(loss)})
+                  "row-subset fwd + masked bwd propagation, Adam)", "nnz": g1.nnz, "ms": t,
+                  "ms_full_forward": res[False][0],
+                  "equiv_edges_per_s": 2 * 3 * g1.nnz / (t * 1e-3), "loss": float(loss)})
             del m, g1, opt, samp
         if 8 in a.configs and world == 1:
             from src.ops import score_topk
