@@ -108,7 +108,9 @@ def lightgcn_train_step_dist(dg: DistributedGraph, emb_local: torch.nn.Parameter
     loss.backward()
     with torch.no_grad():
         dy = torch.zeros_like(emb_local)
-        dy.index_add_(0, ids[mine] - b0, rb.grad[mine])
+        # sort-based accumulate (deterministic, as autograd's indexing backward), not
+        # index_add_'s atomics: repeated batch rows sum in a fixed order
+        dy.index_put_((ids[mine] - b0,), rb.grad[mine], accumulate=True)
         bwd_masks = None
         if native:   # hops 1..K-1 skip the zero rows; hop 1 also the rows none reaches
             from ..ops.functional import row_nonzero

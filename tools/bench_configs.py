@@ -214,7 +214,7 @@ def main(argv=None):
                 t, loss = timed(step9, a.steps, a.warmup, world, device)
             emit({"config": 9, "workload": "G100M LightGCN K=3 d=64 BPR train step, row-sharded "
                   "(batch 2048, fwd + bwd propagation with per-hop exchanges, sharded Adam)",
-                  "nnz": g100.nnz, "ms": t, "edges_per_s": 2 * 3 * g100.nnz / (t * 1e-3),
+                  "nnz": g100.nnz, "ms": t, "equiv_edges_per_s": 2 * 3 * g100.nnz / (t * 1e-3),
                   "loss": float(loss), "exchange": dg.exchange_mode if world > 1 else None})
             del dg, emb, opt
         if 6 in a.configs and world == 1:
