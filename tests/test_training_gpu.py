@@ -9,9 +9,11 @@ from test_training import _golden_graph, _run_steps
 pytestmark = pytest.mark.gpu
 
 
-def test_three_adam_steps_native_match_reference(cuda):
+@pytest.mark.parametrize("fused", [False, True])
+def test_three_adam_steps_native_match_reference(cuda, fused):
+    """Golden pinned by the reference trainer; fused=True is make_adam's GPU optimizer."""
     g, _, _ = _golden_graph()
-    f, m, losses = _run_steps(g.to(cuda), cuda)
+    f, m, losses = _run_steps(g.to(cuda), cuda, fused=fused)
     # forward is bit-exact; the backward sums in a different order than torch's sparse
     # transpose-mm, and Adam normalises the gradient, so hold it to fp32 tolerance
     np.testing.assert_allclose(losses, f["losses"], rtol=1e-5)

@@ -195,14 +195,14 @@ def main(argv=None):
             emit(rec)
             del m, dg, x0p, work, mine
         if 9 in a.configs:
-            from src.training import lightgcn_train_step_dist
+            from src.training import lightgcn_train_step_dist, make_adam
             torch.manual_seed(0)
             m = LightGCN(1_000_000, 1_000_000, 64, 3, 0.1)
             dg = DistributedGraph(g100, rank, world, device)
             x0 = m._initial_table().detach()
             emb = torch.nn.Parameter(x0[dg.row_begin:dg.row_end].to(device).clone())
             del m, x0
-            opt = torch.optim.Adam([emb], lr=1e-3, weight_decay=1e-4)
+            opt = make_adam([emb], 1e-3, 1e-4, device)
             gen = torch.Generator().manual_seed(0)      # the same batches on every rank
 
             def step9():
@@ -218,7 +218,7 @@ def main(argv=None):
                   "loss": float(loss), "exchange": dg.exchange_mode if world > 1 else None})
             del dg, emb, opt
         if 6 in a.configs and world == 1:
-            from src.training import BPRLoss, DeviceSampler, train_step
+            from src.training import BPRLoss, DeviceSampler, make_adam, train_step
             torch.manual_seed(0)
             m = LightGCN(1_000_000, 1_000_000, 64, 3, 0.1).to(device).train()
             g1 = g100.to(device)
@@ -226,7 +226,7 @@ def main(argv=None):
             users = np.repeat(np.arange(1_000_000), np.diff(rp[:1_000_001]))
             items = g100.col.numpy()[:rp[1_000_000]] - 1_000_000
             samp = DeviceSampler(users, items, 1_000_000, 2048, 1, device, seed=0)
-            opt = torch.optim.Adam(m.parameters(), lr=1e-3, weight_decay=1e-4)
+            opt = make_adam(m.parameters(), 1e-3, 1e-4, device)
             loss_fn = BPRLoss()
             res = {}
             for subset in (True, False):
