@@ -34,6 +34,7 @@ import torch.distributed as dist
 
 from ..ops.distributed import DistributedGraph, _exchanged, lightgcn_propagate_dist
 from .losses import BPRLoss
+from .optim import NativeAdam
 
 
 def _all_reduce(t: torch.Tensor, dg: DistributedGraph, op=dist.ReduceOp.SUM) -> torch.Tensor:
@@ -123,12 +124,17 @@ def lightgcn_train_step_dist(dg: DistributedGraph, emb_local: torch.nn.Parameter
                 return xm, ya
         grad = lightgcn_propagate_dist(dg, _exchanged(dg, dy), K, hop_fn=hop_fn,
                                        masks=bwd_masks)
+        coef = None
         if max_grad_norm > 0:
-            sq = (grad.double() ** 2).sum().view(1)
+            sq = (torch.linalg.vector_norm(grad, 2, dtype=torch.float64) ** 2).view(1)
             _all_reduce(sq, dg)
             coef = torch.clamp(max_grad_norm / (sq.sqrt() + 1e-6), max=1.0).to(grad.dtype)
-            grad.mul_(coef)
+            if not isinstance(optimizer, NativeAdam):
+                grad.mul_(coef)
     optimizer.zero_grad()
     emb_local.grad = grad
-    optimizer.step()
+    if isinstance(optimizer, NativeAdam):
+        optimizer.step(grad_scale=coef)
+    else:
+        optimizer.step()
     return loss.detach()

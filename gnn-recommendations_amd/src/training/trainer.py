@@ -28,6 +28,7 @@ import torch.nn as nn
 
 from ..evaluation.evaluator import Evaluator
 from .losses import BPRLoss
+from .optim import NativeAdam
 from .sampler import DeviceSampler, ReferenceSampler
 
 
@@ -45,10 +46,24 @@ def bpr_scores(user_emb: torch.Tensor, item_emb: torch.Tensor, users: torch.Tens
 
 def make_adam(params, lr: float, weight_decay: float, device) -> torch.optim.Optimizer:
     """The reference's optimizer (trainer.py:59-63: Adam with L2 weight decay); on a GPU the
-    fused single-kernel form (one pass over param/grad/moments instead of the multi-tensor
-    loop's ~75 launches per step: 3.3 ms -> see DESIGN §6b at G100M)."""
-    fused = torch.device(device).type == "cuda"
-    return torch.optim.Adam(params, lr=lr, weight_decay=weight_decay, fused=fused)
+    native one-kernel-per-parameter form (NativeAdam)."""
+    if torch.device(device).type == "cuda":
+        return NativeAdam(params, lr=lr, weight_decay=weight_decay)
+    return torch.optim.Adam(params, lr=lr, weight_decay=weight_decay)
+
+
+def clip_and_step(params, optimizer, max_grad_norm: float) -> None:
+    """clip_grad_norm_(params, max_grad_norm) + optimizer.step(); NativeAdam takes the clip
+    coefficient into its update instead of scaling the gradients in place (same product)."""
+    if max_grad_norm > 0 and isinstance(optimizer, NativeAdam):
+        grads = [p.grad for p in params if p.grad is not None]
+        total = torch.nn.utils.get_total_norm(grads, 2.0)
+        coef = torch.clamp(max_grad_norm / (total + 1e-6), max=1.0)
+        optimizer.step(grad_scale=coef)
+        return
+    if max_grad_norm > 0:
+        torch.nn.utils.clip_grad_norm_(params, max_grad_norm)
+    optimizer.step()
 
 
 def batch_rows(n_users: int, n_items: int, users, pos_items, neg_items) -> torch.Tensor:
@@ -82,9 +97,7 @@ def train_step(model: nn.Module, adj, users, pos_items, neg_items, optimizer,
         loss = loss + model.get_regularization_loss()
     optimizer.zero_grad()
     loss.backward()
-    if max_grad_norm > 0:
-        torch.nn.utils.clip_grad_norm_(model.parameters(), max_grad_norm)
-    optimizer.step()
+    clip_and_step(list(model.parameters()), optimizer, max_grad_norm)
     return loss.detach()
 
 

@@ -309,6 +309,19 @@ int gnnrec_normalize_values_device(const int64_t* row_ptr, const int32_t* col, c
                                    int64_t n_rows, const float* dis, int32_t mode, float* val,
                                    gnnrec_stream_t stream);
 
+/* ---- §8f1: optimizer step of the training path ------------------------------------------
+ * Replaces torch.optim.Adam.step (L2 weight decay, no amsgrad) that the reference trainer
+ * runs after every batch (trainer.py:59-63, 271-272) for one fp32 parameter of n elements:
+ * param, grad, exp_avg, exp_avg_sq device arrays, 16-B aligned. The caller keeps the step
+ * count and passes step_size = lr / (1 - beta1^t) and bias_correction2_sqrt =
+ * sqrt(1 - beta2^t) (computed in double, as torch does). grad_scale (device float, may be
+ * NULL) multiplies the gradient first — clip_grad_norm_'s coefficient without a pass over
+ * the gradient. The gradient is not modified. Async on `stream`. */
+int gnnrec_adam_step_f32(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                         int64_t n, float step_size, float beta1, float beta2,
+                         float bias_correction2_sqrt, float eps, float weight_decay,
+                         const float* grad_scale, gnnrec_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

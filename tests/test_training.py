@@ -9,7 +9,8 @@ from conftest import golden_csr, load_golden
 
 from src.models import LightGCN
 from src.ops import CsrGraph
-from src.training import BPRLoss, DeviceSampler, ReferenceSampler, Trainer, bpr_scores, train_step
+from src.training import (BPRLoss, DeviceSampler, ReferenceSampler, Trainer, bpr_scores, make_adam,
+                          train_step)
 
 
 def _golden_graph():
@@ -39,13 +40,14 @@ def test_bpr_loss_keeps_the_broadcast():
     assert torch.equal(BPRLoss()(pos, neg), ref)
 
 
-def _run_steps(adj, device, row_subset=True, fused=False):
+def _run_steps(adj, device, row_subset=True, native_adam=False):
     f = load_golden("bpr_train_K3_d64")
     _, nu, ni = _golden_graph()
     torch.manual_seed(56)
     m = LightGCN(nu, ni, embedding_dim=64, n_layers=3, init_scale=0.1).to(device)
     np.testing.assert_array_equal(m.user_embedding.weight.detach().cpu().numpy(), f["user_w0"])
-    opt = torch.optim.Adam(m.parameters(), lr=1e-2, weight_decay=1e-4, fused=fused)
+    opt = (make_adam(m.parameters(), 1e-2, 1e-4, device) if native_adam
+           else torch.optim.Adam(m.parameters(), lr=1e-2, weight_decay=1e-4))
     m.train()
     losses = []
     for b in range(3):

@@ -9,11 +9,11 @@ from test_training import _golden_graph, _run_steps
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("fused", [False, True])
-def test_three_adam_steps_native_match_reference(cuda, fused):
-    """Golden pinned by the reference trainer; fused=True is make_adam's GPU optimizer."""
+@pytest.mark.parametrize("opt", ["torch", "native"])
+def test_three_adam_steps_native_match_reference(cuda, opt):
+    """Golden pinned by the reference trainer; "native" is make_adam's GPU optimizer."""
     g, _, _ = _golden_graph()
-    f, m, losses = _run_steps(g.to(cuda), cuda, fused=fused)
+    f, m, losses = _run_steps(g.to(cuda), cuda, native_adam=opt == "native")
     # forward is bit-exact; the backward sums in a different order than torch's sparse
     # transpose-mm, and Adam normalises the gradient, so hold it to fp32 tolerance
     np.testing.assert_allclose(losses, f["losses"], rtol=1e-5)
@@ -73,7 +73,8 @@ def test_sharded_step_world1_native_matches_reference(cuda):
     x0 = torch.cat([m.user_embedding.weight, m.item_embedding.weight]).detach()
     dg = DistributedGraph(g, 0, 1, cuda)
     emb = torch.nn.Parameter(x0.to(cuda).clone())
-    opt = torch.optim.Adam([emb], lr=1e-2, weight_decay=1e-4)
+    from src.training import make_adam
+    opt = make_adam([emb], 1e-2, 1e-4, cuda)      # NativeAdam, clip folded into its update
     losses = [float(lightgcn_train_step_dist(dg, emb, 3, nu,
                                              *[torch.from_numpy(f[k][b]).to(cuda)
                                                for k in ("users", "pos", "neg")], opt))
@@ -108,3 +109,31 @@ def test_sharded_step_row_subset_same_bits(cuda):
         res.append((losses, emb.detach().clone()))
     assert res[0][0] == res[1][0]
     assert torch.equal(res[0][1], res[1][1])
+
+
+def test_native_adam_matches_torch_adam(cuda):
+    """NativeAdam (one kernel per parameter, optional clip coefficient) follows
+    torch.optim.Adam's update within fp32 rounding over several steps, odd sizes included."""
+    from src.training import NativeAdam
+    torch.manual_seed(0)
+    shapes = [(1000, 64), (7,), (33, 3)]
+    p1 = [torch.nn.Parameter(torch.randn(s, device=cuda)) for s in shapes]
+    p2 = [torch.nn.Parameter(p.detach().clone()) for p in p1]
+    o1 = NativeAdam(p1, lr=1e-2, weight_decay=1e-4)
+    o2 = torch.optim.Adam(p2, lr=1e-2, weight_decay=1e-4)
+    for it in range(5):
+        grads = [torch.randn(s, device=cuda) for s in shapes]
+        scale = torch.tensor(0.5 if it % 2 else 1.0, device=cuda)
+        for a, b, g in zip(p1, p2, grads):
+            a.grad = g.clone()
+            b.grad = g * scale
+        o1.step(grad_scale=scale)
+        o2.step()
+        assert torch.equal(p1[0].grad, grads[0])          # the gradient is left unscaled
+    for a, b in zip(p1, p2):
+        np.testing.assert_allclose(a.detach().cpu().numpy(), b.detach().cpu().numpy(),
+                                   rtol=1e-6, atol=1e-7)
+    st1, st2 = o1.state[p1[0]], o2.state[p2[0]]
+    np.testing.assert_allclose(st1["exp_avg_sq"].cpu().numpy(), st2["exp_avg_sq"].cpu().numpy(),
+                               rtol=1e-6, atol=1e-12)
+    assert float(st1["step"]) == float(st2["step"]) == 5
