@@ -130,9 +130,9 @@ def test_native_adam_matches_torch_adam(cuda):
         o1.step(grad_scale=scale)
         o2.step()
         assert torch.equal(p1[0].grad, grads[0])          # the gradient is left unscaled
-    for a, b in zip(p1, p2):
+    for a, b in zip(p1, p2):   # a few ulps of the O(1) weights (updates are O(lr) = 1e-2)
         np.testing.assert_allclose(a.detach().cpu().numpy(), b.detach().cpu().numpy(),
-                                   rtol=1e-6, atol=1e-7)
+                                   rtol=1e-6, atol=1e-6)
     st1, st2 = o1.state[p1[0]], o2.state[p2[0]]
     np.testing.assert_allclose(st1["exp_avg_sq"].cpu().numpy(), st2["exp_avg_sq"].cpu().numpy(),
                                rtol=1e-6, atol=1e-12)
