@@ -61,8 +61,8 @@ __global__ __launch_bounds__(kAdamBlock) void adam_kernel(float* __restrict__ p,
 using namespace gnnrec;
 
 extern "C" int gnnrec_adam_step_f32(float* param, const float* grad, float* exp_avg,
-                                    float* exp_avg_sq, int64_t n, float step_size, float beta1,
-                                    float beta2, float bias_correction2_sqrt, float eps,
+                                    float* exp_avg_sq, int64_t n, float step_size, double beta1,
+                                    double beta2, float bias_correction2_sqrt, float eps,
                                     float weight_decay, const float* grad_scale,
                                     gnnrec_stream_t stream) {
   GNNREC_REQUIRE(n >= 0, "adam: negative size");
@@ -71,8 +71,10 @@ extern "C" int gnnrec_adam_step_f32(float* param, const float* grad, float* exp_
   GNNREC_REQUIRE(aligned16(param) && aligned16(grad) && aligned16(exp_avg) && aligned16(exp_avg_sq),
                  "adam: tensors must be 16-B aligned");
   GNNREC_REQUIRE(bias_correction2_sqrt > 0.f, "adam: bias_correction2_sqrt must be > 0");
-  const AdamArgs a{step_size, beta1, beta2, 1.f - beta1, 1.f - beta2, bias_correction2_sqrt, eps,
-                   weight_decay};
+  // 1 - beta in double, then rounded (as torch's Python-scalar arithmetic does: 1 - 0.999f
+  // would be 1.3e-5 off)
+  const AdamArgs a{step_size,         (float)beta1,          (float)beta2, (float)(1.0 - beta1),
+                   (float)(1.0 - beta2), bias_correction2_sqrt, eps,          weight_decay};
   const int64_t want = ceil_div(ceil_div(n, 4), kAdamBlock);
   const unsigned grid = (unsigned)(want < 8192 ? want : 8192);
   hipLaunchKernelGGL(adam_kernel, dim3(grid), dim3(kAdamBlock), 0, as_hip(stream), param, grad,

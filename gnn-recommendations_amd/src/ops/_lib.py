@@ -69,7 +69,8 @@ _SIGNATURES = {
     "gnnrec_build_bipartite_csr_device": [_p, _p, _i64, _i64, _i64, _i32, _p, _p, _p, _p, _p,
                                           _p, _p, _p],
     "gnnrec_normalize_values_device": [_p, _p, _p, _i64, _p, _i32, _p, _p],
-    "gnnrec_adam_step_f32": [_p, _p, _p, _p, _i64, _f32, _f32, _f32, _f32, _f32, _f32, _p, _p],
+    "gnnrec_adam_step_f32": [_p, _p, _p, _p, _i64, _f32, C.c_double, C.c_double, _f32, _f32,
+                             _f32, _p, _p],
 }
 _RESTYPES = {"gnnrec_version": C.c_char_p, "gnnrec_last_error": C.c_char_p,
              "gnnrec_abi_version": C.c_int}

@@ -318,7 +318,7 @@ int gnnrec_normalize_values_device(const int64_t* row_ptr, const int32_t* col, c
  * NULL) multiplies the gradient first — clip_grad_norm_'s coefficient without a pass over
  * the gradient. The gradient is not modified. Async on `stream`. */
 int gnnrec_adam_step_f32(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
-                         int64_t n, float step_size, float beta1, float beta2,
+                         int64_t n, float step_size, double beta1, double beta2,
                          float bias_correction2_sqrt, float eps, float weight_decay,
                          const float* grad_scale, gnnrec_stream_t stream);
 
