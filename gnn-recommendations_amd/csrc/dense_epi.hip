@@ -115,9 +115,34 @@ __global__ __launch_bounds__(64 * NW) void spmm_mfma_kernel(DenseParams p) {
   __syncthreads();
 
   const int64_t n_tiles = ceil_div(p.A.n_rows, TR);
+  // GATHER = false streams rows: the next tile's rows are loaded into registers while this
+  // tile multiplies and stores (one tile in flight per workgroup doubles the bytes in flight)
+  VecF<VEC> pre_n[GATHER ? 1 : PASSES], pre_x[GATHER ? 1 : PASSES];
+  auto load_rows = [&](int64_t tile, VecF<VEC>* n, VecF<VEC>* xs) {
+#pragma unroll
+    for (int ps = 0; ps < PASSES; ++ps) {
+      const int64_t r = tile * TR + ps * PASS_ROWS + wave * RPW + lane / GROUP;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) n[ps].v[q] = xs[ps].v[q] = 0.f;
+      if (tile < n_tiles && r < p.A.n_rows) {
+        n[ps] = ldv<VEC>(p.x + r * p.ldx + VEC * gl);
+        if (MODE == 0) xs[ps] = ldv<VEC>(p.x_self + r * p.ld_self + VEC * gl);
+      }
+    }
+  };
+  if constexpr (!GATHER) load_rows(blockIdx.x, pre_n, pre_x);
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     const int64_t row0 = tile * TR;
     // ---- phase 1: gather rows into the A tile
+    VecF<VEC> cur_n[GATHER ? 1 : PASSES], cur_x[GATHER ? 1 : PASSES];
+    if constexpr (!GATHER) {
+#pragma unroll
+      for (int ps = 0; ps < PASSES; ++ps) {
+        cur_n[ps] = pre_n[ps];
+        cur_x[ps] = pre_x[ps];
+      }
+      load_rows(tile + gridDim.x, pre_n, pre_x);
+    }
 #pragma unroll
     for (int ps = 0; ps < PASSES; ++ps) {
       const int slot = ps * PASS_ROWS + wave * RPW + lane / GROUP;
@@ -125,13 +150,15 @@ __global__ __launch_bounds__(64 * NW) void spmm_mfma_kernel(DenseParams p) {
       VecF<VEC> n, xs;
 #pragma unroll
       for (int q = 0; q < VEC; ++q) n.v[q] = xs.v[q] = 0.f;
-      if (r < p.A.n_rows) {
-        if constexpr (GATHER)
+      if constexpr (GATHER) {
+        if (r < p.A.n_rows) {
           n = gather_row_v<VEC, GROUP, CH>(p.A.col, p.A.val, p.A.row_ptr[r], p.A.row_ptr[r + 1],
                                            p.x, p.ldx, gl);
-        else
-          n = ldv<VEC>(p.x + r * p.ldx + VEC * gl);
-        if (MODE == 0) xs = ldv<VEC>(p.x_self + r * p.ld_self + VEC * gl);
+          if (MODE == 0) xs = ldv<VEC>(p.x_self + r * p.ld_self + VEC * gl);
+        }
+      } else {
+        n = cur_n[ps];
+        xs = cur_x[ps];
       }
 #pragma unroll
       for (int q = 0; q < VEC; ++q) {
