@@ -36,27 +36,17 @@ class NGCFLayer(nn.Module):
             and self.W1.in_features == self.W1.out_features
             and self.W1.in_features in (32, 64, 128))
 
-    def native_ok(self, x: torch.Tensor, a, gas: Optional[nn.Module] = None) -> bool:
-        return self._fused_ok(x, a) and (gas is None or gas.fusable())
-
-    def forward(self, x: torch.Tensor, adj_matrix, gas: Optional[nn.Module] = None,
-                out: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """`out`: a row-major [N, out_dim] view to write the native path's result into."""
+    def forward(self, x: torch.Tensor, adj_matrix, gas: Optional[nn.Module] = None) -> torch.Tensor:
         a = ops.as_operand(adj_matrix)
-        if self.native_ok(x, a, gas):
+        if self._fused_ok(x, a) and (gas is None or gas.fusable()):
             blocks, perm = (gas.blocks(), gas.perm) if gas is not None else (None, None)
             return ops.ngcf_layer(a, x, self.W1.weight, self.W1.bias, self.W2.weight,
                                   self.W2.bias, self.activation.negative_slope,
-                                  gas_blocks=blocks, gas_perm=perm, fused=self.single_kernel,
-                                  out=out)
+                                  gas_blocks=blocks, gas_perm=perm, fused=self.single_kernel)
         n = ops.sparse_mm(a, x)
-        h = self.W1(n) + self.W2(x * n)
-        h = self.dropout(self.activation(h))
-        h = gas(h) if gas is not None else h
-        if out is not None:
-            out.copy_(h)
-            return out
-        return h
+        out = self.W1(n) + self.W2(x * n)
+        out = self.dropout(self.activation(out))
+        return gas(out) if gas is not None else out
 
 
 class NGCF(BaseRecommender):
@@ -85,35 +75,15 @@ class NGCF(BaseRecommender):
                 nn.init.xavier_uniform_(lin.weight)
                 nn.init.zeros_(lin.bias)
 
-    def _layers_forward(self, adj_matrix, gs_layers=None) -> Tuple[torch.Tensor, torch.Tensor]:
-        """x_final = cat(x0, x1, ..., xK) along features (ngcf.py:178-186). When every layer
-        takes the native path, the layers write straight into their column slice of one
-        [N, sum(dims)] table (their next input is that slice): no concat pass (2 GB at
-        G100M)."""
+    def forward(self, adj_matrix) -> Tuple[torch.Tensor, torch.Tensor]:
         x = self._initial_table()
-        gs_layers = list(gs_layers) if gs_layers is not None else [None] * self.n_layers
-        a = ops.as_operand(adj_matrix)
-        widths = [x.shape[1]] + [layer.W1.out_features for layer in self.layers]
-        if isinstance(a, CsrGraph) and all(
-                layer.native_ok(x, a, gs) and layer.W1.in_features == widths[0]
-                for layer, gs in zip(self.layers, gs_layers)):
-            x_final = torch.empty((x.shape[0], sum(widths)), dtype=x.dtype, device=x.device)
-            x_final[:, :widths[0]].copy_(x)
-            c = widths[0]
-            for layer, gs, w in zip(self.layers, gs_layers, widths[1:]):
-                layer(x_final[:, c - widths[0]:c], a, gas=gs, out=x_final[:, c:c + w])
-                c += w
-        else:
-            outs = [x]
-            for layer, gs in zip(self.layers, gs_layers):
-                x = layer(x, adj_matrix, gas=gs)
-                outs.append(x)
-            x_final = torch.cat(outs, dim=1)
+        outs = [x]
+        for layer in self.layers:
+            x = layer(x, adj_matrix)
+            outs.append(x)
+        x_final = torch.cat(outs, dim=1)
         user_emb, item_emb = torch.split(x_final, [self.n_users, self.n_items], dim=0)
         return user_emb, item_emb
-
-    def forward(self, adj_matrix) -> Tuple[torch.Tensor, torch.Tensor]:
-        return self._layers_forward(adj_matrix)
 
     def predict(self, users, items, adj_matrix=None) -> torch.Tensor:
         if adj_matrix is None:
@@ -142,4 +112,11 @@ class NGCFGroupShuffle(NGCF):
                                        for d in self.layer_sizes)
 
     def forward(self, adj_matrix) -> Tuple[torch.Tensor, torch.Tensor]:
-        return self._layers_forward(adj_matrix, self.gs_layers)
+        x = self._initial_table()
+        outs = [x]
+        for layer, gs in zip(self.layers, self.gs_layers):
+            x = layer(x, adj_matrix, gas=gs)
+            outs.append(x)
+        x_final = torch.cat(outs, dim=1)
+        user_emb, item_emb = torch.split(x_final, [self.n_users, self.n_items], dim=0)
+        return user_emb, item_emb
