@@ -107,10 +107,26 @@ __global__ __launch_bounds__(64 * NW) void spmm_mfma_kernel(DenseParams p) {
   int pj[VEC];
 #pragma unroll
   for (int q = 0; q < VEC; ++q) pj[q] = 0;
+  // GAS on the matrix cores when each wave owns one output tile (d <= 64): out = o @ G with
+  // G[k][j] = blockdiag(blocks)[k][perm[j]], the B fragments (D/4 per lane) in VGPRs. The
+  // MFMA chain runs over all k in order; the off-block terms are fmaf(o, +0, acc) == acc, so
+  // the bits equal gas_row_v's 8-term chain (o is a finite LeakyReLU output).
+  constexpr bool GAS_MFMA = MODE == 0 && TPW == 1 && TILES == NW && D <= 64;
+  float gf[GAS_MFMA ? D / 4 : 1];
   if (gas) {
     for (int i = threadIdx.x; i < D * p.gas_bs; i += NTH) w_gas[i] = p.gas_blocks[i];
 #pragma unroll
     for (int q = 0; q < VEC; ++q) pj[q] = p.gas_perm[VEC * gl + q];
+    if constexpr (GAS_MFMA) {
+      const int bs = p.gas_bs;
+      const int c = p.gas_perm[16 * (wave % NT) + i16];   // output column j -> z column c
+      const int b = c / bs, e = c - b * bs;
+#pragma unroll
+      for (int st = 0; st < D / 4; ++st) {
+        const int k = 4 * st + k4;
+        gf[st] = (k / bs == b) ? p.gas_blocks[(int64_t)(b * bs + (k - b * bs)) * bs + e] : 0.f;
+      }
+    }
   }
   __syncthreads();
 
@@ -201,6 +217,20 @@ __global__ __launch_bounds__(64 * NW) void spmm_mfma_kernel(DenseParams p) {
       }
     }
     __syncthreads();
+    if constexpr (GAS_MFMA) {
+      if (gas) {  // phase 2b: o_tile @ G on MFMA, written back over o_tile
+        const int mt = wave / NT, nt = wave % NT;
+        floatx4 c = {0.f, 0.f, 0.f, 0.f};
+        const float* arow = &o_lds[16 * mt + i16][k4];
+#pragma unroll
+        for (int st = 0; st < D / 4; ++st)
+          c = __builtin_amdgcn_mfma_f32_16x16x4f32(arow[4 * st], gf[st], c, 0, 0, 0);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o_lds[16 * mt + 4 * k4 + q][16 * nt + i16] = c[q];
+        __syncthreads();
+      }
+    }
     // ---- phase 3: row epilogue + coalesced store
 #pragma unroll
     for (int ps = 0; ps < PASSES; ++ps) {
@@ -209,7 +239,7 @@ __global__ __launch_bounds__(64 * NW) void spmm_mfma_kernel(DenseParams p) {
       if (r >= p.A.n_rows) continue;
       VecF<VEC> o;
       if (MODE == 0) {
-        if (gas) {
+        if (gas && !GAS_MFMA) {
           o = gas_row_v<VEC>(&o_lds[slot][0], w_gas, p.gas_bs, pj);
         } else {
 #pragma unroll

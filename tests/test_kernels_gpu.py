@@ -186,6 +186,10 @@ def test_ngcf_gas_vs_oracle(cuda, d, fused):
                      gas_perm=T(perm), fused=fused).cpu().numpy()
     ref = oracle.gas(oracle.ngcf_layer(rp, col, val, x, W1, b1, W2, b2, 0.2), blocks, perm)
     np.testing.assert_allclose(y, ref, rtol=0, atol=1e-5)
+    # the epilogue GAS (MFMA for d <= 64, VALU above) == the standalone VALU GAS kernel on
+    # the un-transformed layer output, bit for bit
+    plain = F.ngcf_layer(g, T(x), T(W1), T(b1), T(W2), T(b2), 0.2, fused=fused)
+    np.testing.assert_array_equal(bits(y), bits(F.gas(plain, T(blocks), T(perm)).cpu().numpy()))
 
 
 @pytest.mark.parametrize("fused", [False, True])
