@@ -69,23 +69,30 @@ __global__ __launch_bounds__(kBlock) void spmm_generic_kernel(
 
 // Heavy rows (one workgroup of kHeavyThreads per listed row). The bit-exact order makes a row
 // one sequential fmaf chain per feature, so a long row cannot be split; what is parallelised
-// is the GATHER: all 8 waves fetch neighbour rows into an LDS double buffer (a chunk =
-// kHeavyChunkFloats fp32 = 64 KB of neighbour rows) while wave 0 runs the chain over the
-// other half. Loads are software-pipelined: in round c the workgroup issues the row gathers
-// of chunk c+2 (whose columns arrived in round c-1) and the (col, val) loads of chunk c+3,
-// wave 0 consumes chunk c from LDS, and chunk c+1 (gathered in round c-1) is parked in the
-// free LDS half. A row gather never waits behind its own column load, and every load has the
-// consumer's whole round to land.
+// is the GATHER. Wave 0 is the consumer and does nothing but the chain; waves 1..7 (the
+// loaders) fetch the neighbour rows chunk by chunk into an LDS double buffer. Software
+// pipeline, round c: the loaders issue the row gathers of chunk c+2 (whose columns arrived in
+// round c-1) and the (col, val) loads of chunk c+3, then park chunk c+1 (gathered in round
+// c-1) in the free buffer, while wave 0 consumes chunk c; one barrier per round.
+//
+// The parked chunk is stored FEATURE-major, [d][S] with S = chk + 2 (S/2 odd): consumer lane f
+// reads neighbours j, j+1 of its feature with one conflict-free ds_read_b64 (two per 4
+// neighbours, plus one 16-B broadcast read of their 4 values), so the consumer issues ~1.75
+// instructions per neighbour around its dependent fmaf instead of a ds_read_b32 each.
 constexpr int kHeavyThreads = 512;
-constexpr int kHeavyChunkFloats = 16384;                 // per LDS buffer
-constexpr int kHeavyPieces = kHeavyChunkFloats / 4 / kHeavyThreads;  // float4 per thread
+constexpr int kHeavyLoaders = kHeavyThreads - 64;       // waves 1..7
+constexpr int kHeavyBufFloats = 16384;                   // per LDS buffer (64 KB)
 constexpr int kHeavyMinD = 16;
-constexpr int kHeavyMaxChunkRows = kHeavyChunkFloats / kHeavyMinD;   // 1024
-constexpr int kHeavyVals = kHeavyMaxChunkRows / kHeavyThreads;       // vals per thread
-constexpr size_t kHeavyLds = 2 * kHeavyChunkFloats * sizeof(float) +
-                             2 * kHeavyMaxChunkRows * sizeof(float);
+constexpr int kHeavyMaxChunk = kHeavyBufFloats / kHeavyMinD;          // vals per buffer
+constexpr int kHeavyPieces = (kHeavyBufFloats / 4 + kHeavyLoaders - 1) / kHeavyLoaders;  // 10
+constexpr int kHeavyVals = (kHeavyMaxChunk + kHeavyLoaders - 1) / kHeavyLoaders;         // 3
+constexpr size_t kHeavyLds = 2 * kHeavyBufFloats * sizeof(float) +
+                             2 * kHeavyMaxChunk * sizeof(float);
 
-struct HeavyCols {        // (col, val) of one chunk, as this thread needs them
+// Neighbours per chunk (a multiple of 4) for a row width d: chk + 2 <= 16384 / d.
+__host__ __device__ constexpr int heavy_chunk(int d) { return ((kHeavyBufFloats / d - 2) / 4) * 4; }
+
+struct HeavyCols {        // (col, val) of one chunk, as this loader thread needs them
   int c[kHeavyPieces];
   float v[kHeavyVals];
 };
@@ -94,36 +101,38 @@ struct HeavyStage {       // one chunk's gathered rows + vals in flight in regis
   float v[kHeavyVals];
 };
 
-// F: features per consumer lane (d <= 64 F); DC: d as a compile-time constant (0 = runtime d),
-// which turns the consumer's LDS addressing into immediate offsets.
+// F: features per consumer lane (d <= 64 F); DC: d as a compile-time constant (0 = runtime d).
 template <int F, int DC>
 __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
     Csr A, const int64_t* __restrict__ rows, const float* __restrict__ x, int64_t ldx,
     float* __restrict__ y, int64_t ldy, int d_rt, int epi, const float* __restrict__ self,
     int64_t ld_self, float* __restrict__ acc, int64_t ld_acc, float acc_div) {
   const int d = DC ? DC : d_rt;
-  constexpr int STEP = 16 / F;                           // neighbours per consumer step
   extern __shared__ float4 heavy_lds4[];
-  float* buf = reinterpret_cast<float*>(heavy_lds4);     // [2][kHeavyChunkFloats]
-  float* vbuf = buf + 2 * kHeavyChunkFloats;             // [2][kHeavyMaxChunkRows]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* buf = reinterpret_cast<float*>(heavy_lds4);     // [2][kHeavyBufFloats]: [d][S] each
+  float* vbuf = buf + 2 * kHeavyBufFloats;               // [2][kHeavyMaxChunk]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const bool consumer = tid < 64;
+  const int lt = tid - 64;                               // loader thread index
   const int64_t r = rows[blockIdx.x];
   const int64_t beg = A.row_ptr[r], end = A.row_ptr[r + 1];
   const int q4 = d >> 2;                                 // float4 per neighbour row
-  const int chk = kHeavyChunkFloats / d;                 // neighbours per chunk (<= 4096)
+  const int chk = heavy_chunk(d);                        // neighbours per chunk
+  const int S = chk + 2;                                 // LDS row stride of a feature
+  const int npieces = chk * q4;
   const int64_t n_chunks = (end - beg + chk - 1) / chk;
 
   auto load_cols = [&](int64_t c, HeavyCols& hc) {
     const int64_t k0 = beg + c * chk;
 #pragma unroll
     for (int i = 0; i < kHeavyPieces; ++i) {
-      const int j = (tid + i * kHeavyThreads) / q4;
-      const int64_t k = k0 + j;
-      hc.c[i] = (c < n_chunks && j < chk && k < end) ? A.col[k] : -1;
+      const int p = lt + i * kHeavyLoaders;
+      const int64_t k = k0 + p / q4;
+      hc.c[i] = (c < n_chunks && p < npieces && k < end) ? A.col[k] : -1;
     }
 #pragma unroll
     for (int i = 0; i < kHeavyVals; ++i) {
-      const int j = tid + i * kHeavyThreads;
+      const int j = lt + i * kHeavyLoaders;
       const int64_t k = k0 + j;
       hc.v[i] = (c < n_chunks && j < chk && k < end) ? A.val[k] : 0.f;
     }
@@ -131,7 +140,7 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
   auto gather = [&](const HeavyCols& hc, HeavyStage& st) {
 #pragma unroll
     for (int i = 0; i < kHeavyPieces; ++i) {
-      const int p = tid + i * kHeavyThreads, part = p - (p / q4) * q4;
+      const int p = lt + i * kHeavyLoaders, part = p - (p / q4) * q4;
       st.x[i] = hc.c[i] >= 0
                     ? *reinterpret_cast<const float4*>(x + (int64_t)hc.c[i] * ldx + 4 * part)
                     : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -140,16 +149,22 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
     for (int i = 0; i < kHeavyVals; ++i) st.v[i] = hc.v[i];
   };
   auto park = [&](const HeavyStage& st, int b) {
-    float4* dst = reinterpret_cast<float4*>(buf + b * kHeavyChunkFloats);
+    float* dst = buf + b * kHeavyBufFloats;
 #pragma unroll
     for (int i = 0; i < kHeavyPieces; ++i) {
-      const int p = tid + i * kHeavyThreads;
-      if (p / q4 < chk) dst[p] = st.x[i];
+      const int p = lt + i * kHeavyLoaders;
+      if (p < npieces) {
+        const int j = p / q4, f0 = 4 * (p - j * q4);
+        dst[(f0 + 0) * S + j] = st.x[i].x;
+        dst[(f0 + 1) * S + j] = st.x[i].y;
+        dst[(f0 + 2) * S + j] = st.x[i].z;
+        dst[(f0 + 3) * S + j] = st.x[i].w;
+      }
     }
 #pragma unroll
     for (int i = 0; i < kHeavyVals; ++i) {
-      const int j = tid + i * kHeavyThreads;
-      if (j < chk) vbuf[b * kHeavyMaxChunkRows + j] = st.v[i];
+      const int j = lt + i * kHeavyLoaders;
+      if (j < chk) vbuf[b * kHeavyMaxChunk + j] = st.v[i];
     }
   };
 
@@ -158,74 +173,86 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
   for (int f = 0; f < F; ++f) a[f] = 0.f;
   // consumer lanes: feature lane + 64 f, clamped into the row so no lane is masked off (a
   // clamped lane computes a duplicate it never stores) and the LDS reads need no branches
-  int fcol[F];
+  int fo[F];
 #pragma unroll
-  for (int f = 0; f < F; ++f) fcol[f] = min(lane + 64 * f, d - 1);
-  // One step = the LDS reads of STEP neighbours, then their ordered FMAs. The chain itself
-  // (one dependent fmaf per neighbour) bounds the consumer.
+  for (int f = 0; f < F; ++f) fo[f] = min(lane + 64 * f, d - 1) * S;
+  // One step = 4 neighbours: their values (one broadcast float4) and, per feature, two
+  // float2 reads of the feature-major chunk; then the 4 ordered fmafs per feature.
   struct Step {
-    float v[STEP];
-    float x[STEP][F];
+    float4 v;
+    float2 x[F][2];
   };
   auto fetch = [&](const float* xb, const float* vb, int j, Step& st) {
+    st.v = *reinterpret_cast<const float4*>(vb + j);
 #pragma unroll
-    for (int t = 0; t < STEP; t += 4) {   // vals: one 16-B broadcast read per 4 neighbours
-      const float4 v4 = *reinterpret_cast<const float4*>(vb + j + t);
-      st.v[t] = v4.x; st.v[t + 1] = v4.y; st.v[t + 2] = v4.z; st.v[t + 3] = v4.w;
+    for (int f = 0; f < F; ++f) {
+      st.x[f][0] = *reinterpret_cast<const float2*>(xb + fo[f] + j);
+      st.x[f][1] = *reinterpret_cast<const float2*>(xb + fo[f] + j + 2);
     }
-#pragma unroll
-    for (int t = 0; t < STEP; ++t)
-#pragma unroll
-      for (int f = 0; f < F; ++f) st.x[t][f] = xb[(j + t) * d + fcol[f]];
   };
   auto apply = [&](const Step& st) {
 #pragma unroll
-    for (int t = 0; t < STEP; ++t)
+    for (int f = 0; f < F; ++f) a[f] = __builtin_fmaf(st.v.x, st.x[f][0].x, a[f]);
 #pragma unroll
-      for (int f = 0; f < F; ++f) a[f] = __builtin_fmaf(st.v[t], st.x[t][f], a[f]);
+    for (int f = 0; f < F; ++f) a[f] = __builtin_fmaf(st.v.y, st.x[f][0].y, a[f]);
+#pragma unroll
+    for (int f = 0; f < F; ++f) a[f] = __builtin_fmaf(st.v.z, st.x[f][1].x, a[f]);
+#pragma unroll
+    for (int f = 0; f < F; ++f) a[f] = __builtin_fmaf(st.v.w, st.x[f][1].y, a[f]);
   };
   auto consume = [&](int64_t c) {
-    const float* xb = buf + (c & 1) * kHeavyChunkFloats;
-    const float* vb = vbuf + (c & 1) * kHeavyMaxChunkRows;
+    const float* xb = buf + (c & 1) * kHeavyBufFloats;
+    const float* vb = vbuf + (c & 1) * kHeavyMaxChunk;
     const int m = (int)min<int64_t>(chk, end - (beg + c * chk));
-    const int steps = m / STEP;
-    for (int q = 0; q < steps; ++q) {   // (a two-set software pipeline measured 6 % slower)
-      Step s0;
-      fetch(xb, vb, q * STEP, s0);
+    const int steps = m >> 2;
+    // two register sets: the reads of step q+1 are in flight while step q's chain runs
+    Step s0, s1;
+    if (steps > 0) fetch(xb, vb, 0, s0);
+    int q = 0;
+    for (; q + 2 <= steps; q += 2) {
+      fetch(xb, vb, 4 * (q + 1), s1);
       apply(s0);
+      fetch(xb, vb, 4 * min(q + 2, steps - 1), s0);
+      apply(s1);
     }
-    for (int j = steps * STEP; j < m; ++j) {
+    if (q < steps) apply(s0);
+    for (int j = steps * 4; j < m; ++j) {
       const float v = vb[j];
 #pragma unroll
-      for (int f = 0; f < F; ++f) a[f] = __builtin_fmaf(v, xb[j * d + fcol[f]], a[f]);
+      for (int f = 0; f < F; ++f) a[f] = __builtin_fmaf(v, xb[fo[f] + j], a[f]);
     }
   };
 
-  // prologue: chunk 0 parked, chunk 1 gathering, columns of chunk 2 loading
+  // prologue (loaders): chunk 0 parked, chunk 1 gathering, columns of chunk 2 loading
   HeavyCols ca, cb;
   HeavyStage sa, sb;
-  load_cols(0, ca);
-  gather(ca, sa);
-  load_cols(1, cb);
-  park(sa, 0);
-  gather(cb, sb);
-  load_cols(2, ca);
+  if (!consumer) {
+    load_cols(0, ca);
+    gather(ca, sa);
+    load_cols(1, cb);
+    park(sa, 0);
+    gather(cb, sb);
+    load_cols(2, ca);
+  }
   __syncthreads();
-  // round c: columns of c+3 -> gather of c+2 -> consume c -> park c+1 -> barrier.
+  // round c: loaders gather c+2, load the columns of c+3, park c+1; wave 0 consumes c.
   // Unrolled by two so the register sets alternate statically.
   auto round = [&](int64_t c, HeavyCols& cols_c2, HeavyCols& cols_c3, HeavyStage& st_c1,
                    HeavyStage& st_c2) {
-    gather(cols_c2, st_c2);                  // columns of c+2 arrived during round c-1
-    load_cols(c + 3, cols_c3);
-    if (wave == 0) consume(c);
-    if (c + 1 < n_chunks) park(st_c1, (int)((c + 1) & 1));
+    if (consumer) {
+      consume(c);
+    } else {
+      gather(cols_c2, st_c2);                // columns of c+2 arrived during round c-1
+      load_cols(c + 3, cols_c3);
+      if (c + 1 < n_chunks) park(st_c1, (int)((c + 1) & 1));
+    }
     __syncthreads();
   };
   for (int64_t c = 0; c < n_chunks; c += 2) {
     round(c, ca, cb, sb, sa);                // c+1 in sb, c+2 -> sa, cols c+2 in ca, c+3 -> cb
     if (c + 1 < n_chunks) round(c + 1, cb, ca, sa, sb);
   }
-  if (wave != 0) return;
+  if (!consumer) return;
 #pragma unroll
   for (int f = 0; f < F; ++f) {
     const int col_f = lane + 64 * f;
