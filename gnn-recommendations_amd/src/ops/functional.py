@@ -47,6 +47,25 @@ def _csr_args(adj: CsrGraph):
 SPMM_HEAVY_THRESHOLD = 256
 
 
+# Column-ordered hop (gnnrec_spmm_tiled_f32): the same bits, used for d = 64
+# when the operand fills at least one pass of the persistent grid (256 CUs x 600 rows) and has
+# no row longer than TILED_MAX_DEGREE (a long row's panel run stays on one wave and would hold
+# its step). G100M hop: 6.99 -> 5.55 ms. Masked / row-subset hops keep the CSR kernel.
+TILED_HOP = True
+TILED_MIN_ROWS = 256 * 600
+TILED_MAX_DEGREE = 4096
+
+
+def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None):
+    """The column-ordered plan spmm_into would use for (adj, x), or None (CSR kernel)."""
+    if (not TILED_HOP or x_mask is not None or y_active is not None or x.shape[1] != 64
+            or adj.n_rows < TILED_MIN_ROWS or adj.nnz == 0
+            or x.shape[0] * x.stride(0) * 4 >= 1 << 32
+            or adj.max_degree() > TILED_MAX_DEGREE):
+        return None
+    return adj.tiled_plan(x.stride(0))
+
+
 def _heavy_args(adj: CsrGraph, x: torch.Tensor, heavy_threshold: int):
     """(heavy_rows ptr, n_heavy, threshold) for the split launch, or the no-split triple."""
     d = x.shape[1]
@@ -82,6 +101,10 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
                                  or y_active.numel() < adj.n_rows):
         raise ValueError("y_active must be a uint8 tensor on x's device with a byte per "
                          "destination row")
+    plan = tiled_plan_for(adj, x, x_mask, y_active)
+    if plan is not None:
+        spmm_tiled_into(adj, x, y, plan, epi=epi, self_rows=self_rows, acc=acc, acc_div=acc_div)
+        return
     check(L.gnnrec_spmm_csr_masked_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(x_mask),
                                        ptr(y_active), ptr(y), y.stride(0) if y is not None else d, d, epi,
                                        ptr(self_rows),
@@ -89,6 +112,23 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
                                        ptr(acc), acc.stride(0) if acc is not None else d,
                                        float(acc_div), *_heavy_args(adj, x, ht),
                                        _lib.stream_of(adj.device)), "gnnrec_spmm_csr_masked_f32")
+
+
+def spmm_tiled_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], plan: dict, *,
+                    epi: int = 0, self_rows: Optional[torch.Tensor] = None,
+                    acc: Optional[torch.Tensor] = None, acc_div: float = 1.0) -> None:
+    """spmm_into through the column-ordered kernel with an explicit plan (adj.tiled_plan(ldx)
+    for this x's row stride); same results, bit for bit. The plan's sync words make
+    concurrent launches of one plan on different streams unsafe."""
+    _require_device(adj, x, y, self_rows, acc)
+    d = x.shape[1]
+    check(_lib.lib().gnnrec_spmm_tiled_f32(
+        ptr(plan["xoff"]), ptr(plan["val"]), ptr(plan["meta"]), ptr(plan["wave_ptr"]),
+        ptr(plan["n_steps"]), plan["n_blocks"], plan["rows_per_block"], ptr(x), x.shape[0],
+        x.stride(0), ptr(y), y.stride(0) if y is not None else d, adj.n_rows, d, epi,
+        ptr(self_rows), self_rows.stride(0) if self_rows is not None else d, ptr(acc),
+        acc.stride(0) if acc is not None else d, float(acc_div), ptr(plan["sync"]),
+        _lib.stream_of(adj.device)), "gnnrec_spmm_tiled_f32")
 
 
 def row_nonzero(x: torch.Tensor) -> torch.Tensor:
@@ -195,6 +235,9 @@ def lightgcn_forward(adj: CsrGraph, x0: torch.Tensor, n_layers: int,
     n, d = x0.shape
     if adj.n_rows != n or adj.shape[1] != n:
         raise ValueError("LightGCN propagation needs a square operand matching x0")
+    if not return_layers and tiled_plan_for(adj, x0) is not None:
+        # per-hop launches of the column-ordered kernel, same epilogue order and bits
+        return _lightgcn_hops(adj, x0, int(n_layers), lambda k, x_in: (None, None)), None
     out = torch.empty_like(x0)
     layers = work0 = work1 = None
     if return_layers:

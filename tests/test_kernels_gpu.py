@@ -371,3 +371,67 @@ def test_lightgcn_forward_rows_equal_full(cuda, K, d):
     F.spmm_into(g, x0, y2)
     sel = ya.bool()
     np.testing.assert_array_equal(bits(y1[sel].cpu().numpy()), bits(y2[sel].cpu().numpy()))
+
+
+# ---- column-ordered ("tiled") hop: gnnrec_spmm_tiled_f32 ------------------------------------
+@pytest.mark.parametrize("R,panel", [(600, 32768), (37, 64), (1, 1), (600, 1 << 30)])
+def test_spmm_tiled_bit_exact(cuda, R, panel):
+    g, (rp, col, val) = random_graph(3000, 2500, 60000, R + panel, cuda, heavy_user=2400)
+    x = torch.randn(g.shape[0], 64, generator=torch.Generator().manual_seed(R)) * 0.1
+    ref = bits(oracle.spmm(rp, col, val, x.numpy()))
+    xd = x.to(cuda)
+    plan = g.tiled_plan(64, rows_per_block=R, panel=panel)
+    y = torch.full((g.shape[0], 64), float("nan"), device=cuda)
+    F.spmm_tiled_into(g, xd, y, plan)
+    np.testing.assert_array_equal(bits(y.cpu().numpy()), ref)
+    F.spmm_tiled_into(g, xd, y, plan)                   # sync words reset per launch
+    np.testing.assert_array_equal(bits(y.cpu().numpy()), ref)
+
+
+def test_spmm_tiled_epilogues_strides_and_empty_rows(cuda):
+    g, (rp, col, val) = random_graph(4000, 3000, 8000, 5, cuda)    # has empty rows
+    assert (np.diff(rp) == 0).any()
+    n = g.shape[0]
+    big = torch.randn(n, 96, device=cuda) * 0.1
+    x = big[:, 16:80]                                    # ldx = 96
+    xs = x.contiguous().cpu().numpy()
+    yr = oracle.spmm(rp, col, val, xs)
+    plan = g.tiled_plan(96, rows_per_block=100, panel=512)
+    acc = torch.empty(n, 64, device=cuda)
+    y = torch.full((n, 128), 7.0, device=cuda)
+    F.spmm_tiled_into(g, x, y[:, 32:96], plan, epi=_lib.EPI_ACC_INIT, self_rows=x, acc=acc)
+    np.testing.assert_array_equal(bits(y[:, 32:96].cpu().numpy()), bits(yr))
+    assert torch.all(y[:, :32] == 7.0) and torch.all(y[:, 96:] == 7.0)
+    np.testing.assert_array_equal(bits(acc.cpu().numpy()), bits(xs + yr))
+    acc2 = acc.clone()
+    F.spmm_tiled_into(g, x, None, plan, epi=_lib.EPI_ACC_ADD | _lib.EPI_ACC_DIV | _lib.EPI_NO_Y,
+                      acc=acc2, acc_div=3.0)
+    np.testing.assert_array_equal(bits(acc2.cpu().numpy()),
+                                  bits((acc.cpu().numpy() + yr) / np.float32(3.0)))
+
+
+def test_spmm_tiled_rejects_bad_arguments(cuda):
+    g, _ = random_graph(300, 200, 2000, 1, cuda)
+    plan = g.tiled_plan(32)
+    x = torch.zeros(g.shape[0], 32, device=cuda)
+    with pytest.raises(ValueError, match="d must be 64"):
+        F.spmm_tiled_into(g, x, torch.empty_like(x), plan)
+
+
+def test_lightgcn_through_tiled_hop_is_bit_exact(cuda, monkeypatch):
+    """The model path routes d=64 hops through the column-ordered kernel once the operand is
+    large enough (here forced): every output bit equals the oracle and the CSR path."""
+    g, (rp, col, val) = random_graph(6000, 5000, 150000, 9, cuda)
+    x = torch.randn(g.shape[0], 64, generator=torch.Generator().manual_seed(2)) * 0.1
+    ref = bits(oracle.lightgcn(rp, col, val, x.numpy(), 3))
+    xd = x.to(cuda)
+    monkeypatch.setattr(F, "TILED_HOP", False)
+    csr, _ = F.lightgcn_forward(g, xd, 3)
+    monkeypatch.setattr(F, "TILED_HOP", True)
+    monkeypatch.setattr(F, "TILED_MIN_ROWS", 0)
+    assert F.tiled_plan_for(g, xd) is not None
+    out, _ = F.lightgcn_forward(g, xd, 3)
+    np.testing.assert_array_equal(bits(out.cpu().numpy()), ref)
+    np.testing.assert_array_equal(bits(csr.cpu().numpy()), ref)
+    m = torch.zeros(g.shape[0], dtype=torch.uint8, device=cuda)
+    assert F.tiled_plan_for(g, xd, x_mask=m) is None     # masked hops keep the CSR kernel

@@ -98,6 +98,73 @@ def test_partition_covers_rows_and_remaps_columns(world):
         np.testing.assert_array_equal(glob, G.col.numpy()[k0:k0 + s.nnz])
 
 
+def _walk_tiled_plan(plan, n_rows, R, row_bytes=256):
+    """Replay gnnrec_spmm_tiled_f32's schedule on the host: per row, the (col, val) sequence
+    its accumulator receives, in kernel order; checks the plan's structural rules on the way."""
+    xo = plan["xoff"].numpy().view(np.uint32)
+    val = plan["val"].numpy()
+    meta = plan["meta"].numpy().view(np.uint16)
+    wp = plan["wave_ptr"].numpy()
+    ns = plan["n_steps"].numpy()
+    W, CH = 16, 16
+    seq = [[] for _ in range(n_rows)]
+    for b in range(plan["n_blocks"]):
+        owner = {}            # (step, row) -> wave: a row lives on one wave per step
+        events = []           # (step, wave, slot index, row, col, val)
+        for w in range(W):
+            s0, s1 = wp[b * W + w], wp[b * W + w + 1]
+            assert (s1 - s0) % CH == 0
+            cur = 0
+            for c in range(s0, s1, CH):
+                cur += (int(meta[c]) >> 10) & 31
+                for t in range(CH):
+                    m = int(meta[c + t])
+                    row, chain = m & 1023, m >> 15
+                    if t > 0:
+                        assert (m >> 10) & 31 == 0
+                        prev = int(meta[c + t - 1]) & 1023
+                        assert chain == (1 if (row == prev and row != R) else 0) or row == R
+                    if row == R:
+                        assert val[c + t] == 0 and chain == 0
+                        continue
+                    assert owner.setdefault((cur, row), w) == w
+                    assert xo[c + t] % row_bytes == 0
+                    events.append((cur, w, c + t, row, int(xo[c + t]) // row_bytes, val[c + t]))
+            assert cur <= max(ns[b] - 1, 0)
+        events.sort(key=lambda e: (e[0], e[2]))
+        for _, _, _, row, col, v in events:
+            seq[b * R + row].append((col, v))
+    return seq
+
+
+@pytest.mark.parametrize("R,panel", [(600, 32768), (37, 5), (1, 1), (16, 1 << 30)])
+def test_tiled_plan_preserves_every_row_chain(R, panel):
+    """The column-ordered plan visits each row's neighbours exactly in CSR order (ascending
+    columns: the fmaf order that makes the hop bit-exact), once each, one wave per row and
+    step, with chain flags exactly on run continuations inside a chunk."""
+    rng = np.random.default_rng(R + panel)
+    u = np.concatenate([rng.integers(0, 700, 6000), np.zeros(300, np.int64)])  # a long row
+    i = np.concatenate([rng.integers(0, 900, 6000), np.arange(300)])
+    G = CsrGraph.from_interactions(u, i, 701, 900)     # user 700: an empty row
+    plan = G.tiled_plan(64, rows_per_block=R, panel=panel)
+    n = G.shape[0]
+    assert plan["n_blocks"] == (n + R - 1) // R
+    assert plan["n_slots"] >= G.nnz and plan["xoff"].numel() == plan["n_slots"] + 16
+    seq = _walk_tiled_plan(plan, n, R)
+    rp, col, val = G.row_ptr.numpy(), G.col.numpy(), G.val.numpy()
+    for r in range(n):
+        got = seq[r]
+        assert [c for c, _ in got] == col[rp[r]:rp[r + 1]].tolist(), r
+        np.testing.assert_array_equal(np.array([v for _, v in got], np.float32),
+                                      val[rp[r]:rp[r + 1]])
+
+
+def test_tiled_plan_rejects_tables_over_4gb():
+    G = CsrGraph.from_interactions([0, 1], [0, 1], 2, 2)
+    with pytest.raises(ValueError, match="4 GB"):
+        G.tiled_plan(1 << 30)
+
+
 def test_heavy_row_plan_segments_cover_heavy_rows():
     rng = np.random.default_rng(0)
     u = np.concatenate([rng.integers(0, 30, 500), np.zeros(200, np.int64)])

@@ -261,9 +261,57 @@ __global__ __launch_bounds__(NW * 64) void stepped_hop(
   extern __shared__ float acc[];  // [(R+1)][64]
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nwc = ctr ? NW - 1 : NW;  // waves carrying edges
+  // slack < 0: no pacer wave; instead the workgroups of a blockIdx%8 group meet at every
+  // block (pass) start (counter barrier, bounded wait)
+  const bool pass_sync = ctr && slack < 0;
+  const int nwc = (ctr && !pass_sync) ? NW - 1 : NW;  // waves carrying edges
   const __amdgpu_buffer_rsrc_t xr =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0, (int)x_bytes, 0x00020000);
+  if (pass_sync) {
+    unsigned* c = ctr + (blockIdx.x % 8) * 32;
+    const long long G = gridDim.x / 8 + ((blockIdx.x % 8) < (gridDim.x % 8) ? 1 : 0);
+    long long p = 0;
+    for (int blk = blockIdx.x; blk < n_blocks; blk += gridDim.x, ++p) {
+      if (threadIdx.x == 0 && p > 0) {
+        __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long t0 = wall_clock64();
+        while ((long long)__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                   G * p && wall_clock64() - t0 < 20000)   // <= 200 us
+          __builtin_amdgcn_s_sleep(2);
+      }
+      for (int i = threadIdx.x; i < (R + 1) * 64; i += NW * 64) acc[i] = 0.f;
+      __syncthreads();  // B0
+      const int64_t s = (int64_t)blk * NW + w;
+      const int64_t b = wptr[s], e = wptr[s + 1];
+      int cur = 0;
+      if (b < e) {
+        Chunk2 A, B;
+        int64_t cc = b;
+        fetch2<GMODE>(sx, sv, sm, cc, xr, lane, A);
+        for (;;) {
+          fetch2<GMODE>(sx, sv, sm, cc + CH, xr, lane, B);
+          apply3<GMODE, ADDTID>(acc, lane, A, cur);
+          cc += CH;
+          if (cc >= e) break;
+          fetch2<GMODE>(sx, sv, sm, cc + CH, xr, lane, A);
+          apply3<GMODE, ADDTID>(acc, lane, B, cur);
+          cc += CH;
+          if (cc >= e) break;
+        }
+      }
+      const int ns = nsteps[blk];
+      for (int i = cur; i < ns; ++i) __syncthreads();
+      const int64_t r0 = (int64_t)blk * R;
+      for (int i = w; i < R; i += NW) {
+        const int64_t r = r0 + i;
+        if (r < n_rows) y[r * 64 + lane] = acc[i * 64 + lane];
+      }
+      __syncthreads();  // B_end
+    }
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_add(c, 1u << 24, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   if (w == nwc) {  // pacer
     unsigned* c = ctr + (blockIdx.x % 8) * 32;
     const long long G = gridDim.x / 8 + ((blockIdx.x % 8) < (gridDim.x % 8) ? 1 : 0);

@@ -201,7 +201,7 @@ def main():
             built = {}
             ctr = torch.zeros(8 * 32, dtype=torch.int32, device=dev)
             for mode, gm, slack in [(m, gm, sl) for m in a.modes for gm in a.grids for sl in a.slack]:
-                nw = 15 if slack else 16
+                nw = 15 if slack > 0 else 16
                 if nw not in built:
                     built.clear()
                     t0 = time.perf_counter()
