@@ -184,8 +184,15 @@ void push_slot(BlockPlan& bp, int w, uint32_t xo, float v, uint16_t m) {
   bp.meta[w].push_back(m);
 }
 
+struct Slot {
+  const Run* run;   // nullptr: dummy
+  int32_t t;        // edge of the run
+};
+
 void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_t n_rows,
-                 int R, int panel, int64_t row_bytes, int64_t b, BlockPlan& out) {
+                 int R, int panel, int sub_panel, int64_t row_bytes, int64_t b, BlockPlan& out) {
+  std::vector<Slot> slots, seq, pending, deferred;
+  std::vector<int> in_chunk, blocked;
   const int64_t r0 = b * R, r1 = std::min<int64_t>(n_rows, r0 + R);
   std::vector<Run> runs;
   for (int64_t r = r0; r < r1; ++r) {
@@ -226,27 +233,71 @@ void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_
     }
     for (int w = 0; w < kTiledWaves; ++w) {
       if (wl[w].empty()) continue;
-      int32_t bar = step - cur[w];
-      while (bar > kTiledMaxBar) {   // more barriers than the field holds: an empty chunk
-        for (int s = 0; s < kTiledChunk; ++s)
-          push_slot(out, w, 0u, 0.f, (uint16_t)(R | (s == 0 ? kTiledMaxBar << 10 : 0)));
-        bar -= kTiledMaxBar;
-      }
-      int s = 0;                      // slot inside the current chunk
-      uint32_t x0 = 0;                // xoff of the chunk's first slot (for dummies)
-      for (const Run* e : wl[w]) {
-        for (int t = 0; t < e->n; ++t) {
-          const int64_t k = e->k + t;
-          const uint32_t xo = (uint32_t)(col[k] * row_bytes);
-          if (s == 0) x0 = xo;
-          const int chain = (s > 0 && t > 0) ? 1 : 0;
-          push_slot(out, w, xo, val[k],
-                    (uint16_t)(e->row | (s == 0 ? bar << 10 : 0) | (chain << 15)));
-          if (s == 0) bar = 0;
-          s = (s + 1) % kTiledChunk;
+      // the wave's slots in ascending column sub-panel, rows in order inside one (a row's
+      // edges keep their column order): the group's waves sweep the panel together
+      slots.clear();
+      for (const Run* e : wl[w])
+        for (int t = 0; t < e->n; ++t) slots.push_back({e, t});
+      if (sub_panel > 0)
+        std::stable_sort(slots.begin(), slots.end(), [&](const Slot& a, const Slot& c) {
+          const int32_t ka = col[a.run->k + a.t] / sub_panel, kc = col[c.run->k + c.t] / sub_panel;
+          return ka != kc ? ka < kc : a.run->row < c.run->row;
+        });
+      // chunks: a row appears in a chunk only as one run of consecutive slots (the kernel reads
+      // every accumulator at the chunk start); a slot that would repeat a row non-adjacently is
+      // deferred to a later chunk with the rest of that row (per-row order kept)
+      seq.clear();
+      pending.swap(slots);
+      while (!pending.empty()) {
+        deferred.clear();
+        in_chunk.clear();
+        blocked.clear();
+        int n = 0, last = -1;
+        const size_t start = seq.size();
+        for (size_t q = 0; q < pending.size(); ++q) {
+          const Slot& sl = pending[q];
+          if (n == kTiledChunk) {   // chunk full: the rest keeps its order for the next ones
+            deferred.insert(deferred.end(), pending.begin() + q, pending.end());
+            break;
+          }
+          const int r = sl.run->row;
+          const bool is_blocked = std::find(blocked.begin(), blocked.end(), r) != blocked.end();
+          const bool seen = std::find(in_chunk.begin(), in_chunk.end(), r) != in_chunk.end();
+          if (is_blocked || (seen && r != last)) {
+            if (seen && r != last && !is_blocked) blocked.push_back(r);
+            deferred.push_back(sl);
+            continue;
+          }
+          seq.push_back(sl);
+          if (!seen) in_chunk.push_back(r);
+          last = r;
+          ++n;
         }
+        while (seq.size() - start < (size_t)kTiledChunk) seq.push_back({nullptr, 0});
+        pending.swap(deferred);
       }
-      for (; s != 0; s = (s + 1) % kTiledChunk) push_slot(out, w, x0, 0.f, (uint16_t)R);
+      int32_t bar = step - cur[w];
+      for (size_t c = 0; c < seq.size(); c += kTiledChunk) {
+        while (bar > kTiledMaxBar) {   // more barriers than the field holds: an empty chunk
+          for (int s = 0; s < kTiledChunk; ++s)
+            push_slot(out, w, 0u, 0.f, (uint16_t)(R | (s == 0 ? kTiledMaxBar << 10 : 0)));
+          bar -= kTiledMaxBar;
+        }
+        const uint32_t x0 = (uint32_t)(col[seq[c].run->k + seq[c].t] * row_bytes);
+        for (int s = 0; s < kTiledChunk; ++s) {
+          const Slot& sl = seq[c + s];
+          const int bits = s == 0 ? bar << 10 : 0;
+          if (!sl.run) {            // dummy: scratch row, value 0, an already-fetched row
+            push_slot(out, w, x0, 0.f, (uint16_t)(R | bits));
+            continue;
+          }
+          const int64_t k = sl.run->k + sl.t;
+          const int chain = (s > 0 && seq[c + s - 1].run == sl.run) ? 1 : 0;
+          push_slot(out, w, (uint32_t)(col[k] * row_bytes), val[k],
+                    (uint16_t)(sl.run->row | bits | (chain << 15)));
+        }
+        bar = 0;
+      }
       cur[w] = step;
     }
     ++step;
@@ -262,12 +313,14 @@ using namespace gnnrec;
 
 extern "C" int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* col,
                                        const float* val, int64_t n_rows, int32_t rows_per_block,
-                                       int32_t panel, int64_t row_bytes, int32_t n_threads,
-                                       void** plan, int64_t* n_slots, int64_t* n_blocks) {
+                                       int32_t panel, int32_t sub_panel, int64_t row_bytes,
+                                       int32_t n_threads, void** plan, int64_t* n_slots,
+                                       int64_t* n_blocks) {
   GNNREC_REQUIRE(row_ptr && plan && n_slots && n_blocks && n_rows >= 0, "tiled_plan: bad args");
   GNNREC_REQUIRE(rows_per_block >= 1 && rows_per_block <= GNNREC_TILED_MAX_ROWS,
                  "tiled_plan: rows_per_block must be in [1, %d]", GNNREC_TILED_MAX_ROWS);
-  GNNREC_REQUIRE(panel >= 1 && row_bytes > 0, "tiled_plan: bad panel / row_bytes");
+  GNNREC_REQUIRE(panel >= 1 && sub_panel >= 0 && row_bytes > 0,
+                 "tiled_plan: bad panel / sub_panel / row_bytes");
   const int64_t nnz = n_rows > 0 ? row_ptr[n_rows] - row_ptr[0] : 0;
   GNNREC_REQUIRE(nnz == 0 || (col && val), "tiled_plan: null col/val");
   auto* pl = new (std::nothrow) TiledPlan;
@@ -284,7 +337,8 @@ extern "C" int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* co
       for (int64_t k = row_ptr[r0]; k < row_ptr[r1]; ++k)
         if (col[k] < 0 || (int64_t)col[k] * row_bytes + row_bytes > (int64_t)UINT32_MAX)
           bad_col = true;
-      build_block(row_ptr, col, val, n_rows, rows_per_block, panel, row_bytes, b, pl->blocks[b]);
+      build_block(row_ptr, col, val, n_rows, rows_per_block, panel, sub_panel, row_bytes, b,
+                  pl->blocks[b]);
     }
   };
   std::vector<std::thread> pool;

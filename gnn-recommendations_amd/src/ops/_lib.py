@@ -43,7 +43,7 @@ _SIGNATURES = {
     "gnnrec_spmm_csr_masked_f32": [_p, _p, _p, _i64, _p, _i64, _p, _p, _p, _i64, _i32, _i32,
                                    _p, _i64, _p, _i64, _f32, _p, _i64, _i64, _p],
     "gnnrec_mark_active_rows": [_p, _p, _i64, _p, _i64, _p, _p],
-    "gnnrec_tiled_plan_build": [_p, _p, _p, _i64, _i32, _i32, _i64, _i32, _p, _p, _p],
+    "gnnrec_tiled_plan_build": [_p, _p, _p, _i64, _i32, _i32, _i32, _i64, _i32, _p, _p, _p],
     "gnnrec_tiled_plan_emit": [_p, _p, _p, _p, _p, _p],
     "gnnrec_tiled_plan_free": [_p],
     "gnnrec_spmm_tiled_f32": [_p, _p, _p, _p, _p, _i64, _i32, _p, _i64, _i64, _p, _i64, _i64,

@@ -354,13 +354,15 @@ class CsrGraph:
             self._plans["max_degree"] = int(deg.max()) if deg.numel() else 0
         return self._plans["max_degree"]
 
-    def tiled_plan(self, ldx: int, rows_per_block: int = 600, panel: int = 32768) -> dict:
+    def tiled_plan(self, ldx: int, rows_per_block: int = 600, panel: int = 131072,
+                   sub_panel: int = 4096) -> dict:
         """Column-ordered re-layout of this operand for gnnrec_spmm_tiled_f32 (DESIGN.md
         §3.1c), for x tables with row stride `ldx` (cached per stride): built once on the host
         from the CSR (gnnrec_tiled_plan_build/emit), uploaded to this graph's device.
         Defaults from the G100M sweep (profiles/r01/exp_tiled/): 600 rows per block fill the
-        LDS, 32K-column panels."""
-        key = ("tiled", int(ldx), int(rows_per_block), int(panel))
+        LDS, 128K-column panels (steps), each wave's slots in ascending 4K-column sub-panels
+        inside a step (0: no sub-panel order)."""
+        key = ("tiled", int(ldx), int(rows_per_block), int(panel), int(sub_panel))
         if key not in self._plans:
             import ctypes as C
             L = _lib.lib()
@@ -370,7 +372,8 @@ class CsrGraph:
             h, n_slots, n_blocks = C.c_void_p(), C.c_int64(), C.c_int64()
             _lib.check(L.gnnrec_tiled_plan_build(rp.ctypes.data, col.ctypes.data, val.ctypes.data,
                                                  self.n_rows, int(rows_per_block), int(panel),
-                                                 4 * int(ldx), 0, C.byref(h), C.byref(n_slots),
+                                                 int(sub_panel), 4 * int(ldx), 0, C.byref(h),
+                                                 C.byref(n_slots),
                                                  C.byref(n_blocks)), "gnnrec_tiled_plan_build")
             nb = n_blocks.value
             total = n_slots.value + 16                     # + GNNREC_TILED_CHUNK tail slots

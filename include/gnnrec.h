@@ -149,7 +149,7 @@ int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col, const
 
 int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* col, const float* val,
                             int64_t n_rows, int32_t rows_per_block, int32_t panel,
-                            int64_t row_bytes, int32_t n_threads, void** plan,
+                            int32_t sub_panel, int64_t row_bytes, int32_t n_threads, void** plan,
                             int64_t* n_slots, int64_t* n_blocks);
 int gnnrec_tiled_plan_emit(void* plan, uint32_t* xoff, float* val, uint16_t* meta,
                            int64_t* wave_ptr, int32_t* n_steps);

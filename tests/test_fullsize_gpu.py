@@ -36,6 +36,11 @@ def test_g100m_lightgcn_every_layer_bit_exact(cuda, g100m):
         acc = acc + x
     ref = acc / np.float32(4.0)
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    # the bench path: no per-layer outputs, so the hops run through the column-ordered kernel
+    gd, xd = g.to(cuda), torch.from_numpy(x0).to(cuda)
+    assert F.tiled_plan_for(gd, xd) is not None
+    out_t, _ = F.lightgcn_forward(gd, xd, 3)
+    np.testing.assert_array_equal(out_t.cpu().numpy().view(np.uint32), ref.view(np.uint32))
 
 
 def test_g100m_device_builder_bit_identical(cuda, g100m):

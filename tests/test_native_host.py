@@ -117,6 +117,10 @@ def _walk_tiled_plan(plan, n_rows, R, row_bytes=256):
             cur = 0
             for c in range(s0, s1, CH):
                 cur += (int(meta[c]) >> 10) & 31
+                rows_in_chunk = [int(meta[c + t]) & 1023 for t in range(CH)]
+                runs = [r for t, r in enumerate(rows_in_chunk)
+                        if r != R and (t == 0 or rows_in_chunk[t - 1] != r)]
+                assert len(runs) == len(set(runs)), "a row must be one run inside a chunk"
                 for t in range(CH):
                     m = int(meta[c + t])
                     row, chain = m & 1023, m >> 15
@@ -137,16 +141,18 @@ def _walk_tiled_plan(plan, n_rows, R, row_bytes=256):
     return seq
 
 
-@pytest.mark.parametrize("R,panel", [(600, 32768), (37, 5), (1, 1), (16, 1 << 30)])
-def test_tiled_plan_preserves_every_row_chain(R, panel):
+@pytest.mark.parametrize("R,panel,sub", [(600, 32768, 0), (600, 131072, 4096), (37, 5, 2),
+                                         (37, 64, 8), (1, 1, 0), (16, 1 << 30, 64)])
+def test_tiled_plan_preserves_every_row_chain(R, panel, sub):
     """The column-ordered plan visits each row's neighbours exactly in CSR order (ascending
     columns: the fmaf order that makes the hop bit-exact), once each, one wave per row and
-    step, with chain flags exactly on run continuations inside a chunk."""
-    rng = np.random.default_rng(R + panel)
+    step, a row at most one run of slots per chunk (sub-panel order interleaves rows), with
+    chain flags exactly on run continuations inside a chunk."""
+    rng = np.random.default_rng(R + panel + sub)
     u = np.concatenate([rng.integers(0, 700, 6000), np.zeros(300, np.int64)])  # a long row
     i = np.concatenate([rng.integers(0, 900, 6000), np.arange(300)])
     G = CsrGraph.from_interactions(u, i, 701, 900)     # user 700: an empty row
-    plan = G.tiled_plan(64, rows_per_block=R, panel=panel)
+    plan = G.tiled_plan(64, rows_per_block=R, panel=panel, sub_panel=sub)
     n = G.shape[0]
     assert plan["n_blocks"] == (n + R - 1) // R
     assert plan["n_slots"] >= G.nnz and plan["xoff"].numel() == plan["n_slots"] + 16
