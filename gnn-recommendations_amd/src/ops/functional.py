@@ -50,10 +50,22 @@ SPMM_HEAVY_THRESHOLD = 256
 # Column-ordered hop (gnnrec_spmm_tiled_f32): the same bits, used for d = 64
 # when the operand fills at least one pass of the persistent grid (256 CUs x 600 rows) and has
 # no row longer than TILED_MAX_DEGREE (a long row's panel run stays on one wave and would hold
-# its step). G100M hop: 6.99 -> 5.55 ms. Masked / row-subset hops keep the CSR kernel.
+# its step). G100M hop: 6.99 -> 5.23 ms. Masked / row-subset hops keep the CSR kernel.
+# Rows per block are evened out so every pass of the persistent grid is full (G100M: 14
+# passes of 559 rows instead of 13 of 600 plus a 6-block tail pass).
 TILED_HOP = True
 TILED_MIN_ROWS = 256 * 600
 TILED_MAX_DEGREE = 4096
+TILED_MAX_ROWS = 600                 # GNNREC_TILED_MAX_ROWS
+TILED_BALANCE_PASSES = True
+
+
+def _tiled_rows_per_block(n_rows: int, device) -> int:
+    if not TILED_BALANCE_PASSES:
+        return TILED_MAX_ROWS
+    cus = torch.cuda.get_device_properties(device).multi_processor_count
+    passes = -(-n_rows // (cus * TILED_MAX_ROWS))
+    return min(TILED_MAX_ROWS, -(-n_rows // (passes * cus)))
 
 
 def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None):
@@ -63,7 +75,7 @@ def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None):
             or x.shape[0] * x.stride(0) * 4 >= 1 << 32
             or adj.max_degree() > TILED_MAX_DEGREE):
         return None
-    return adj.tiled_plan(x.stride(0))
+    return adj.tiled_plan(x.stride(0), rows_per_block=_tiled_rows_per_block(adj.n_rows, x.device))
 
 
 def _heavy_args(adj: CsrGraph, x: torch.Tensor, heavy_threshold: int):

@@ -15,7 +15,10 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
-constexpr int NW = 16;  // waves per workgroup
+#ifndef EXP_NW
+#define EXP_NW 16
+#endif
+constexpr int NW = EXP_NW;  // waves per workgroup
 constexpr int CH = 16;
 
 template <int MODE>

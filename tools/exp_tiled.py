@@ -23,7 +23,8 @@ import bench  # noqa: E402
 from src.ops import functional as F  # noqa: E402
 
 CH = 16
-lib = C.CDLL(str(ROOT / "tools" / "exp_tiled.so"))
+import os  # noqa: E402
+lib = C.CDLL(str(ROOT / "tools" / os.environ.get("EXP_TILED_SO", "exp_tiled.so")))
 lib.exp_stepped_hop.argtypes = [C.c_int] + [C.c_void_p] * 6 + [C.c_int64, C.c_void_p, C.c_int64,
                                                               C.c_int, C.c_int, C.c_int,
                                                               C.c_void_p, C.c_int, C.c_void_p]
@@ -201,7 +202,7 @@ def main():
             built = {}
             ctr = torch.zeros(8 * 32, dtype=torch.int32, device=dev)
             for mode, gm, slack in [(m, gm, sl) for m in a.modes for gm in a.grids for sl in a.slack]:
-                nw = 15 if slack > 0 else 16
+                nw = 15 if slack > 0 else a.nw
                 if nw not in built:
                     built.clear()
                     t0 = time.perf_counter()

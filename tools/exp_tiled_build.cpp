@@ -17,6 +17,7 @@
 #include <cstdint>
 #include <cstring>
 #include <vector>
+#include <cstdlib>
 
 namespace {
 
@@ -43,6 +44,7 @@ constexpr int kMaxBar = 31;
 
 void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_t N, int R,
                  int Wp, int NW, int CH, int64_t row_bytes, int64_t b, BlockOut& out) {
+  static const int sub = getenv("EXP_SUB") ? atoi(getenv("EXP_SUB")) : 0;
   const int64_t r0 = b * R, r1 = std::min<int64_t>(N, r0 + R);
   std::vector<Entry> ent;
   for (int64_t r = r0; r < r1; ++r) {
@@ -88,7 +90,46 @@ void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_
       std::vector<std::pair<const Entry*, int>> slots;
       for (const Entry* e : wl[w])
         for (int t = 0; t < e->n; ++t) slots.push_back({e, t});
-      const int C = (int)((slots.size() + CH - 1) / CH);
+      if (sub > 0)   // column sub-panels in ascending order inside the step (rows keep order)
+        std::stable_sort(slots.begin(), slots.end(), [&](const std::pair<const Entry*, int>& a,
+                                                         const std::pair<const Entry*, int>& c) {
+          const int32_t ka = col[a.first->k + a.second] / sub, kc = col[c.first->k + c.second] / sub;
+          if (ka != kc) return ka < kc;
+          return a.first->row < c.first->row;
+        });
+      // chunking: a row may appear in a chunk only as one contiguous run (the kernel reads all
+      // accumulators at the chunk start); a slot that would repeat a row non-adjacently is
+      // deferred to a later chunk together with that row's later slots (per-row order kept)
+      std::vector<std::pair<const Entry*, int>> seq;   // padded to chunks; first == null: dummy
+      {
+        std::vector<std::pair<const Entry*, int>> pending = slots, deferred;
+        std::vector<int> in_chunk;
+        std::vector<int> blocked;
+        while (!pending.empty()) {
+          deferred.clear();
+          in_chunk.clear();
+          blocked.clear();
+          int n = 0, last = -1;
+          const size_t start = seq.size();
+          for (const auto& sl : pending) {
+            const int r = sl.first->row;
+            const bool is_blocked = std::find(blocked.begin(), blocked.end(), r) != blocked.end();
+            const bool seen = std::find(in_chunk.begin(), in_chunk.end(), r) != in_chunk.end();
+            if (n == CH || is_blocked || (seen && r != last)) {
+              if (seen && r != last && !is_blocked) blocked.push_back(r);
+              deferred.push_back(sl);
+              continue;
+            }
+            seq.push_back(sl);
+            if (!seen) in_chunk.push_back(r);
+            last = r;
+            ++n;
+          }
+          while (seq.size() - start < (size_t)CH) seq.push_back({nullptr, 0});
+          pending.swap(deferred);
+        }
+      }
+      const int C = (int)(seq.size() / CH);
       int32_t bar = step - cur[w];
       for (int c = 0; c < C; ++c) {
         while (bar > kMaxBar) {   // more barriers than the field holds: an empty chunk
@@ -100,19 +141,19 @@ void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_
           bar -= kMaxBar;
         }
         const size_t base = (size_t)c * CH;
-        const int64_t k0 = slots[base].first->k + slots[base].second;
+        const int64_t k0 = seq[base].first->k + seq[base].second;
         const uint32_t x0 = (uint32_t)(col[k0] * row_bytes);
         for (int s = 0; s < CH; ++s) {
           uint32_t xo = x0;
           float v = 0.f;
           int row = R, chain = 0;
-          if (base + s < slots.size()) {
-            const auto& sl = slots[base + s];
+          const auto& sl = seq[base + s];
+          if (sl.first) {
             const int64_t k = sl.first->k + sl.second;
             xo = (uint32_t)(col[k] * row_bytes);
             v = val[k];
             row = sl.first->row;
-            chain = (s > 0 && sl.second > 0) ? 1 : 0;
+            chain = (s > 0 && seq[base + s - 1].first == sl.first) ? 1 : 0;
           }
           out.xoff[w].push_back(xo);
           out.val[w].push_back(v);
