@@ -18,9 +18,13 @@ point-to-point with 1/4/8 overlap chunks, whichever whole steps time fastest bef
 timed region (src/ops/distributed.py); t_step = max over ranks.
 
 Also reported: roofline of the dominant kernel (the SpMM hop) from HIP events around every
-hop launch inside the timed region, the PMC-measured HBM traffic per launch when a
-profile summary exists under profiles/, and the reference's CPU SpMM (COO
-torch.sparse.mm, restated in oracle/torch_ref.py) timed on this host's cores.
+hop launch inside the timed region — `achieved`/`frac` on SURVEY §8(d)'s compulsory bytes
+B_hop = 8 nnz + 8 (rows+1) + 4 d |src| + 4 d rows, and beside it the same launch priced with
+its fused layer-mean epilogue bytes — the PMC-measured HBM traffic per launch when a profile
+summary made from THIS kernel source and plan exists under profiles/ (else null), and the
+reference's CPU path (SURVEY §8 d3, restated op for op in oracle/torch_ref.py) on this host's
+cores: the scipy operand build over every pair and the full K-hop torch.sparse.mm propagation
++ stack().mean(0), each compared bit for bit with the GPU's operand, hop 1 and output.
 """
 from __future__ import annotations
 
@@ -40,6 +44,7 @@ sys.path.insert(0, str(ROOT / "gnn-recommendations_amd"))
 sys.path.insert(0, str(ROOT))
 
 from src.ops import CsrGraph  # noqa: E402
+from src.ops import functional as F  # noqa: E402
 from src.ops.distributed import (DistributedGraph, lightgcn_propagate_dist,  # noqa: E402
                                  make_work, _native_hop)
 
@@ -94,11 +99,19 @@ class HopTimer:
         return [s.elapsed_time(e) for s, e in self.pairs]
 
 
+def hop_bytes_alg(nnz: int, rows: int, src: int, d: int) -> int:
+    """SURVEY §8(d) compulsory bytes of one hop: CSR once (int64 row_ptr, int32 col, fp32 val),
+    every distinct source row once, every destination row written once. G100M d=64, one
+    GPU: 2.640e9 B."""
+    return 8 * nnz + 8 * (rows + 1) + 4 * d * src + 4 * d * rows
+
+
 def hop_bytes(nnz: int, rows: int, src: int, d: int, K: int, world: int) -> list:
-    """Algorithmic (compulsory) bytes of each hop launch: CSR once, every distinct source
-    row once, the hop output written once (not on the last hop), the layer-mean accumulator
-    written every hop and read from hop 2 on; rank-local self rows read on hop 1 when
-    sharded (with one GPU they are part of the gathered table already)."""
+    """Bytes of each hop launch as the kernel is used here, fused layer-mean epilogue
+    included: CSR once, every distinct source row once, the hop output written once (not
+    on the last hop), the layer-mean accumulator written every hop and read from hop 2 on;
+    rank-local self rows read on hop 1 when sharded (with one GPU they are part of the
+    gathered table already)."""
     out = []
     for k in range(1, K + 1):
         b = 8 * nnz + 8 * (rows + 1) + 4 * d * src
@@ -110,42 +123,99 @@ def hop_bytes(nnz: int, rows: int, src: int, d: int, K: int, world: int) -> list
     return out
 
 
-def load_traffic(workload_key: str):
-    """Per-launch HBM bytes from the committed PMC summary (profiles/pmc_<key>.json)."""
+def kernel_key(tiled_plan) -> str:
+    """Identity of the hop kernel a PMC summary was measured on: SHA-256 of the kernel
+    sources that build it and of the plan parameters the launch uses. A summary whose key
+    differs from the running build is never reported (traffic: null)."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = ROOT / "gnn-recommendations_amd" / "csrc"
+    files = ["common.h", "tiled.hip"] if tiled_plan is not None else ["common.h", "gather.h",
+                                                                      "spmm.hip"]
+    for f in files + ["../../include/gnnrec.h"]:
+        h.update((csrc / f).read_bytes())
+    if tiled_plan is not None:
+        h.update(json.dumps({k: tiled_plan[k] for k in sorted(tiled_plan)
+                             if isinstance(tiled_plan[k], (int, float, str))},
+                            sort_keys=True).encode())
+    return h.hexdigest()[:16]
+
+
+def load_traffic(workload_key: str, key: str):
+    """Per-launch HBM bytes from the committed PMC summary (profiles/pmc_<workload>.json) if
+    it was measured on this kernel build and plan (same kernel_key), else (None, reason)."""
     p = ROOT / "profiles" / f"pmc_{workload_key}.json"
     if not p.exists():
-        return None
+        return None, "no PMC summary for this workload"
     try:
-        return float(json.loads(p.read_text())["hbm_bytes_per_launch"])
-    except Exception:
+        d = json.loads(p.read_text())
+    except Exception as e:  # noqa: BLE001
+        return None, f"unreadable PMC summary: {e}"
+    if d.get("kernel_key") != key:
+        return None, f"PMC summary is of kernel_key {d.get('kernel_key')}, running {key}"
+    return float(d["hbm_bytes_per_launch"]), p.name
+
+
+def tiled_plan_info(g: CsrGraph, x: torch.Tensor):
+    """The plan parameters of the hop launch (None: the CSR kernel runs)."""
+    plan = F.tiled_plan_for(g, x)
+    if plan is None:
         return None
+    return {k: v for k, v in plan.items() if not isinstance(v, torch.Tensor)}
 
 
-def cpu_baseline(g: CsrGraph, x0: torch.Tensor, n_users: int, reps: int = 2) -> dict:
-    """Reference CPU path (COO torch.sparse.mm) on a bounded sample: one hop over the user
-    rows of A (half of the operand) with the full x table."""
+def cpu_baseline(g: CsrGraph, x0: torch.Tensor, K: int, n_users: int, gpu_hop1: np.ndarray,
+                 gpu_out: np.ndarray) -> dict:
+    """The reference's CPU path as SURVEY §8 d3 specifies it, on this host's cores, for the
+    WHOLE workload:
+      * graph build (graph_builder.py:16-174: scipy COO -> tocsr -> D^-1/2 A D^-1/2 -> torch
+        COO) over every deduplicated pair, compared bit for bit with the GPU's operand;
+      * propagation (lightgcn.py:76-95): x = cat(U, I); K x torch.sparse.mm on the
+        reference-layout uncoalesced int64 COO; torch.stack(layers).mean(0), no_grad.
+    One untimed warm-up hop over a 1 % row slice (thread pool / MKL start-up), then one timed
+    full propagation (a single rep: ~70 s of CPU work at 16 threads for G100M). Hop 1 and the
+    output are compared bit for bit with the GPU's (cpu_parity)."""
     import oracle.torch_ref as tr
     threads = host_threads()
     torch.set_num_threads(threads)
     rp = g.row_ptr.cpu().numpy()
-    A = tr.coo_operand(rp, g.col.cpu().numpy(), g.val.cpu().numpy(), g.shape[1],
-                       slice(0, n_users))
-    nnz = int(rp[n_users] - rp[0])
-    xc = x0.detach().cpu().contiguous()
-    torch.sparse.mm(A, xc)  # warm-up
-    ts = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        torch.sparse.mm(A, xc)
-        ts.append(time.perf_counter() - t0)
-    t = float(np.median(ts))
-    # the reference's graph build (scipy, graph_builder.py:16-174) on a 10M-pair sample
-    rng = np.random.default_rng(1)
-    su = rng.integers(0, n_users, 10_000_000)
-    si = rng.integers(0, g.shape[0] - n_users, 10_000_000)
+    col = g.col.cpu().numpy()
+    val = g.val.cpu().numpy()
+    N = g.shape[0]
+    n_items = N - n_users
+    # the deduplicated pairs are the user rows of A: (u, n_users + i)
+    nnz_u = int(rp[n_users])
+    pu = np.repeat(np.arange(n_users, dtype=np.int64), np.diff(rp[:n_users + 1]))
+    pi = col[:nnz_u].astype(np.int64) - n_users
     t0 = time.perf_counter()
-    tr.scipy_operand(su, si, n_users, g.shape[0] - n_users)
+    A_ref = tr.scipy_operand(pu, pi, n_users, n_items)
     t_build = time.perf_counter() - t0
+    del pu, pi
+    ri = A_ref._indices()
+    operand_same = bool(A_ref._nnz() == g.nnz
+                        and np.array_equal(ri[1].numpy(), col.astype(np.int64))
+                        and np.array_equal(np.diff(np.searchsorted(ri[0].numpy(), np.arange(N + 1))),
+                                           np.diff(rp))
+                        and np.array_equal(A_ref._values().numpy().view(np.uint32),
+                                           val.view(np.uint32)))
+    del ri
+    xc = x0.detach().cpu().contiguous()
+    with torch.no_grad():
+        warm = tr.coo_operand(rp, col, val, N, slice(0, max(1, N // 100)))
+        torch.sparse.mm(warm, xc)
+        del warm
+        t0 = time.perf_counter()
+        layers = [xc]
+        x = xc
+        for _ in range(K):
+            x = torch.sparse.mm(A_ref, x)
+            layers.append(x)
+        out = torch.stack(layers, dim=0).mean(dim=0)
+        t = time.perf_counter() - t0
+    hop1_same = bool(np.array_equal(layers[1].numpy().view(np.uint32), gpu_hop1.view(np.uint32)))
+    out_same = bool(np.array_equal(out.numpy().view(np.uint32), gpu_out.view(np.uint32)))
+    max_abs = float(np.abs(out.numpy() - gpu_out).max())
+    del layers, out, x, A_ref
     cpu_model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -154,17 +224,21 @@ def cpu_baseline(g: CsrGraph, x0: torch.Tensor, n_users: int, reps: int = 2) -> 
                 break
     except OSError:
         pass
-    return {"value": nnz / t, "unit": "edges/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model,
-            "graph_build": {"pairs": 10_000_000, "seconds": t_build,
-                            "what": "scipy COO -> tocsr -> D^-1/2 A D^-1/2 -> torch COO "
-                                    "(oracle/torch_ref.scipy_operand)"},
-            "sample": f"1 hop of torch.sparse.mm on the reference-layout uncoalesced COO "
-                      f"(graph_builder.py:163-172) over the {n_users} user rows of A "
-                      f"({nnz} nnz, half the operand) x full x0 [{g.shape[1]}, {x0.shape[1]}]; "
-                      f"1 warm-up + median of {reps}; torch {torch.__version__} "
+    return {"value": K * g.nnz / t, "unit": "edges/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model, "seconds": t,
+            "sample": f"the whole workload: LightGCN K={K} propagation (x0 [{N}, {xc.shape[1]}], "
+                      f"{K} x torch.sparse.mm on the reference-layout uncoalesced int64 COO of "
+                      f"all {g.nnz} nnz, graph_builder.py:163-172, then stack().mean(0), "
+                      f"lightgcn.py:76-95), no_grad, 1 untimed warm-up hop over a 1% row "
+                      f"slice then 1 timed rep; torch {torch.__version__} "
                       f"({torch.get_num_threads()} threads)",
-            "seconds_per_rep": t}
+            "graph_build": {"pairs": nnz_u, "seconds": t_build,
+                            "what": "scipy COO -> tocsr -> D^-1/2 A D^-1/2 -> torch COO over "
+                                    "every deduplicated pair (oracle/torch_ref.scipy_operand)",
+                            "bit_exact_vs_gpu_operand": operand_same},
+            "cpu_parity": hop1_same and out_same,
+            "parity_detail": {"hop1_bit_exact": hop1_same, "output_bit_exact": out_same,
+                              "output_max_abs_diff": max_abs}}
 
 
 def verify(dg, full: CsrGraph, x0, x0_pad, K, out, device, rank) -> dict:
@@ -242,11 +316,12 @@ def main(argv=None) -> int:
     x0_pad = dg.pad_table(x0)
     work = make_work(dg, d, device)
     # operand re-layout for the column-ordered hop (built once, outside the timed region)
-    from src.ops import functional as F
+    t1 = time.perf_counter()
     tiled = F.tiled_plan_for(dg.shard, x0_pad) is not None
+    plan_s = time.perf_counter() - t1
     torch.cuda.synchronize()
     log(f"rank {rank}: rows [{dg.row_begin},{dg.row_end}) nnz={dg.shard.nnz} src={src} "
-        f"uploaded in {time.perf_counter() - t0:.1f}s")
+        f"uploaded in {time.perf_counter() - t0:.1f}s (tiled plan {plan_s:.1f}s)")
     cpu_graph = full if (rank == 0 and world == 1 and not a.no_cpu_baseline) else None
     verify_graph = full if a.verify else None
     del full
@@ -306,12 +381,14 @@ def main(argv=None) -> int:
     ms_per_step = elapsed / a.steps * 1e3
 
     durs = timer.durations_ms()
+    alg_bytes = float(hop_bytes_alg(dg.shard.nnz, dg.n_local, src, d))
     per_hop = hop_bytes(dg.shard.nnz, dg.n_local, src, d, K, world)
     launch_bytes = float(np.mean(per_hop))
     # kernel time per hop (= per launch at N=1; the sum of its chunk launches when the hop is
     # split into overlap chunks)
     launch_ms = float(np.sum(durs)) / (a.steps * K)
-    achieved = launch_bytes / (launch_ms * 1e-3) / 1e9
+    achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
+    achieved_fused = launch_bytes / (launch_ms * 1e-3) / 1e9
 
     # cross-rank totals
     nnz_total = torch.tensor([float(dg.shard.nnz)], dtype=torch.float64, device=device)
@@ -330,12 +407,20 @@ def main(argv=None) -> int:
         del verify_graph
 
     workload_key = f"g100m_lightgcn_k{K}_d{d}_n{world}" + ("_tiled" if tiled else "")
-    traffic = load_traffic(workload_key) if world == 1 else None
+    kkey = kernel_key(tiled_plan_info(dg.shard, x0_pad))
+    traffic, traffic_src = load_traffic(workload_key, kkey) if world == 1 else (None, "N > 1")
 
     cpu = None
     if cpu_graph is not None:
-        log("timing the reference CPU SpMM (bounded sample) ...")
-        cpu = cpu_baseline(cpu_graph, x0, a.users)
+        # the GPU's hop 1 of the same operand and x0, for the CPU parity check
+        hop1 = torch.empty_like(x0_pad)
+        F.spmm_into(dg.shard, x0_pad, hop1)
+        gpu_hop1 = hop1.cpu().numpy()
+        gpu_out = out.cpu().numpy()
+        del hop1
+        log("timing the reference CPU path (scipy build + K-hop torch.sparse.mm) ...")
+        cpu = cpu_baseline(cpu_graph, x0, K, a.users, gpu_hop1, gpu_out)
+        del gpu_hop1, gpu_out
 
     if rank == 0:
         line = {
@@ -367,11 +452,17 @@ def main(argv=None) -> int:
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
+                "algorithmic_bytes_per_hop": alg_bytes,
+                "bytes_model": "SURVEY 8(d) B_hop = 8 nnz + 8 (rows+1) + 4 d |src| + 4 d rows",
+                "achieved_with_fused_epilogue": achieved_fused,
+                "frac_with_fused_epilogue": achieved_fused / HBM_PEAK_GBPS,
+                "kernel_key": kkey,
+                "traffic_source": traffic_src,
                 "kernel": ("tiled_hop_kernel (column-ordered panels, LDS accumulators; "
                            "one launch per hop)" if tiled else
                            f"spmm_vec_kernel<{d}> (one launch per hop)"),
                 "launch_ms": launch_ms,
-                "algorithmic_bytes_per_launch": launch_bytes,
+                "bytes_per_launch_with_fused_epilogue": launch_bytes,
                 # the same launch priced by its MEASURED memory-side traffic (PMC): how close
                 # the random row gather runs to the fabric/HBM rate
                 "traffic_gbps": (traffic / (launch_ms * 1e-3) / 1e9) if traffic else None,
@@ -379,6 +470,7 @@ def main(argv=None) -> int:
                 if traffic else None,
             },
             "cpu_baseline": cpu,
+            "operand_prep_s": {"tiled_plan_build": plan_s if tiled else None},
             "edges_per_s_per_interaction": value / 2.0,
             "hbm_gbps_algorithmic_step": K * launch_bytes * world / (ms_per_step * 1e-3) / 1e9,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,

@@ -1,3 +1,3 @@
-from .evaluator import Evaluator, compute_metrics_from_topk
+from .evaluator import Evaluator, compute_metrics_from_topk, embedding_statistics
 
-__all__ = ["Evaluator", "compute_metrics_from_topk"]
+__all__ = ["Evaluator", "compute_metrics_from_topk", "embedding_statistics"]

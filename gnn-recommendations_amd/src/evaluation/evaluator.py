@@ -50,6 +50,45 @@ def compute_metrics_from_topk(topk_items, user_ids: List[int], ground_truth: Dic
     return out
 
 
+def embedding_statistics(emb: torch.Tensor, exact_limit: int = 65536,
+                         chunk: int = 4096) -> Dict[str, float]:
+    """The over-smoothing statistics evaluate() adds (evaluator.py:116-121 ->
+    training/metrics.py:229-315), on the propagated table where it lives:
+    mcs = mean off-diagonal cosine similarity, mad = mean off-diagonal pairwise Euclidean
+    distance (||a||^2 + ||b||^2 - 2ab, clamped at 0), variance = mean per-dimension unbiased
+    variance. The reference materialises the [N, N] matrices (infeasible past ~5e4 nodes);
+    here mcs is the exact identity (||sum e_n||^2 - sum ||e_n||^2) / (N (N-1)) over
+    L2-normalised rows and mad runs over row chunks, so nothing N x N is held. Above
+    `exact_limit` nodes mad is taken over a fixed-seed sample of that many rows (flagged
+    'mad_sampled'). Values agree with the reference to fp32 reassociation."""
+    e = emb.detach().float()
+    n = e.shape[0]
+    out: Dict[str, float] = {}
+    if n < 2:
+        return {"mcs": float("nan"), "mad": float("nan"), "variance": float("nan")}
+    en = torch.nn.functional.normalize(e, p=2, dim=1).double()
+    s = en.sum(0)
+    out["mcs"] = float(((s @ s) - (en * en).sum()) / (n * (n - 1)))
+    sub = e
+    if n > exact_limit:
+        g = torch.Generator(device="cpu").manual_seed(0)
+        sub = e[torch.randperm(n, generator=g)[:exact_limit].to(e.device)]
+        out["mad_sampled"] = float(exact_limit)
+    m = sub.shape[0]
+    nsq = (sub ** 2).sum(1)
+    tot = torch.zeros((), dtype=torch.float64, device=e.device)
+    for r0 in range(0, m, chunk):
+        blk = sub[r0:r0 + chunk]
+        d2 = nsq[r0:r0 + chunk, None] + nsq[None, :] - 2 * (blk @ sub.T)
+        d = torch.sqrt(torch.clamp(d2, min=0))
+        idx = torch.arange(blk.shape[0], device=e.device)
+        d[idx, r0 + idx] = 0.0                       # the diagonal is excluded from the mean
+        tot += d.double().sum()
+    out["mad"] = float(tot / (m * (m - 1)))
+    out["variance"] = float(e.var(dim=0).mean())
+    return out
+
+
 class Evaluator:
     def __init__(self, k_values=(10, 20), device: Optional[torch.device] = None):
         self.k_values = list(k_values)
@@ -102,4 +141,6 @@ class Evaluator:
                 return {}
             seen_ptr, seen_col = dataset.seen_items(include_valid=mask_valid)
             topk = self.topk(user_emb, item_emb, users, max(self.k_values), seen_ptr, seen_col)
-            return compute_metrics_from_topk(topk, users, gt, dataset.n_items, self.k_values)
+            metrics = compute_metrics_from_topk(topk, users, gt, dataset.n_items, self.k_values)
+            metrics.update(embedding_statistics(torch.cat([user_emb, item_emb], dim=0)))
+            return metrics

@@ -64,11 +64,23 @@ class BaseRecommender(nn.Module):
         def ident(o):
             if o is None:
                 return None
-            rp = getattr(o, "row_ptr", None)
-            return (id(o), rp.data_ptr() if rp is not None else None,
-                    getattr(o, "nnz", None) if rp is not None else o.shape)
+            if getattr(o, "row_ptr", None) is not None:          # CsrGraph
+                t = (o.row_ptr, o.col, o.val)
+            elif isinstance(o, torch.Tensor) and o.layout == torch.sparse_coo:
+                t = (o._indices(), o._values())
+            elif isinstance(o, torch.Tensor) and o.layout == torch.sparse_csr:
+                t = (o.crow_indices(), o.col_indices(), o.values())
+            elif isinstance(o, torch.Tensor):
+                t = (o,)
+            else:
+                return (id(o),)
+            return (id(o), tuple(o.shape) if hasattr(o, "shape") else None,
+                    tuple((a.data_ptr(), a.numel(), a._version) for a in t))
         key = (param_key(list(self.parameters())), tuple(ident(o) for o in operands))
         if getattr(self, "_serving_key", None) != key:
             self._serving_cache = self.get_all_embeddings(*operands)
             self._serving_key = key
+            # the operands stay referenced while cached: their id() and storage cannot be
+            # recycled by a different graph that would then hit this entry
+            self._serving_operands = operands
         return self._serving_cache

@@ -126,6 +126,12 @@ class OrthogonalBundleGNN(BaseRecommender):
         return x_final[:self.n_users], x_final[self.n_users:]
 
     def _graph_conv_edge_index(self, x, edge_index):
+        """index_add_(dst, x[src]) (model.py:215-220): on a ROCm device the edge list becomes a
+        cached CSR of edge multiplicities and this is one native SpMM (same sum, fp32
+        reassociation only)."""
+        if x.is_cuda and x.dim() == 2 and x.stride(1) == 1:
+            from .parallel_transport import edge_index_operand
+            return ops.spmm(edge_index_operand(edge_index, x.size(0)), x)
         src, dst = edge_index
         out = torch.zeros_like(x)
         out.index_add_(0, dst, x[src])

@@ -20,8 +20,10 @@ def edge_index_operand(edge_index: torch.Tensor, num_nodes: int,
                        mask: torch.Tensor = None, tag=None) -> CsrGraph:
     """CsrGraph of B[dst, src] = multiplicity of (src -> dst), on edge_index's device (only
     the edges where `mask` holds, when given; `tag` names the subset in the cache key)."""
-    key = (edge_index.data_ptr(), edge_index.shape[1], num_nodes, edge_index.device, tag)
-    g = _EDGE_CACHE.get(key)
+    key = (id(edge_index), edge_index.data_ptr(), edge_index._version, edge_index.shape[1],
+           num_nodes, edge_index.device, tag)
+    hit = _EDGE_CACHE.get(key)
+    g = hit[0] if hit is not None else None
     if g is None:
         src, dst = edge_index[0].long(), edge_index[1].long()
         if mask is not None:
@@ -31,7 +33,8 @@ def edge_index_operand(edge_index: torch.Tensor, num_nodes: int,
         g = CsrGraph.from_torch_sparse(coo, symmetric=False)
         if len(_EDGE_CACHE) > 16:
             _EDGE_CACHE.clear()
-        _EDGE_CACHE[key] = g
+        # holding edge_index keeps its id() and storage from being recycled while cached
+        _EDGE_CACHE[key] = (g, edge_index)
     return g
 
 

@@ -30,8 +30,11 @@ _CACHE: dict = {}
 
 def _cache_key(adj: torch.Tensor):
     if adj.layout == torch.sparse_coo:
-        return (id(adj), adj._values().data_ptr(), adj._nnz(), tuple(adj.shape))
-    return (id(adj), adj.values().data_ptr(), adj._nnz(), tuple(adj.shape))
+        parts = (adj._indices(), adj._values())
+    else:
+        parts = (adj.crow_indices(), adj.col_indices(), adj.values())
+    return (id(adj), tuple(adj.shape), adj._nnz(),
+            tuple((t.data_ptr(), t._version) for t in parts))
 
 
 def as_operand(adj):
@@ -48,7 +51,11 @@ def as_operand(adj):
             if g is None:
                 _CACHE.clear()
                 g = CsrGraph.from_torch_sparse(adj)
-                _CACHE[key] = g
+                # the entry holds the source tensor: while cached, neither its id() nor its
+                # storage can be recycled by another operand that would then map to this graph
+                _CACHE[key] = (g, adj)
+            else:
+                g = g[0]
             return g
     return adj
 

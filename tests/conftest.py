@@ -59,3 +59,23 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.skip("no ROCm GPU visible")
     return torch.device("cuda", 0)
+
+
+def sha256(a) -> str:
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def long_rows_case():
+    """Config 2's ML-1M-shaped graph (max degree 5 857, 343 rows > 256) and the reference's
+    LightGCN K=3 d=64 on it (tests/golden/lightgcn_ml1m_K3_d64.npz): (f, users, items, nu, ni,
+    x0) with x0 re-drawn by the drop-in LightGCN from the golden's seed."""
+    import torch
+    from src.models import LightGCN
+    f = load_golden("lightgcn_ml1m_K3_d64")
+    nu, ni = int(f["n_users"]), int(f["n_items"])
+    torch.manual_seed(int(f["seed"]))
+    m = LightGCN(nu, ni, embedding_dim=64, n_layers=3, init_scale=0.1)
+    x0 = torch.cat([m.user_embedding.weight, m.item_embedding.weight]).detach()
+    assert sha256(x0.numpy()) == f["layers_sha256"][0], "seeded init drifted from the reference"
+    return f, f["users"].astype(np.int64), f["items"].astype(np.int64), nu, ni, x0

@@ -2,7 +2,7 @@
 
 Run ONLY in the build container, where the reference is importable:
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [--only long_rows,edge_paths]
 
 It imports timur1arkhipov/gnn-recommendations from /root/reference/gnn-recommendations
 (read-only; no bytecode is written) and runs the reference's own functions and modules on
@@ -11,8 +11,12 @@ tests/golden/. The reference itself never travels to the GPU box; these fixtures
 """
 from __future__ import annotations
 
+import argparse
+import hashlib
 import os
+import subprocess
 import sys
+import tempfile
 from pathlib import Path
 
 import numpy as np
@@ -64,10 +68,159 @@ def ref_graph(gb, u, i, nu, ni, self_loop=False):
     return norm, deg, t
 
 
+def sha256(a) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def ml1m_pairs():
+    """Config 2's graph (BASELINE configs[1]): the train pairs of the repo's ML-1M-shaped
+    synthetic dataset (RecommendationDataset.synthetic_movielens(6040, 3706, 1_000_209,
+    seed=1): Zipf item popularity -> rating >= 3, 5-core, temporal split). Made in a child
+    process because the repo's package is also named `src`."""
+    pkg = Path(__file__).resolve().parents[2] / "gnn-recommendations_amd"
+    with tempfile.TemporaryDirectory() as td:
+        out = Path(td) / "pairs.npz"
+        code = ("import sys, numpy as np; sys.path.insert(0, sys.argv[1]); "
+                "from src.data.dataset import RecommendationDataset as R; "
+                "ds = R.synthetic_movielens(6040, 3706, 1_000_209, seed=1, name='ml-1m'); "
+                "np.savez(sys.argv[2], u=ds.train_data.userId.to_numpy(), "
+                "i=ds.train_data.itemId.to_numpy(), nu=ds.n_users, ni=ds.n_items)")
+        subprocess.run([sys.executable, "-c", code, str(pkg), str(out)], check=True,
+                       env=dict(os.environ, PYTHONDONTWRITEBYTECODE="1"))
+        with np.load(out) as z:
+            return z["u"], z["i"], int(z["nu"]), int(z["ni"])
+
+
+def make_long_rows(gb, LightGCN):
+    """LightGCN K=3 d=64 on the ML-1M-shaped graph: rows up to 5 857 neighbours (343 rows
+    above the heavy-row threshold), so the reference's torch.sparse.mm chain order is pinned
+    on long rows, not only on the <= 28-nnz rows of g_small. Every layer is pinned by the
+    SHA-256 of its fp32 bytes (bit-exact or nothing); the final output and the heavy rows of
+    every hop are stored as values too."""
+    import torch
+    u, i, nu, ni = ml1m_pairs()
+    norm, deg, t_adj = ref_graph(gb, u, i, nu, ni)
+    N = nu + ni
+    rp = np.zeros(N + 1, np.int64)
+    np.add.at(rp, norm.row.astype(np.int64) + 1, 1)
+    rp = np.cumsum(rp)
+    col = norm.col.astype(np.int32)
+    val = norm.data.astype(np.float32)
+    torch.manual_seed(2024)
+    m = LightGCN(nu, ni, embedding_dim=64, n_layers=3, init_scale=0.1)
+    m.eval()
+    with torch.no_grad():
+        ue, ie = m(t_adj)
+        layers = [x.numpy() for x in m.get_layer_embeddings(t_adj)]
+    out = np.concatenate([ue.numpy(), ie.numpy()])
+    heavy = np.nonzero(np.diff(rp) > 256)[0].astype(np.int64)
+    np.savez_compressed(
+        OUT / "lightgcn_ml1m_K3_d64.npz", users=u.astype(np.int16), items=i.astype(np.int16),
+        n_users=nu, n_items=ni, seed=2024, nnz=int(rp[-1]), max_degree=int(np.diff(rp).max()),
+        operand_sha256=np.array([sha256(rp), sha256(col), sha256(val)]),
+        layers_sha256=np.array([sha256(x) for x in layers]), out_sha256=sha256(out),
+        user_out=ue.numpy(), item_out=ie.numpy(), heavy_rows=heavy,
+        layers_heavy=np.stack([x[heavy] for x in layers[1:]]))
+    print(f"long_rows: N={N} nnz={rp[-1]} max degree {np.diff(rp).max()}, {heavy.size} heavy rows")
+
+
+def make_edge_paths(gb, OBG, ESBC, PT):
+    """use_edge_index=True paths of OrthogonalBundleGNN (model.py:160-181, 215-220,
+    parallel_transport.py:5-52) with and without parallel transport, and the per-edge-type
+    connection EdgeSpecificBundleConnection (bundle_layer.py:106-149) through the 3-D
+    bmm branch of parallel_transport_along_edges (:37-43). The edge list is the g_small
+    interactions in both directions, shuffled, with 150 repeated edges (multiplicity 2)."""
+    import torch
+    nu, ni = 300, 500
+    u, i = interactions(0, nu, ni, 5000)
+    rng = np.random.default_rng(61)
+    src = np.concatenate([u, nu + i])
+    dst = np.concatenate([nu + i, u])
+    rep = rng.choice(src.size, 150, replace=False)
+    src = np.concatenate([src, src[rep]])
+    dst = np.concatenate([dst, dst[rep]])
+    order = rng.permutation(src.size)
+    src, dst = src[order], dst[order]
+    ei = torch.from_numpy(np.vstack([src, dst]).astype(np.int64))
+    for pt in (True, False):
+        torch.manual_seed(62 + int(pt))
+        m = OBG(nu, ni, embedding_dim=64, n_layers=3, block_size=8, residual_alpha=0.1,
+                dropout=0.0, init_scale=0.01, use_parallel_transport=pt, use_edge_index=True)
+        with torch.no_grad():
+            m.layer_weights.copy_(torch.tensor([0.3, -0.2, 0.5, 0.1]))
+            conn = list(m.connection_layers) if pt else []
+            for L in list(m.local_transform_layers) + conn:
+                for p in L.skew_params:
+                    p.mul_(20.0)
+        m.eval()
+        with torch.no_grad():
+            ue, ie = m(edge_index=ei)
+            layers = m.get_layer_embeddings(edge_index=ei)
+        arrs = dict(edge_index=ei.numpy(), n_users=nu, n_items=ni, seed=62 + int(pt),
+                    use_parallel_transport=int(pt),
+                    user_w=m.user_embedding.weight.detach().numpy(),
+                    item_w=m.item_embedding.weight.detach().numpy(), user_out=ue.numpy(),
+                    item_out=ie.numpy(), layers=np.stack([x.numpy() for x in layers]))
+        for li in range(3):
+            gsl = m.local_transform_layers[li]
+            arrs[f"gs_skew_{li}"] = np.stack([p.detach().numpy() for p in gsl.skew_params])
+            arrs[f"gs_perm_{li}"] = gsl.perm.numpy()
+            if pt:
+                bcl = m.connection_layers[li]
+                arrs[f"bc_skew_{li}"] = np.stack([p.detach().numpy() for p in bcl.skew_params])
+                arrs[f"bc_perm_{li}"] = bcl.shuffle_perm.numpy()
+        np.savez_compressed(OUT / f"ob_edge_index_pt{int(pt)}_d64.npz", **arrs)
+    torch.manual_seed(71)
+    esbc = ESBC(64, 8, n_edge_types=2)
+    with torch.no_grad():
+        for L in esbc.connection_layers:
+            for p in L.skew_params:
+                p.mul_(20.0)
+    et = torch.from_numpy((src >= nu).astype(np.int64))   # 0: user -> item, 1: item -> user
+    x = torch.randn(nu + ni, 64) * 0.1
+    with torch.no_grad():
+        W = esbc(ei, et)
+        y = PT(x, ei, W)
+        Wt = np.stack([L().numpy() for L in esbc.connection_layers])
+    np.savez_compressed(
+        OUT / "edge_specific_d64.npz", edge_index=ei.numpy(), edge_type=et.numpy(), x=x.numpy(),
+        y=y.numpy(), W_types=Wt, skew=np.stack([np.stack([p.detach().numpy() for p in L.skew_params])
+                                                for L in esbc.connection_layers]),
+        perm=np.stack([L.shuffle_perm.numpy() for L in esbc.connection_layers]))
+    print(f"edge_paths: E={src.size}")
+
+
+def make_emb_stats():
+    """The over-smoothing statistics Evaluator.evaluate adds (evaluator.py:116-121 ->
+    training/metrics.py:229-315) on a table with a zero row and two identical rows."""
+    import torch
+    from src.training.metrics import (embedding_variance, mean_average_distance,
+                                      mean_cosine_similarity)
+    torch.manual_seed(81)
+    e = torch.randn(700, 64) * 0.1 + 0.02
+    e[5] = 0.0
+    e[9] = e[3]
+    np.savez(OUT / "emb_stats.npz", emb=e.numpy(), mcs=mean_cosine_similarity(e),
+             mad=mean_average_distance(e), variance=embedding_variance(e))
+
+
 def main():
     import torch
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="", help="comma list: long_rows, edge_paths, emb_stats")
+    only = set(filter(None, ap.parse_args().only.split(",")))
     gb, LightGCN, NGCF, GAT, GSL, BCL, OBG = _import_reference()
     torch.set_num_threads(1)
+    if only:
+        from src.models.orthogonal_bundle.bundle_layer import EdgeSpecificBundleConnection
+        from src.models.orthogonal_bundle.parallel_transport import parallel_transport_along_edges
+        if "long_rows" in only:
+            make_long_rows(gb, LightGCN)
+        if "edge_paths" in only:
+            make_edge_paths(gb, OBG, EdgeSpecificBundleConnection, parallel_transport_along_edges)
+        if "emb_stats" in only:
+            make_emb_stats()
+        return
     meta = dict(torch=torch.__version__, numpy=np.__version__)
     import scipy
     meta["scipy"] = scipy.__version__
@@ -245,6 +398,12 @@ def main():
     seen_col = np.array([c for s in seen for c in s], dtype=np.int64)
     np.savez(OUT / "topk_d64.npz", U=U.numpy(), I=I.numpy(), seen_ptr=seen_ptr, seen_col=seen_col,
              scores=scores.numpy(), topk_idx=topk.indices.numpy(), topk_val=topk.values.numpy())
+
+    from src.models.orthogonal_bundle.bundle_layer import EdgeSpecificBundleConnection
+    from src.models.orthogonal_bundle.parallel_transport import parallel_transport_along_edges
+    make_long_rows(gb, LightGCN)
+    make_edge_paths(gb, OBG, EdgeSpecificBundleConnection, parallel_transport_along_edges)
+    make_emb_stats()
 
     with open(OUT / "VERSIONS.txt", "w") as f:
         for k, v in meta.items():

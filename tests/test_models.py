@@ -185,3 +185,79 @@ def test_predict_serving_cache_tracks_parameters():
         c = m.predict(users, items, adj)
         ue, ie = m.get_all_embeddings(adj)
     assert torch.equal(c, (ue[users] * ie[items]).sum(1)) and not torch.equal(a, c)
+
+
+def load_ob_edge(pt: int):
+    """OrthogonalBundleGNN(use_edge_index=True) seeded as in make_golden.make_edge_paths;
+    returns (model, golden, edge_index). The seeded construction must reproduce the
+    reference's parameters exactly (same RNG order)."""
+    f = load_golden(f"ob_edge_index_pt{pt}_d64")
+    torch.manual_seed(int(f["seed"]))
+    m = OrthogonalBundleGNN(300, 500, embedding_dim=64, n_layers=3, block_size=8,
+                            residual_alpha=0.1, dropout=0.0, init_scale=0.01,
+                            use_parallel_transport=bool(pt), use_edge_index=True)
+    with torch.no_grad():
+        m.layer_weights.copy_(torch.tensor([0.3, -0.2, 0.5, 0.1]))
+        conn = list(m.connection_layers) if pt else []
+        for L in list(m.local_transform_layers) + conn:
+            for p in L.skew_params:
+                p.mul_(20.0)
+    np.testing.assert_array_equal(m.user_embedding.weight.detach().numpy(), f["user_w"])
+    np.testing.assert_array_equal(m.item_embedding.weight.detach().numpy(), f["item_w"])
+    for li in range(3):
+        gs = m.local_transform_layers[li]
+        np.testing.assert_array_equal(np.stack([p.detach().numpy() for p in gs.skew_params]),
+                                      f[f"gs_skew_{li}"])
+        np.testing.assert_array_equal(gs.perm.numpy(), f[f"gs_perm_{li}"])
+        if pt:
+            bc = m.connection_layers[li]
+            np.testing.assert_array_equal(np.stack([p.detach().numpy() for p in bc.skew_params]),
+                                          f[f"bc_skew_{li}"])
+            np.testing.assert_array_equal(bc.shuffle_perm.numpy(), f[f"bc_perm_{li}"])
+    return m.eval(), f, torch.from_numpy(f["edge_index"])
+
+
+def load_edge_specific():
+    """EdgeSpecificBundleConnection seeded as make_golden.make_edge_paths (params checked)."""
+    from src.models.orthogonal_bundle import EdgeSpecificBundleConnection
+    f = load_golden("edge_specific_d64")
+    torch.manual_seed(71)
+    esbc = EdgeSpecificBundleConnection(64, 8, n_edge_types=2)
+    with torch.no_grad():
+        for L in esbc.connection_layers:
+            for p in L.skew_params:
+                p.mul_(20.0)
+    for t, L in enumerate(esbc.connection_layers):
+        np.testing.assert_array_equal(np.stack([p.detach().numpy() for p in L.skew_params]),
+                                      f["skew"][t])
+        np.testing.assert_array_equal(L.shuffle_perm.numpy(), f["perm"][t])
+    return esbc, f
+
+
+@pytest.mark.parametrize("pt", [0, 1])
+def test_ob_edge_index_cpu_matches_reference(pt):
+    """use_edge_index=True (model.py:160-181, 215-220): golden from the reference itself."""
+    m, f, ei = load_ob_edge(pt)
+    with torch.no_grad():
+        u, i = m(edge_index=ei)
+        layers = m.get_layer_embeddings(edge_index=ei)
+    np.testing.assert_allclose(u.numpy(), f["user_out"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(i.numpy(), f["item_out"], rtol=1e-6, atol=1e-6)
+    for k in range(4):
+        np.testing.assert_allclose(layers[k].numpy(), f["layers"][k], rtol=1e-6, atol=1e-6)
+
+
+def test_edge_specific_cpu_matches_reference():
+    """EdgeSpecificBundleConnection (bundle_layer.py:106-149) + the bmm transport
+    (parallel_transport.py:37-43): both forward() + the torch transport and transport()
+    against the reference's output."""
+    from src.models.orthogonal_bundle.parallel_transport import parallel_transport_along_edges
+    esbc, f = load_edge_specific()
+    ei, et = torch.from_numpy(f["edge_index"]), torch.from_numpy(f["edge_type"])
+    x = torch.from_numpy(f["x"])
+    with torch.no_grad():
+        np.testing.assert_allclose(esbc.type_matrices().numpy(), f["W_types"], rtol=0, atol=1e-7)
+        ref_path = parallel_transport_along_edges(x, ei, esbc(ei, et))
+        out = esbc.transport(x, ei, et)
+    np.testing.assert_allclose(ref_path.numpy(), f["y"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(out.numpy(), f["y"], rtol=1e-6, atol=1e-6)

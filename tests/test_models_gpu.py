@@ -115,20 +115,25 @@ def test_orthogonal_bundle_model_fused(cuda):
         np.testing.assert_allclose(layers[k].cpu().numpy(), f["layers"][k], rtol=0, atol=1e-5)
 
 
-def test_orthogonal_bundle_edge_index_path(cuda):
-    """use_edge_index=True: edge-list transport mapped onto the CSR kernel, vs the torch path."""
-    f = load_golden("ob_d64")
-    m = load_ob(f)
-    m.use_edge_index = True
-    rp, col, val, nu, ni = golden_csr("g_small")
-    rows = np.repeat(np.arange(rp.size - 1), np.diff(rp))
-    ei = torch.from_numpy(np.vstack([col.astype(np.int64), rows]))  # src -> dst
+@pytest.mark.parametrize("pt", [0, 1])
+def test_orthogonal_bundle_edge_index_path(cuda, pt):
+    """use_edge_index=True with and without parallel transport (model.py:160-181, 215-220)
+    against the reference's own output (tests/golden/ob_edge_index_pt*_d64.npz): the edge list
+    becomes a cached CSR of edge multiplicities, one native SpMM (+ MFMA transform) per layer."""
+    from test_models import load_ob_edge
+    from src.models.orthogonal_bundle.parallel_transport import _EDGE_CACHE
+    m, f, ei = load_ob_edge(pt)
+    m = m.to(cuda)
+    _EDGE_CACHE.clear()
+    ei = ei.to(cuda)
     with torch.no_grad():
-        ref_u, ref_i = m(edge_index=ei)
-        m = m.to(cuda).eval()
-        u, i = m(edge_index=ei.to(cuda))
-    np.testing.assert_allclose(u.cpu().numpy(), ref_u.numpy(), rtol=0, atol=2e-5)
-    np.testing.assert_allclose(i.cpu().numpy(), ref_i.numpy(), rtol=0, atol=2e-5)
+        u, i = m(edge_index=ei)
+        layers = m.get_layer_embeddings(edge_index=ei)
+    assert len(_EDGE_CACHE) == 1                       # the native edge operand was used
+    np.testing.assert_allclose(u.cpu().numpy(), f["user_out"], rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(i.cpu().numpy(), f["item_out"], rtol=2e-5, atol=2e-5)
+    for k in range(4):
+        np.testing.assert_allclose(layers[k].cpu().numpy(), f["layers"][k], rtol=2e-5, atol=2e-5)
 
 
 def test_gat_model_sparse(cuda):
@@ -203,16 +208,15 @@ def test_gat_shared_rows_equals_replicated_table(cuda, heavy):
 
 
 def test_edge_specific_transport_native(cuda):
-    """§8f4 on the GPU: per-type CSR + SpMM/MFMA transform, no [E, d, d] tensor."""
-    from test_models import _typed_edges
-    from src.models.orthogonal_bundle import EdgeSpecificBundleConnection
-    from src.models.orthogonal_bundle.parallel_transport import parallel_transport_along_edges
-    torch.manual_seed(4)
-    esbc = EdgeSpecificBundleConnection(64, 8)
-    ei, et, x = _typed_edges(1)
+    """§8f4 on the GPU against the reference's EdgeSpecificBundleConnection + bmm transport
+    (tests/golden/edge_specific_d64.npz): one CSR + SpMM/MFMA transform per edge type, no
+    [E, d, d] tensor."""
+    from test_models import load_edge_specific
+    esbc, f = load_edge_specific()
+    esbc = esbc.to(cuda)
     with torch.no_grad():
-        ref = parallel_transport_along_edges(x, ei, esbc(ei, et))
-        esbc = esbc.to(cuda)
-        out = esbc.transport(x.to(cuda), ei.to(cuda), et.to(cuda))
+        out = esbc.transport(torch.from_numpy(f["x"]).to(cuda),
+                             torch.from_numpy(f["edge_index"]).to(cuda),
+                             torch.from_numpy(f["edge_type"]).to(cuda))
     assert out.is_cuda
-    torch.testing.assert_close(out.cpu(), ref, rtol=0, atol=2e-6)
+    np.testing.assert_allclose(out.cpu().numpy(), f["y"], rtol=2e-5, atol=2e-5)

@@ -119,3 +119,19 @@ def test_scipy_operand_restatement_matches_golden():
     np.testing.assert_array_equal(idx[0][order], g["row"][ref])
     np.testing.assert_array_equal(idx[1][order], g["col"][ref])
     np.testing.assert_array_equal(val[order].view(np.uint32), g["val"][ref].view(np.uint32))
+
+
+def test_long_rows_oracle_bit_exact_vs_reference():
+    """The oracle's chain order (ascending-column fmaf from +0) equals torch.sparse.mm on rows
+    of up to 5 857 neighbours (config 2's graph), every layer, by SHA-256 of the fp32 bytes."""
+    from conftest import long_rows_case, sha256
+    f, u, i, nu, ni, x0 = long_rows_case()
+    rp, col, val = oracle.normalized_graph(u, i, nu, ni)
+    assert [sha256(rp), sha256(col.astype(np.int32)), sha256(val)] == list(f["operand_sha256"])
+    assert int(np.diff(rp).max()) == int(f["max_degree"]) == 5857
+    out, layers = oracle.lightgcn(rp, col, val, x0.numpy(), 3, return_layers=True)
+    for k in range(3):
+        assert sha256(layers[k]) == f["layers_sha256"][k + 1], f"hop {k + 1}"
+        np.testing.assert_array_equal(layers[k][f["heavy_rows"]], f["layers_heavy"][k])
+    assert sha256(out) == f["out_sha256"]
+    np.testing.assert_array_equal(out, np.concatenate([f["user_out"], f["item_out"]]))

@@ -65,3 +65,43 @@ def test_run_all_config1_cpu(tmp_path):
     res = json.loads(out.read_text())
     assert rc == 0 and res[0]["status"] == "success"
     assert 0.0 <= res[0]["test_metrics"]["recall@10"] <= 1.0
+
+
+def test_embedding_statistics_match_reference():
+    """mcs / mad / variance that Evaluator.evaluate adds (evaluator.py:116-121), against the
+    reference's own metric functions (tests/golden/emb_stats.npz); mad also through the
+    sampled path's chunking (exact_limit above N)."""
+    import torch
+    from conftest import load_golden
+    from src.evaluation import embedding_statistics
+    f = load_golden("emb_stats")
+    st = embedding_statistics(torch.from_numpy(f["emb"]), chunk=128)
+    assert abs(st["mcs"] - float(f["mcs"])) < 1e-6
+    assert abs(st["mad"] - float(f["mad"])) < 1e-5 * float(f["mad"])
+    assert abs(st["variance"] - float(f["variance"])) < 1e-6 * float(f["variance"])
+    assert "mad_sampled" not in st
+    st2 = embedding_statistics(torch.from_numpy(f["emb"]), exact_limit=300)
+    assert st2["mad_sampled"] == 300.0 and abs(st2["mcs"] - st["mcs"]) < 1e-12
+
+
+def test_bench_cpu_baseline_leg_checks_parity():
+    """bench.py's cpu_baseline leg on a small graph: the scipy build equals the
+    native operand bit for bit, and hop 1 / the output compare bit-exact against the oracle
+    standing in for the GPU's arrays; a perturbed GPU output is reported as a mismatch."""
+    import numpy as np
+    import torch
+    import bench
+    import oracle
+    from src.ops import CsrGraph
+    g = bench.build_graph(300, 500, 6000, 3, 2)
+    torch.manual_seed(0)
+    x0 = torch.randn(800, 64) * 0.1
+    rp, col, val = g.row_ptr.numpy(), g.col.numpy(), g.val.numpy()
+    out, layers = oracle.lightgcn(rp, col, val, x0.numpy(), 3, return_layers=True)
+    res = bench.cpu_baseline(g, x0, 3, 300, layers[0], out)
+    assert res["graph_build"]["bit_exact_vs_gpu_operand"] is True
+    assert res["cpu_parity"] is True and res["value"] > 0
+    bad = out.copy()
+    bad[7, 3] = np.nextafter(bad[7, 3], np.float32(1))
+    res = bench.cpu_baseline(g, x0, 3, 300, layers[0], bad)
+    assert res["cpu_parity"] is False and res["parity_detail"]["hop1_bit_exact"] is True

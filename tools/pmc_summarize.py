@@ -2,6 +2,11 @@
 traffic figure bench.py reports as roofline.traffic.
 
     python tools/pmc_summarize.py <fetch_csv> <write_csv> <out_json> [kernel_substring]
+                                  [bench_json_of_the_pmc_run]
+
+The bench JSON line of the profiled run carries roofline.kernel_key (SHA-256 of the hop
+kernel's sources and plan parameters); it is stored in the summary, and bench.py reports the
+summary's traffic only while its own kernel_key matches.
 
 Counters are collected in two separate passes (MI355X_MICROARCH.md § rocprofv3 PMC slots:
 FETCH_SIZE and WRITE_SIZE do not fit one TCC pass). Both are in KiB. gfx950 correction
@@ -28,12 +33,18 @@ def per_dispatch(path, counter, kernel):
 def main():
     fetch_csv, write_csv, out = sys.argv[1:4]
     kernel = sys.argv[4] if len(sys.argv) > 4 else "spmm_vec_kernel"
+    key = None
+    if len(sys.argv) > 5:
+        for line in open(sys.argv[5]):
+            if line.startswith("{"):
+                key = json.loads(line)["roofline"].get("kernel_key")
     fetch = per_dispatch(fetch_csv, "FETCH_SIZE", kernel)
     write = per_dispatch(write_csv, "WRITE_SIZE", kernel)
     rd = [2.0 * v * 1024 for v in fetch]
     wr = [v * 1024 for v in write]
     res = {
         "kernel": kernel,
+        "kernel_key": key,
         "launches": len(fetch),
         "fetch_size_kib_per_launch": fetch,
         "write_size_kib_per_launch": write,
