@@ -190,6 +190,7 @@ def cpu_baseline(g: CsrGraph, x0: torch.Tensor, K: int, n_users: int, gpu_hop1: 
     t0 = time.perf_counter()
     A_ref = tr.scipy_operand(pu, pi, n_users, n_items)
     t_build = time.perf_counter() - t0
+    log(f"cpu: reference scipy build {t_build:.1f}s; propagating ...")
     del pu, pi
     ri = A_ref._indices()
     operand_same = bool(A_ref._nnz() == g.nnz
