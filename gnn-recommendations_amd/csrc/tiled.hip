@@ -1,4 +1,4 @@
-// Column-ordered ("tiled") SpMM hop for d = 64 (gnnrec_spmm_tiled_f32).
+// Column-ordered ("tiled") SpMM hop for any d % 32 == 0 (gnnrec_spmm_tiled_f32).
 //
 // Same arithmetic as spmm_vec_kernel — replaces torch.sparse.mm(adj, x) of the reference
 // (baselines/lightgcn.py:88,178) with y[r] = fmaf chain over the row's neighbours in ascending
@@ -10,21 +10,28 @@
 // from one step to the next without reordering its chain). The workgroups of a blockIdx % 8
 // group (one XCD under round-robin placement — speed only, never correctness) meet at every
 // pass start (bounded counter wait), so they sweep the same panels together and a gathered
-// source row is reused from the XCD's L2 by the group's other rows: L2 hit rate 12 % -> 32 %.
+// source row is reused from the XCD's L2 by the group's other rows.
 //
-// Plan (host, gnnrec_tiled_plan_build): per (block, wave) a run of chunks of kChunk slots
-//   xoff u32 = byte offset of the source row, val f32,
-//   meta u16 = local row (10 bits) | barriers before the chunk (5 bits, slot 0) << 10
-//              | "continues the previous slot's row" << 15.
-// Inside a step a wave's rows are laid back to back, each a run in column order; a slot that
-// continues a run inside the same chunk takes the previous slot's register value instead of
-// the LDS accumulator (which that slot only writes at the chunk's end). Unused slots are
-// dummies: row R (a scratch row), val 0, xoff of the chunk's first slot.
+// Feature slices: a pass computes ONE 32-feature slice of its block's rows (a gather = one
+// 128-B line of a source row; the LDS row = 128 B), so R is twice what whole 64-feature rows
+// allow and an XCD group's pass covers twice the rows, touching each gathered line for more of
+// them (G100M: 14 passes x 1117 rows x 2 slices instead of 14 x 559 x 1). A d-wide hop is d/32
+// sweeps of the same plan; the work items are (slice, block) pairs, slice-major.
+//
+// The two 32-lane halves of a wave take two slot streams (lane = half * 32 + feature). A chunk
+// holds 16 slots per half. Every lane loads ITS slot's (offset, value, row) once per chunk
+// (lane l: slot (l / 32, l % 16)) and step t broadcasts slot t of each half to that half with
+// DPP row_newbcast:t (a 16-lane row reads its lane t), fused into the address add where the
+// compiler can; per-chunk header words (scalar loads) carry the step barriers and the chain
+// mask (slot t continues slot t-1's row in the same half: take the register value, not LDS).
+// Pipeline per wave: chunk c+2's slot loads, chunk c+1's gathers and chunk c's LDS
+// read-fmaf-write in flight together.
 #include <algorithm>
 #include <atomic>
 #include <mutex>
 #include <new>
 #include <thread>
+#include <utility>
 #include <vector>
 
 #include "common.h"
@@ -32,133 +39,225 @@
 namespace gnnrec {
 
 constexpr int kTiledWaves = GNNREC_TILED_WAVES;
-constexpr int kTiledChunk = GNNREC_TILED_CHUNK;
-constexpr int kTiledD = 64;
-constexpr int kTiledMaxBar = 31;
-static_assert(GNNREC_TILED_MAX_ROWS < 1023, "row field is 10 bits (row R = scratch)");
-static_assert((GNNREC_TILED_MAX_ROWS + 1) * kTiledD * 4 <= 160 * 1024, "LDS");
+constexpr int kTiledChunk = GNNREC_TILED_CHUNK;   // slots per chunk (both halves)
+constexpr int kHalf = kTiledChunk / 2;            // slots per half = steps per chunk
+constexpr int kTiledTail = GNNREC_TILED_TAIL;
+constexpr int kSlice = 32;                        // features per pass
+constexpr int kRowMask = 2047;
+constexpr int kGroup = 8;                         // steps whose reads precede their writes
+static_assert(kHalf == 16, "a half-chunk is one DPP row of 16 lanes");
+static_assert(kHalf == 2 * kGroup, "a half-chunk is applied as two groups");
+static_assert(GNNREC_TILED_MAX_ROWS < kRowMask, "row field is 11 bits (row R = scratch)");
+static_assert((GNNREC_TILED_MAX_ROWS + 1) * kSlice * 4 <= 160 * 1024, "LDS");
 
 // ---- device -----------------------------------------------------------------------------
-struct TiledChunk {
-  uint32_t o[kTiledChunk];
-  float v[kTiledChunk];
-  uint32_t m[kTiledChunk / 2];
-  float x[kTiledChunk];
+#ifdef GNNREC_TILED_TRACE
+// Diagnostic build only (tools/trace_tiled.py): wave 0 of each workgroup stamps wall_clock64
+// at every pass start and step barrier into g_tiled_trace[blockIdx][event].
+constexpr int kTraceEvents = 1024;
+__device__ unsigned long long* g_tiled_trace;
+#define GNNREC_TILED_STAMP(ev)                                                    \
+  do {                                                                            \
+    if (threadIdx.x == 0 && g_tiled_trace && (ev) < kTraceEvents)                 \
+      g_tiled_trace[(size_t)blockIdx.x * kTraceEvents + (ev)] = wall_clock64();   \
+    ++(ev);                                                                       \
+  } while (0)
+#else
+#define GNNREC_TILED_STAMP(ev) ((void)0)
+#endif
+
+struct TiledSlots {   // this lane's slot of the chunk: (half, lane % 16)
+  uint32_t o;         // byte offset of the source row
+  float v;
+  uint32_t r;         // byte offset of the destination row's accumulator in LDS
 };
 
-// Slot metadata by scalar loads (the chunk offset is wave-uniform), then the chunk's 16 row
-// gathers (64 lanes x 4 B each) by buffer loads with the row offset in soffset.
-__device__ __forceinline__ void tiled_fetch(const uint32_t* __restrict__ sx,
-                                            const float* __restrict__ sv,
-                                            const uint32_t* __restrict__ sm, int64_t c,
-                                            __amdgpu_buffer_rsrc_t xr, int lane, TiledChunk& k) {
-#pragma unroll
-  for (int t = 0; t < kTiledChunk; ++t) {
-    k.o[t] = sx[c + t];
-    k.v[t] = sv[c + t];
-  }
-#pragma unroll
-  for (int t = 0; t < kTiledChunk / 2; ++t) k.m[t] = sm[c / 2 + t];
-#pragma unroll
-  for (int t = 0; t < kTiledChunk; ++t)
-    k.x[t] = __builtin_bit_cast(float,
-                                __builtin_amdgcn_raw_buffer_load_b32(xr, lane * 4, k.o[t], 0));
+template <int T>
+__device__ __forceinline__ uint32_t bcast(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + T, 0xF, 0xF, true);
+}
+template <int T>
+__device__ __forceinline__ float bcastf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                               0x150 + T, 0xF, 0xF, true));
 }
 
-__device__ __forceinline__ void tiled_apply(float* acc, int lane, const TiledChunk& k,
-                                            int& cur) {
-  const int bar = (k.m[0] >> 10) & kTiledMaxBar;
-  for (int i = 0; i < bar; ++i) __syncthreads();   // step boundaries before this chunk
-  cur += bar;
-  int rr[kTiledChunk];
-#pragma unroll
-  for (int t = 0; t < kTiledChunk; ++t)
-    rr[t] = ((t & 1) ? (k.m[t / 2] >> 16) : k.m[t / 2]) & 1023;
-  float av[kTiledChunk];
-#pragma unroll
-  for (int t = 0; t < kTiledChunk; ++t) av[t] = acc[rr[t] * kTiledD + lane];
-#pragma unroll
-  for (int t = 0; t < kTiledChunk; ++t) {
-    float base = av[t];
-    if (t > 0) {
-      const bool chain = ((t & 1) ? (k.m[t / 2] >> 31) : (k.m[t / 2] >> 15)) & 1;
-      base = chain ? av[t - 1] : base;
-    }
-    av[t] = __builtin_fmaf(k.v[t], k.x[t], base);
-  }
-#pragma unroll
-  for (int t = 0; t < kTiledChunk; ++t) acc[rr[t] * kTiledD + lane] = av[t];
+__device__ __forceinline__ void tiled_slots(const uint32_t* __restrict__ sx,
+                                            const float* __restrict__ sv,
+                                            const uint16_t* __restrict__ sm, int64_t c,
+                                            int my_slot, TiledSlots& m) {
+  const int64_t i = c * kTiledChunk + my_slot;
+  m.o = sx[i];
+  m.v = sv[i];
+  m.r = (uint32_t)(sm[i] & kRowMask) * (kSlice * 4);
+}
+
+template <int... T>
+__device__ __forceinline__ void tiled_gather(std::integer_sequence<int, T...>,
+                                             __amdgpu_buffer_rsrc_t xr, uint32_t f4,
+                                             const TiledSlots& m, float (&x)[kHalf]) {
+  ((x[T] = __builtin_bit_cast(
+        float, __builtin_amdgcn_raw_buffer_load_b32(xr, bcast<T>(m.o) + f4, 0, 0))),
+   ...);
+}
+
+// lane-wise select on a wave-uniform 64-bit lane mask held in SGPRs (no compare per lane)
+__device__ __forceinline__ float select_lanes(float if0, float if1, uint64_t mask) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if0), "v"(if1), "s"(mask));
+  return r;
+}
+
+template <int T>
+__device__ __forceinline__ uint64_t chain_lanes(uint32_t cm) {
+  // slot T of half 0 (lanes 0-31): bit T; of half 1 (lanes 32-63): bit 16 + T
+  const uint32_t lo = 0u - ((cm >> T) & 1u), hi = 0u - ((cm >> (16 + T)) & 1u);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Steps G .. G+7 of a chunk: 8 accumulator reads, 8 chained fmaf, 8 writes. A chunk is
+// applied as two such groups, so a row may appear in both groups of a piece: the second
+// group's reads follow the first group's writes in the wave's LDS order (and a slot at step 8
+// chaining on step 7 selects the value step 7 just wrote).
+template <int G, int... T>
+__device__ __forceinline__ void tiled_apply8(std::integer_sequence<int, T...>, char* base,
+                                             uint32_t f4, const TiledSlots& m,
+                                             const float (&x)[kHalf], uint32_t cm,
+                                             float& prev) {
+  uint32_t a[sizeof...(T)];
+  ((a[T] = bcast<G + T>(m.r) + f4), ...);
+  float av[sizeof...(T)];
+  ((av[T] = *reinterpret_cast<float*>(base + a[T])), ...);
+  // slot t continuing slot t-1's row (same half) chains on its register value
+  ((av[T] = __builtin_fmaf(bcastf<G + T>(m.v), x[G + T],
+                           G + T > 0 ? select_lanes(av[T], T > 0 ? av[T > 0 ? T - 1 : 0] : prev,
+                                                    chain_lanes<G + T>(cm))
+                                     : av[T])),
+   ...);
+  ((*reinterpret_cast<float*>(base + a[T]) = av[T]), ...);
+  prev = av[sizeof...(T) - 1];
+}
+
+__device__ __forceinline__ void tiled_apply(float* acc, uint32_t f4, const TiledSlots& m,
+                                            const float (&x)[kHalf], uint32_t cm) {
+  constexpr auto k8 = std::make_integer_sequence<int, kGroup>{};
+  char* base = reinterpret_cast<char*>(acc);
+  float prev = 0.f;
+  tiled_apply8<0>(k8, base, f4, m, x, cm, prev);
+  tiled_apply8<kGroup>(k8, base, f4, m, x, cm, prev);
 }
 
 __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     const uint32_t* __restrict__ sx, const float* __restrict__ sv,
-    const uint32_t* __restrict__ sm, const int64_t* __restrict__ wptr,
-    const int32_t* __restrict__ nsteps, int n_blocks, int R, const float* __restrict__ x,
-    uint32_t x_bytes, float* __restrict__ y, int64_t ldy, int64_t n_rows, int epi,
-    const float* __restrict__ self, int64_t ld_self, float* __restrict__ accg, int64_t ld_acc,
-    float acc_div, unsigned* __restrict__ sync) {
-  extern __shared__ float acc[];  // [(R+1)][64]: row R is the dummies' scratch row
+    const uint16_t* __restrict__ sm, const uint32_t* __restrict__ hdr,
+    const int64_t* __restrict__ wptr, const int32_t* __restrict__ nsteps, int n_blocks,
+    int nb_pad, int n_items, int R, const float* __restrict__ x, uint32_t x_bytes,
+    float* __restrict__ y, int64_t ldy, int64_t n_rows, int epi, const float* __restrict__ self,
+    int64_t ld_self, float* __restrict__ accg, int64_t ld_acc, float acc_div,
+    unsigned* __restrict__ sync, unsigned meet_ticks) {
+  extern __shared__ float acc[];  // [(R+1)][32]: row R is the padding slots' scratch row
+  constexpr auto kSeq = std::make_integer_sequence<int, kHalf>{};
   const int lane = threadIdx.x & 63;
+  const int half = lane >> 5;
+  const int f = lane & 31;
+  const uint32_t f4 = (uint32_t)f * 4;
+  const int my_slot = half * kHalf + (lane & 15);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const __amdgpu_buffer_rsrc_t xr =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0, (int)x_bytes, 0x00020000);
   unsigned* ctr = sync + (blockIdx.x % 8) * 32;   // the group's counter, own 128-B line
   const long long G = gridDim.x / 8 + ((blockIdx.x % 8) < (gridDim.x % 8) ? 1 : 0);
   long long pass = 0;
-  for (int blk = blockIdx.x; blk < n_blocks; blk += gridDim.x, ++pass) {
-    if (threadIdx.x == 0 && pass > 0) {
-      // pass start: report the finished pass, wait (<= 200 us) for the group's others
+#ifdef GNNREC_TILED_TRACE
+  int ev = 0;
+#endif
+  for (int item = blockIdx.x; item < n_items; item += gridDim.x, ++pass) {
+    if (threadIdx.x == 0 && pass > 0 && meet_ticks > 0) {
+      // pass start: report the finished pass, wait (bounded) for the group's others
       __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned long long t0 = wall_clock64();
       while ((long long)__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
                  G * pass &&
-             wall_clock64() - t0 < 20000)
+             wall_clock64() - t0 < meet_ticks)
         __builtin_amdgcn_s_sleep(2);
     }
-    for (int i = threadIdx.x; i < (R + 1) * kTiledD; i += kTiledWaves * 64) acc[i] = 0.f;
+    const int slice = item / nb_pad, blk = item - slice * nb_pad;
+    if (blk >= n_blocks) continue;   // padding item (uniform over the workgroup)
+    for (int i = threadIdx.x; i < (R + 1) * kSlice; i += kTiledWaves * 64) acc[i] = 0.f;
     __syncthreads();
+    GNNREC_TILED_STAMP(ev);
+    const uint32_t soff = (uint32_t)slice * kSlice * 4;
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(x) + (size_t)slice * kSlice, 0, (int)(x_bytes - soff), 0x00020000);
     const int64_t s = (int64_t)blk * kTiledWaves + w;
     const int64_t b = wptr[s], e = wptr[s + 1];
     int cur = 0;
     if (b < e) {
-      // two chunk register sets: the next chunk's gathers fly while this one's chain runs
-      TiledChunk A, B;
+      // slot loads two chunks ahead, gathers one chunk ahead of the LDS chain
+      TiledSlots M0, M1, M2;
+      float X0[kHalf], X1[kHalf];
       int64_t c = b;
-      tiled_fetch(sx, sv, sm, c, xr, lane, A);
+      tiled_slots(sx, sv, sm, c, my_slot, M0);
+      tiled_slots(sx, sv, sm, c + 1, my_slot, M1);
+      tiled_gather(kSeq, xr, f4, M0, X0);
+#define GNNREC_TILED_STAGE(MLOAD, MG, XG, MA, XA)                       \
+  {                                                                     \
+    tiled_slots(sx, sv, sm, c + 2, my_slot, MLOAD);                     \
+    tiled_gather(kSeq, xr, f4, MG, XG);                                 \
+    const int bar = __builtin_amdgcn_readfirstlane((int)hdr[2 * c]);    \
+    for (int i = 0; i < bar; ++i) {                                     \
+      __syncthreads();                                                  \
+      GNNREC_TILED_STAMP(ev);                                           \
+    }                                                                   \
+    cur += bar;                                                         \
+    const uint32_t cm = __builtin_amdgcn_readfirstlane((int)hdr[2 * c + 1]); \
+    tiled_apply(acc, f4, MA, XA, cm);                                   \
+    if (++c >= e) break;                                                \
+  }
       for (;;) {
-        tiled_fetch(sx, sv, sm, c + kTiledChunk, xr, lane, B);
-        tiled_apply(acc, lane, A, cur);
-        c += kTiledChunk;
-        if (c >= e) break;
-        tiled_fetch(sx, sv, sm, c + kTiledChunk, xr, lane, A);
-        tiled_apply(acc, lane, B, cur);
-        c += kTiledChunk;
-        if (c >= e) break;
+        GNNREC_TILED_STAGE(M2, M1, X1, M0, X0)
+        GNNREC_TILED_STAGE(M0, M2, X0, M1, X1)
+        GNNREC_TILED_STAGE(M1, M0, X1, M2, X0)
+        GNNREC_TILED_STAGE(M2, M1, X0, M0, X1)
+        GNNREC_TILED_STAGE(M0, M2, X1, M1, X0)
+        GNNREC_TILED_STAGE(M1, M0, X0, M2, X1)
       }
+#undef GNNREC_TILED_STAGE
     }
     const int ns = nsteps[blk];
-    for (int i = cur; i < ns; ++i) __syncthreads();  // this wave's remaining steps + the last
+    for (int i = cur; i < ns; ++i) {  // this wave's remaining steps + the last
+      __syncthreads();
+      GNNREC_TILED_STAMP(ev);
+    }
     const int64_t r0 = (int64_t)blk * R;
-    for (int i = w; i < R; i += kTiledWaves) {
+    const int64_t cf = (int64_t)slice * kSlice + f;
+    for (int i = 2 * w + half; i < R; i += 2 * kTiledWaves) {
       const int64_t r = r0 + i;
       if (r >= n_rows) break;
-      const float a = acc[i * kTiledD + lane];
-      if (!(epi & GNNREC_EPI_NO_Y)) y[r * ldy + lane] = a;
+      const float a = acc[i * kSlice + f];
+      if (!(epi & GNNREC_EPI_NO_Y)) y[r * ldy + cf] = a;
       if (epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) {
-        float bsum = (epi & GNNREC_EPI_ACC_INIT) ? self[r * ld_self + lane] : accg[r * ld_acc + lane];
+        float bsum = (epi & GNNREC_EPI_ACC_INIT) ? self[r * ld_self + cf] : accg[r * ld_acc + cf];
         bsum = bsum + a;
         if (epi & GNNREC_EPI_ACC_DIV) bsum = bsum / acc_div;
-        accg[r * ld_acc + lane] = bsum;
+        accg[r * ld_acc + cf] = bsum;
       }
     }
     __syncthreads();
   }
   // finished: never hold the group back again
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u << 24, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0 && meet_ticks > 0)
+    __hip_atomic_fetch_add(ctr, 1u << 24, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+#ifdef GNNREC_TILED_TRACE
+extern "C" int gnnrec_debug_tiled_trace(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_tiled_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 // ---- host plan builder --------------------------------------------------------------------
 namespace {
+
+constexpr int kVirt = 2 * kTiledWaves;   // slot streams per block: (wave, half)
 
 struct Run {
   int32_t p, row;   // panel, local row
@@ -170,6 +269,7 @@ struct BlockPlan {
   std::vector<uint32_t> xoff[kTiledWaves];
   std::vector<float> val[kTiledWaves];
   std::vector<uint16_t> meta[kTiledWaves];
+  std::vector<uint32_t> hdr[kTiledWaves];
   int32_t nsteps = 0;
 };
 
@@ -178,21 +278,62 @@ struct TiledPlan {
   std::vector<BlockPlan> blocks;
 };
 
-void push_slot(BlockPlan& bp, int w, uint32_t xo, float v, uint16_t m) {
-  bp.xoff[w].push_back(xo);
-  bp.val[w].push_back(v);
-  bp.meta[w].push_back(m);
-}
-
 struct Slot {
-  const Run* run;   // nullptr: dummy
+  const Run* run;   // nullptr: padding
   int32_t t;        // edge of the run
 };
 
+// One stream's slots of a step cut into groups of kGroup (two groups = its half of a chunk):
+// slots in ascending column sub-panel, rows in order inside one (a row's edges keep their
+// column order); a row appears in a group only as ONE run of consecutive slots (the kernel
+// reads a group's accumulators before it writes any) — a slot that would repeat a row
+// non-adjacently is deferred, with the rest of that row, to a later group (per-row order
+// kept). Padded to a multiple of kHalf.
+void half_chunks(const std::vector<const Run*>& runs, const int32_t* col, int sub_panel,
+                 std::vector<Slot>& seq) {
+  std::vector<Slot> pending, deferred;
+  std::vector<int> in_chunk, blocked;
+  seq.clear();
+  for (const Run* e : runs)
+    for (int t = 0; t < e->n; ++t) pending.push_back({e, t});
+  if (sub_panel > 0)
+    std::stable_sort(pending.begin(), pending.end(), [&](const Slot& a, const Slot& c) {
+      const int32_t ka = col[a.run->k + a.t] / sub_panel, kc = col[c.run->k + c.t] / sub_panel;
+      return ka != kc ? ka < kc : a.run->row < c.run->row;
+    });
+  while (!pending.empty()) {
+    deferred.clear();
+    in_chunk.clear();
+    blocked.clear();
+    int n = 0, last = -1;
+    const size_t start = seq.size();
+    for (size_t q = 0; q < pending.size(); ++q) {
+      const Slot& sl = pending[q];
+      if (n == kGroup) {   // group full: the rest keeps its order for the next ones
+        deferred.insert(deferred.end(), pending.begin() + q, pending.end());
+        break;
+      }
+      const int r = sl.run->row;
+      const bool is_blocked = std::find(blocked.begin(), blocked.end(), r) != blocked.end();
+      const bool seen = std::find(in_chunk.begin(), in_chunk.end(), r) != in_chunk.end();
+      if (is_blocked || (seen && r != last)) {
+        if (seen && r != last && !is_blocked) blocked.push_back(r);
+        deferred.push_back(sl);
+        continue;
+      }
+      seq.push_back(sl);
+      if (!seen) in_chunk.push_back(r);
+      last = r;
+      ++n;
+    }
+    while (seq.size() - start < (size_t)kGroup) seq.push_back({nullptr, 0});
+    pending.swap(deferred);
+  }
+  while (seq.size() % kHalf) seq.push_back({nullptr, 0});
+}
+
 void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_t n_rows,
                  int R, int panel, int sub_panel, int64_t row_bytes, int64_t b, BlockPlan& out) {
-  std::vector<Slot> slots, seq, pending, deferred;
-  std::vector<int> in_chunk, blocked;
   const int64_t r0 = b * R, r1 = std::min<int64_t>(n_rows, r0 + R);
   std::vector<Run> runs;
   for (int64_t r = r0; r < r1; ++r) {
@@ -208,94 +349,64 @@ void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_
   }
   std::stable_sort(runs.begin(), runs.end(), [](const Run& a, const Run& c) { return a.p < c.p; });
   int32_t cur[kTiledWaves] = {};    // step of each wave's last emitted chunk
-  int64_t load[kTiledWaves];
-  std::vector<const Run*> wl[kTiledWaves];
+  int64_t load[kVirt];
+  std::vector<const Run*> wl[kVirt];
   std::vector<const Run*> g;
+  std::vector<Slot> hs[2];
   int32_t step = 0;
   size_t i = 0;
   while (i < runs.size()) {
     size_t j = i;
     while (j < runs.size() && runs[j].p == runs[i].p) ++j;
-    // LPT: longest run first onto the least loaded wave
+    // LPT over the (wave, half) streams: longest run first onto the least loaded
     g.clear();
     for (size_t q = i; q < j; ++q) g.push_back(&runs[q]);
     std::stable_sort(g.begin(), g.end(), [](const Run* a, const Run* c) { return a->n > c->n; });
-    for (int w = 0; w < kTiledWaves; ++w) {
-      load[w] = 0;
-      wl[w].clear();
+    for (int v = 0; v < kVirt; ++v) {
+      load[v] = 0;
+      wl[v].clear();
     }
     for (const Run* e : g) {
-      int w = 0;
-      for (int q = 1; q < kTiledWaves; ++q)
-        if (load[q] < load[w]) w = q;
-      load[w] += e->n;
-      wl[w].push_back(e);
+      int v = 0;
+      for (int q = 1; q < kVirt; ++q)
+        if (load[q] < load[v]) v = q;
+      load[v] += e->n;
+      wl[v].push_back(e);
     }
     for (int w = 0; w < kTiledWaves; ++w) {
-      if (wl[w].empty()) continue;
-      // the wave's slots in ascending column sub-panel, rows in order inside one (a row's
-      // edges keep their column order): the group's waves sweep the panel together
-      slots.clear();
-      for (const Run* e : wl[w])
-        for (int t = 0; t < e->n; ++t) slots.push_back({e, t});
-      if (sub_panel > 0)
-        std::stable_sort(slots.begin(), slots.end(), [&](const Slot& a, const Slot& c) {
-          const int32_t ka = col[a.run->k + a.t] / sub_panel, kc = col[c.run->k + c.t] / sub_panel;
-          return ka != kc ? ka < kc : a.run->row < c.run->row;
-        });
-      // chunks: a row appears in a chunk only as one run of consecutive slots (the kernel reads
-      // every accumulator at the chunk start); a slot that would repeat a row non-adjacently is
-      // deferred to a later chunk with the rest of that row (per-row order kept)
-      seq.clear();
-      pending.swap(slots);
-      while (!pending.empty()) {
-        deferred.clear();
-        in_chunk.clear();
-        blocked.clear();
-        int n = 0, last = -1;
-        const size_t start = seq.size();
-        for (size_t q = 0; q < pending.size(); ++q) {
-          const Slot& sl = pending[q];
-          if (n == kTiledChunk) {   // chunk full: the rest keeps its order for the next ones
-            deferred.insert(deferred.end(), pending.begin() + q, pending.end());
+      if (wl[2 * w].empty() && wl[2 * w + 1].empty()) continue;
+      for (int h = 0; h < 2; ++h) half_chunks(wl[2 * w + h], col, sub_panel, hs[h]);
+      const size_t n = std::max(hs[0].size(), hs[1].size());
+      for (int h = 0; h < 2; ++h) hs[h].resize(n, Slot{nullptr, 0});
+      uint32_t bar = (uint32_t)(step - cur[w]);
+      for (size_t c = 0; c < n; c += kHalf) {
+        // padding slots gather a line the chunk fetches anyway (its first real slot's)
+        uint32_t x0 = 0;
+        for (int q = 0; q < kTiledChunk; ++q) {
+          const Slot& sl = hs[q / kHalf][c + q % kHalf];
+          if (sl.run) {
+            x0 = (uint32_t)(col[sl.run->k + sl.t] * row_bytes);
             break;
           }
-          const int r = sl.run->row;
-          const bool is_blocked = std::find(blocked.begin(), blocked.end(), r) != blocked.end();
-          const bool seen = std::find(in_chunk.begin(), in_chunk.end(), r) != in_chunk.end();
-          if (is_blocked || (seen && r != last)) {
-            if (seen && r != last && !is_blocked) blocked.push_back(r);
-            deferred.push_back(sl);
-            continue;
+        }
+        uint32_t cmask = 0;
+        for (int h = 0; h < 2; ++h)
+          for (int t = 0; t < kHalf; ++t) {
+            const Slot& sl = hs[h][c + t];
+            if (!sl.run) {
+              out.xoff[w].push_back(x0);
+              out.val[w].push_back(0.f);
+              out.meta[w].push_back((uint16_t)R);
+              continue;
+            }
+            const int64_t k = sl.run->k + sl.t;
+            if (t > 0 && hs[h][c + t - 1].run == sl.run) cmask |= 1u << (16 * h + t);
+            out.xoff[w].push_back((uint32_t)(col[k] * row_bytes));
+            out.val[w].push_back(val[k]);
+            out.meta[w].push_back((uint16_t)sl.run->row);
           }
-          seq.push_back(sl);
-          if (!seen) in_chunk.push_back(r);
-          last = r;
-          ++n;
-        }
-        while (seq.size() - start < (size_t)kTiledChunk) seq.push_back({nullptr, 0});
-        pending.swap(deferred);
-      }
-      int32_t bar = step - cur[w];
-      for (size_t c = 0; c < seq.size(); c += kTiledChunk) {
-        while (bar > kTiledMaxBar) {   // more barriers than the field holds: an empty chunk
-          for (int s = 0; s < kTiledChunk; ++s)
-            push_slot(out, w, 0u, 0.f, (uint16_t)(R | (s == 0 ? kTiledMaxBar << 10 : 0)));
-          bar -= kTiledMaxBar;
-        }
-        const uint32_t x0 = (uint32_t)(col[seq[c].run->k + seq[c].t] * row_bytes);
-        for (int s = 0; s < kTiledChunk; ++s) {
-          const Slot& sl = seq[c + s];
-          const int bits = s == 0 ? bar << 10 : 0;
-          if (!sl.run) {            // dummy: scratch row, value 0, an already-fetched row
-            push_slot(out, w, x0, 0.f, (uint16_t)(R | bits));
-            continue;
-          }
-          const int64_t k = sl.run->k + sl.t;
-          const int chain = (s > 0 && seq[c + s - 1].run == sl.run) ? 1 : 0;
-          push_slot(out, w, (uint32_t)(col[k] * row_bytes), val[k],
-                    (uint16_t)(sl.run->row | bits | (chain << 15)));
-        }
+        out.hdr[w].push_back(bar);
+        out.hdr[w].push_back(cmask);
         bar = 0;
       }
       cur[w] = step;
@@ -314,12 +425,12 @@ using namespace gnnrec;
 extern "C" int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* col,
                                        const float* val, int64_t n_rows, int32_t rows_per_block,
                                        int32_t panel, int32_t sub_panel, int64_t row_bytes,
-                                       int32_t n_threads, void** plan, int64_t* n_slots,
+                                       int32_t n_threads, void** plan, int64_t* n_chunks,
                                        int64_t* n_blocks) {
-  GNNREC_REQUIRE(row_ptr && plan && n_slots && n_blocks && n_rows >= 0, "tiled_plan: bad args");
+  GNNREC_REQUIRE(row_ptr && plan && n_chunks && n_blocks && n_rows >= 0, "tiled_plan: bad args");
   GNNREC_REQUIRE(rows_per_block >= 1 && rows_per_block <= GNNREC_TILED_MAX_ROWS,
                  "tiled_plan: rows_per_block must be in [1, %d]", GNNREC_TILED_MAX_ROWS);
-  GNNREC_REQUIRE(panel >= 1 && sub_panel >= 0 && row_bytes > 0,
+  GNNREC_REQUIRE(panel >= 1 && sub_panel >= 0 && row_bytes > 0 && row_bytes % 4 == 0,
                  "tiled_plan: bad panel / sub_panel / row_bytes");
   const int64_t nnz = n_rows > 0 ? row_ptr[n_rows] - row_ptr[0] : 0;
   GNNREC_REQUIRE(nnz == 0 || (col && val), "tiled_plan: null col/val");
@@ -352,41 +463,43 @@ extern "C" int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* co
   }
   int64_t tot = 0;
   for (const auto& bp : pl->blocks)
-    for (int w = 0; w < kTiledWaves; ++w) tot += (int64_t)bp.xoff[w].size();
-  *n_slots = tot;
+    for (int w = 0; w < kTiledWaves; ++w) tot += (int64_t)bp.hdr[w].size() / 2;
+  *n_chunks = tot;
   *n_blocks = pl->n_blocks;
   *plan = pl;
   return GNNREC_OK;
 }
 
 extern "C" int gnnrec_tiled_plan_emit(void* plan, uint32_t* xoff, float* val, uint16_t* meta,
-                                      int64_t* wave_ptr, int32_t* n_steps) {
-  GNNREC_REQUIRE(plan && xoff && val && meta && wave_ptr && n_steps, "tiled_emit: null pointer");
+                                      uint32_t* hdr, int64_t* wave_ptr, int32_t* n_steps) {
+  GNNREC_REQUIRE(plan && xoff && val && meta && hdr && wave_ptr && n_steps,
+                 "tiled_emit: null pointer");
   auto* pl = static_cast<TiledPlan*>(plan);
   const int64_t nb = pl->n_blocks;
   wave_ptr[0] = 0;
   for (int64_t b = 0; b < nb; ++b)
     for (int w = 0; w < kTiledWaves; ++w)
       wave_ptr[b * kTiledWaves + w + 1] =
-          wave_ptr[b * kTiledWaves + w] + (int64_t)pl->blocks[b].xoff[w].size();
+          wave_ptr[b * kTiledWaves + w] + (int64_t)pl->blocks[b].hdr[w].size() / 2;
   for (int64_t b = 0; b < nb; ++b) {
     const BlockPlan& bp = pl->blocks[b];
     n_steps[b] = bp.nsteps;
     for (int w = 0; w < kTiledWaves; ++w) {
-      const int64_t o = wave_ptr[b * kTiledWaves + w];
-      std::copy(bp.xoff[w].begin(), bp.xoff[w].end(), xoff + o);
-      std::copy(bp.val[w].begin(), bp.val[w].end(), val + o);
-      std::copy(bp.meta[w].begin(), bp.meta[w].end(), meta + o);
+      const int64_t c = wave_ptr[b * kTiledWaves + w];
+      std::copy(bp.xoff[w].begin(), bp.xoff[w].end(), xoff + c * kTiledChunk);
+      std::copy(bp.val[w].begin(), bp.val[w].end(), val + c * kTiledChunk);
+      std::copy(bp.meta[w].begin(), bp.meta[w].end(), meta + c * kTiledChunk);
+      std::copy(bp.hdr[w].begin(), bp.hdr[w].end(), hdr + 2 * c);
     }
   }
-  // tail chunk for the last prefetch: harmless slots (row 0 of x, scratch row)
+  // tail chunks for the last prefetches: harmless slots (row 0 of x, scratch row)
   const int64_t end = wave_ptr[nb * kTiledWaves];
-  const uint16_t scratch = (uint16_t)(nb > 0 ? 1023 : 0);
-  for (int s = 0; s < kTiledChunk; ++s) {
-    xoff[end + s] = 0;
-    val[end + s] = 0.f;
-    meta[end + s] = scratch;
+  for (int64_t s = end * kTiledChunk; s < (end + kTiledTail) * kTiledChunk; ++s) {
+    xoff[s] = 0;
+    val[s] = 0.f;
+    meta[s] = (uint16_t)kRowMask;
   }
+  for (int64_t s = 2 * end; s < 2 * (end + kTiledTail); ++s) hdr[s] = 0;
   return GNNREC_OK;
 }
 
@@ -395,46 +508,70 @@ extern "C" int gnnrec_tiled_plan_free(void* plan) {
   return GNNREC_OK;
 }
 
+namespace {
+// The kernel may take all 160 KB of LDS: the attribute is set once per device, and a failure
+// is reported (not ignored) so the caller can fall back to the row-parallel hop.
+int tiled_lds_attribute(int dev) {
+  static std::mutex mu;
+  static std::vector<int> done;   // 0 unset, 1 ok, -1 failed
+  std::lock_guard<std::mutex> lock(mu);
+  if ((int)done.size() <= dev) done.resize(dev + 1, 0);
+  if (done[dev] == 0) {
+    const hipError_t e = hipFuncSetAttribute((const void*)tiled_hop_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             160 * 1024);
+    done[dev] = e == hipSuccess ? 1 : -1;
+    if (e != hipSuccess) (void)hipGetLastError();
+  }
+  return done[dev];
+}
+}  // namespace
+
 extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* xoff, const float* val, const uint16_t* meta,
-                                     const int64_t* wave_ptr, const int32_t* n_steps,
-                                     int64_t n_blocks, int32_t rows_per_block, const float* x,
-                                     int64_t x_rows, int64_t ldx, float* y, int64_t ldy,
-                                     int64_t n_rows, int32_t d, int32_t epi, const float* self,
-                                     int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
-                                     uint32_t* sync, gnnrec_stream_t stream) {
-  GNNREC_REQUIRE(d == kTiledD, "spmm_tiled: d must be 64 (got %d)", (int)d);
+                                     const uint32_t* hdr, const int64_t* wave_ptr,
+                                     const int32_t* n_steps, int64_t n_blocks,
+                                     int32_t rows_per_block, const float* x, int64_t x_rows,
+                                     int64_t ldx, float* y, int64_t ldy, int64_t n_rows, int32_t d,
+                                     int32_t epi, const float* self, int64_t ld_self, float* acc,
+                                     int64_t ld_acc, float acc_div, uint32_t* sync,
+                                     int32_t meet_us, gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(d > 0 && d % kSlice == 0, "spmm_tiled: d must be a multiple of 32 (got %d)",
+                 (int)d);
   GNNREC_REQUIRE(rows_per_block >= 1 && rows_per_block <= GNNREC_TILED_MAX_ROWS,
                  "spmm_tiled: bad rows_per_block");
   GNNREC_REQUIRE(n_rows >= 0 && n_blocks == (n_rows + rows_per_block - 1) / rows_per_block,
                  "spmm_tiled: n_blocks does not match n_rows / rows_per_block");
   GNNREC_REQUIRE(ldx >= d && x_rows >= 0 && x_rows * ldx * 4 < ((int64_t)1 << 32),
-                 "spmm_tiled: the x table must be under 4 GB with ldx >= 64");
+                 "spmm_tiled: the x table must be under 4 GB with ldx >= d");
   GNNREC_REQUIRE((epi & GNNREC_EPI_NO_Y) || (y && ldy >= d), "spmm_tiled: null y or ldy < d");
   GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_INIT) || (self && ld_self >= d),
                  "spmm_tiled: ACC_INIT needs self");
   GNNREC_REQUIRE(!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) || (acc && ld_acc >= d),
                  "spmm_tiled: ACC needs acc");
+  GNNREC_REQUIRE(meet_us >= 0 && meet_us <= 100000, "spmm_tiled: meet_us must be in [0, 1e5]");
   if (n_rows == 0) return GNNREC_OK;
-  GNNREC_REQUIRE(xoff && val && meta && wave_ptr && n_steps && x && sync,
+  GNNREC_REQUIRE(xoff && val && meta && hdr && wave_ptr && n_steps && x && sync,
                  "spmm_tiled: null pointer");
-  GNNREC_REQUIRE(n_blocks < INT32_MAX, "spmm_tiled: too many blocks");
   hipStream_t s = as_hip(stream);
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 256;
-  const size_t lds = (size_t)(rows_per_block + 1) * kTiledD * sizeof(float);
-  static std::once_flag lds_attr;   // per-process: the kernel may take all 160 KB of LDS
-  std::call_once(lds_attr, [] {
-    (void)hipFuncSetAttribute((const void*)tiled_hop_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  });
+  const size_t lds = (size_t)(rows_per_block + 1) * kSlice * sizeof(float);
+  if (lds > 64 * 1024 && tiled_lds_attribute(dev) < 0) {
+    set_error("spmm_tiled: the device refused %zu bytes of dynamic LDS", lds);
+    return GNNREC_EHIP;
+  }
+  const int64_t grid = std::min<int64_t>(cus, n_blocks);
+  const int64_t nb_pad = ceil_div(n_blocks, grid) * grid;   // every slice starts a pass
+  const int64_t n_items = (int64_t)(d / kSlice) * nb_pad;
+  GNNREC_REQUIRE(n_items < INT32_MAX, "spmm_tiled: too many blocks");
   if (hipMemsetAsync(sync, 0, GNNREC_TILED_SYNC_WORDS * sizeof(uint32_t), s) != hipSuccess)
     return check_launch("spmm_tiled (sync reset)");
-  const int grid = (int)std::min<int64_t>(cus, n_blocks);
-  hipLaunchKernelGGL(tiled_hop_kernel, dim3(grid), dim3(kTiledWaves * 64), lds, s, xoff, val,
-                     reinterpret_cast<const uint32_t*>(meta), wave_ptr, n_steps, (int)n_blocks,
-                     (int)rows_per_block, x, (uint32_t)(x_rows * ldx * 4), y, ldy, n_rows, epi,
-                     self, ld_self, acc, ld_acc, acc_div, sync);
+  hipLaunchKernelGGL(tiled_hop_kernel, dim3((unsigned)grid), dim3(kTiledWaves * 64), lds, s,
+                     xoff, val, meta, hdr, wave_ptr, n_steps, (int)n_blocks, (int)nb_pad,
+                     (int)n_items, (int)rows_per_block, x, (uint32_t)(x_rows * ldx * 4), y, ldy,
+                     n_rows, epi, self, ld_self, acc, ld_acc, acc_div, sync,
+                     (unsigned)meet_us * 100u /* wall_clock64 runs at 100 MHz */);
   return check_launch("spmm_tiled");
 }

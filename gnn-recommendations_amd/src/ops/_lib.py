@@ -17,13 +17,19 @@ import torch  # noqa: F401  (load order: torch's HIP runtime first)
 
 _PKG_ROOT = Path(__file__).resolve().parents[2]
 LIB_PATH = Path(os.environ.get("GNNREC_LIB", _PKG_ROOT / "lib" / "libgnnrec.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # gnnrec.h epilogue flags
 EPI_ACC_INIT = 1
 EPI_ACC_ADD = 2
 EPI_ACC_DIV = 4
 EPI_NO_Y = 8
+# column-ordered hop plan layout (include/gnnrec.h GNNREC_TILED_*)
+TILED_WAVES = 16
+TILED_CHUNK = 32
+TILED_TAIL = 2
+TILED_MAX_ROWS = 1279
+TILED_SYNC_WORDS = 256
 
 _p = C.c_void_p
 _i64 = C.c_int64
@@ -44,10 +50,10 @@ _SIGNATURES = {
                                    _p, _i64, _p, _i64, _f32, _p, _i64, _i64, _p],
     "gnnrec_mark_active_rows": [_p, _p, _i64, _p, _i64, _p, _p],
     "gnnrec_tiled_plan_build": [_p, _p, _p, _i64, _i32, _i32, _i32, _i64, _i32, _p, _p, _p],
-    "gnnrec_tiled_plan_emit": [_p, _p, _p, _p, _p, _p],
+    "gnnrec_tiled_plan_emit": [_p, _p, _p, _p, _p, _p, _p],
     "gnnrec_tiled_plan_free": [_p],
-    "gnnrec_spmm_tiled_f32": [_p, _p, _p, _p, _p, _i64, _i32, _p, _i64, _i64, _p, _i64, _i64,
-                              _i32, _i32, _p, _i64, _p, _i64, _f32, _p, _p],
+    "gnnrec_spmm_tiled_f32": [_p, _p, _p, _p, _p, _p, _i64, _i32, _p, _i64, _i64, _p, _i64,
+                              _i64, _i32, _i32, _p, _i64, _p, _i64, _f32, _p, _i32, _p],
     "gnnrec_row_nonzero_f32": [_p, _i64, _i64, _i32, _p, _p],
     "gnnrec_lightgcn_split_f32": [_p, _p, _p, _i64, _p, _i32, _i32, _p, _p, _p, _p, _i64, _p,
                                   _i64, _i64, _p],

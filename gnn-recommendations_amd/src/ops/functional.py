@@ -47,17 +47,20 @@ def _csr_args(adj: CsrGraph):
 SPMM_HEAVY_THRESHOLD = 256
 
 
-# Column-ordered hop (gnnrec_spmm_tiled_f32): the same bits, used for d = 64
-# when the operand fills at least one pass of the persistent grid (256 CUs x 600 rows) and has
-# no row longer than TILED_MAX_DEGREE (a long row's panel run stays on one wave and would hold
-# its step). G100M hop: 6.99 -> 5.23 ms. Masked / row-subset hops keep the CSR kernel.
-# Rows per block are evened out so every pass of the persistent grid is full (G100M: 14
-# passes of 559 rows instead of 13 of 600 plus a 6-block tail pass).
+# Column-ordered hop (gnnrec_spmm_tiled_f32): the same bits, used for any d
+# that is a multiple of 32 when the operand fills at least one pass of the persistent grid and
+# has no row longer than TILED_MAX_DEGREE (a long row's panel run stays on one slot stream and
+# would hold its step). Masked / row-subset hops keep the CSR kernel. Rows per block are
+# evened out so every pass of the persistent grid is full (G100M: 14 passes of 1117 rows —
+# 7 per 32-feature slice at d = 64 — not 6 of 1279 plus a tail pass).
 TILED_HOP = True
 TILED_MIN_ROWS = 256 * 600
 TILED_MAX_DEGREE = 4096
-TILED_MAX_ROWS = 600                 # GNNREC_TILED_MAX_ROWS
+TILED_MAX_ROWS = _lib.TILED_MAX_ROWS
 TILED_BALANCE_PASSES = True
+# bound of the pass-start meeting of an XCD group's workgroups (µs; 0 = no meeting: use when
+# other kernels share the device, e.g. a concurrent exchange)
+TILED_MEET_US = 200
 
 
 def _tiled_rows_per_block(n_rows: int, device) -> int:
@@ -70,7 +73,7 @@ def _tiled_rows_per_block(n_rows: int, device) -> int:
 
 def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None):
     """The column-ordered plan spmm_into would use for (adj, x), or None (CSR kernel)."""
-    if (not TILED_HOP or x_mask is not None or y_active is not None or x.shape[1] != 64
+    if (not TILED_HOP or x_mask is not None or y_active is not None or x.shape[1] % 32
             or adj.n_rows < TILED_MIN_ROWS or adj.nnz == 0
             or x.shape[0] * x.stride(0) * 4 >= 1 << 32
             or adj.max_degree() > TILED_MAX_DEGREE):
@@ -128,18 +131,20 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
 
 def spmm_tiled_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], plan: dict, *,
                     epi: int = 0, self_rows: Optional[torch.Tensor] = None,
-                    acc: Optional[torch.Tensor] = None, acc_div: float = 1.0) -> None:
+                    acc: Optional[torch.Tensor] = None, acc_div: float = 1.0,
+                    meet_us: Optional[int] = None) -> None:
     """spmm_into through the column-ordered kernel with an explicit plan (adj.tiled_plan(ldx)
     for this x's row stride); same results, bit for bit. The plan's sync words make
     concurrent launches of one plan on different streams unsafe."""
     _require_device(adj, x, y, self_rows, acc)
     d = x.shape[1]
     check(_lib.lib().gnnrec_spmm_tiled_f32(
-        ptr(plan["xoff"]), ptr(plan["val"]), ptr(plan["meta"]), ptr(plan["wave_ptr"]),
-        ptr(plan["n_steps"]), plan["n_blocks"], plan["rows_per_block"], ptr(x), x.shape[0],
-        x.stride(0), ptr(y), y.stride(0) if y is not None else d, adj.n_rows, d, epi,
-        ptr(self_rows), self_rows.stride(0) if self_rows is not None else d, ptr(acc),
+        ptr(plan["xoff"]), ptr(plan["val"]), ptr(plan["meta"]), ptr(plan["hdr"]),
+        ptr(plan["wave_ptr"]), ptr(plan["n_steps"]), plan["n_blocks"], plan["rows_per_block"],
+        ptr(x), x.shape[0], x.stride(0), ptr(y), y.stride(0) if y is not None else d, adj.n_rows,
+        d, epi, ptr(self_rows), self_rows.stride(0) if self_rows is not None else d, ptr(acc),
         acc.stride(0) if acc is not None else d, float(acc_div), ptr(plan["sync"]),
+        int(TILED_MEET_US if meet_us is None else meet_us),
         _lib.stream_of(adj.device)), "gnnrec_spmm_tiled_f32")
 
 

@@ -354,14 +354,16 @@ class CsrGraph:
             self._plans["max_degree"] = int(deg.max()) if deg.numel() else 0
         return self._plans["max_degree"]
 
-    def tiled_plan(self, ldx: int, rows_per_block: int = 600, panel: int = 131072,
+    def tiled_plan(self, ldx: int, rows_per_block: int = 1117, panel: int = 49152,
                    sub_panel: int = 4096) -> dict:
         """Column-ordered re-layout of this operand for gnnrec_spmm_tiled_f32 (DESIGN.md
-        §3.1c), for x tables with row stride `ldx` (cached per stride): built once on the host
-        from the CSR (gnnrec_tiled_plan_build/emit), uploaded to this graph's device.
-        Defaults from the G100M sweep (profiles/r01/exp_tiled/): 600 rows per block fill the
-        LDS, 128K-column panels (steps), each wave's slots in ascending 4K-column sub-panels
-        inside a step (0: no sub-panel order)."""
+        §3.1c), for x tables with row stride `ldx` (cached per stride; the same plan serves
+        every d <= ldx that is a multiple of 32): built once on the host from the CSR
+        (gnnrec_tiled_plan_build/emit), uploaded to this graph's device. Defaults from the
+        G100M sweep (profiles/r02/tiled_sweep.jsonl): 1117 rows per block fill the LDS with
+        32-feature accumulators in 14 full passes, 48K-column panels (steps: a workgroup
+        barrier each, which keeps its waves on nearby columns), each stream's slots in
+        ascending 4K-column sub-panels inside a step (0: no sub-panel order)."""
         key = ("tiled", int(ldx), int(rows_per_block), int(panel), int(sub_panel))
         if key not in self._plans:
             import ctypes as C
@@ -369,23 +371,25 @@ class CsrGraph:
             rp = np.ascontiguousarray(_np(self.row_ptr), dtype=np.int64)
             col = np.ascontiguousarray(_np(self.col), dtype=np.int32)
             val = np.ascontiguousarray(_np(self.val), dtype=np.float32)
-            h, n_slots, n_blocks = C.c_void_p(), C.c_int64(), C.c_int64()
+            h, n_chunks, n_blocks = C.c_void_p(), C.c_int64(), C.c_int64()
             _lib.check(L.gnnrec_tiled_plan_build(rp.ctypes.data, col.ctypes.data, val.ctypes.data,
                                                  self.n_rows, int(rows_per_block), int(panel),
                                                  int(sub_panel), 4 * int(ldx), 0, C.byref(h),
-                                                 C.byref(n_slots),
+                                                 C.byref(n_chunks),
                                                  C.byref(n_blocks)), "gnnrec_tiled_plan_build")
             nb = n_blocks.value
-            total = n_slots.value + 16                     # + GNNREC_TILED_CHUNK tail slots
-            xoff = np.empty(total, np.uint32)
-            v = np.empty(total, np.float32)
-            meta = np.empty(total, np.uint16)
-            wave_ptr = np.empty(nb * 16 + 1, np.int64)     # GNNREC_TILED_WAVES per block
+            chunks = n_chunks.value + _lib.TILED_TAIL          # + tail chunks (prefetch)
+            xoff = np.empty(chunks * _lib.TILED_CHUNK, np.uint32)
+            v = np.empty(chunks * _lib.TILED_CHUNK, np.float32)
+            meta = np.empty(chunks * _lib.TILED_CHUNK, np.uint16)
+            hdr = np.empty(chunks * 2, np.uint32)
+            wave_ptr = np.empty(nb * _lib.TILED_WAVES + 1, np.int64)
             n_steps = np.empty(max(nb, 1), np.int32)
             try:
                 _lib.check(L.gnnrec_tiled_plan_emit(h, xoff.ctypes.data, v.ctypes.data,
-                                                    meta.ctypes.data, wave_ptr.ctypes.data,
-                                                    n_steps.ctypes.data), "gnnrec_tiled_plan_emit")
+                                                    meta.ctypes.data, hdr.ctypes.data,
+                                                    wave_ptr.ctypes.data, n_steps.ctypes.data),
+                           "gnnrec_tiled_plan_emit")
             finally:
                 L.gnnrec_tiled_plan_free(h)
             dev = self.device
@@ -393,11 +397,13 @@ class CsrGraph:
                 xoff=torch.from_numpy(xoff.view(np.int32)).to(dev),
                 val=torch.from_numpy(v).to(dev),
                 meta=torch.from_numpy(meta.view(np.int16)).to(dev),
+                hdr=torch.from_numpy(hdr.view(np.int32)).to(dev),
                 wave_ptr=torch.from_numpy(wave_ptr).to(dev),
                 n_steps=torch.from_numpy(n_steps).to(dev),
                 n_blocks=nb, rows_per_block=int(rows_per_block), panel=int(panel),
-                n_slots=n_slots.value,
-                sync=torch.zeros(256, dtype=torch.int32, device=dev))  # GNNREC_TILED_SYNC_WORDS
+                sub_panel=int(sub_panel), n_chunks=n_chunks.value,
+                n_slots=n_chunks.value * _lib.TILED_CHUNK,
+                sync=torch.zeros(_lib.TILED_SYNC_WORDS, dtype=torch.int32, device=dev))
         return self._plans[key]
 
     def heavy_plan(self, threshold: int, seg_len: int):

@@ -43,6 +43,30 @@ def test_g100m_lightgcn_every_layer_bit_exact(cuda, g100m):
     np.testing.assert_array_equal(out_t.cpu().numpy().view(np.uint32), ref.view(np.uint32))
 
 
+@pytest.mark.parametrize("d", [128, 32])
+def test_g100m_tiled_hop_other_widths_bit_exact(cuda, g100m, d):
+    """BASELINE config 4's width (d = 128: four 32-feature sweeps of the same plan) and d = 32
+    (one sweep) through the column-ordered kernel at full G100M size: every hop output and the
+    fused layer mean equal the oracle bit for bit."""
+    g = g100m
+    rp, col, val = g.row_ptr.numpy(), g.col.numpy(), g.val.numpy()
+    x0 = (np.random.default_rng(d).standard_normal((g.shape[0], d)) * 0.1).astype(np.float32)
+    gd, xd = g.to(cuda), torch.from_numpy(x0).to(cuda)
+    assert F.tiled_plan_for(gd, xd) is not None
+    out, _ = F.lightgcn_forward(gd, xd, 3)
+    hop1 = torch.empty_like(xd)
+    F.spmm_into(gd, xd, hop1)
+    x = oracle.spmm(rp, col, val, x0)
+    np.testing.assert_array_equal(hop1.cpu().numpy().view(np.uint32), x.view(np.uint32))
+    del hop1
+    acc = x0 + x
+    for _ in range(2):
+        x = oracle.spmm(rp, col, val, x)
+        acc = acc + x
+    ref = acc / np.float32(4.0)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
 def test_g100m_device_builder_bit_identical(cuda, g100m):
     rng = np.random.default_rng(0)
     u = rng.integers(0, 1_000_000, 100_000_000, dtype=np.int64)

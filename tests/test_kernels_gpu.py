@@ -374,15 +374,22 @@ def test_lightgcn_forward_rows_equal_full(cuda, K, d):
 
 
 # ---- column-ordered ("tiled") hop: gnnrec_spmm_tiled_f32 ------------------------------------
-@pytest.mark.parametrize("R,panel", [(600, 32768), (37, 64), (1, 1), (600, 1 << 30)])
-def test_spmm_tiled_bit_exact(cuda, R, panel):
+@pytest.mark.parametrize("R,panel,d", [(600, 32768, 64), (37, 64, 64), (1, 1, 64),
+                                       (600, 1 << 30, 64), (1117, 4096, 64), (1279, 32768, 32),
+                                       (300, 2048, 128), (1277, 131072, 96)])
+def test_spmm_tiled_bit_exact(cuda, R, panel, d):
+    """Every 32-feature slice of every row equals the oracle's ordered fmaf chain, for plans
+    from one row per block to the LDS maximum and d = 32..128 (d/32 sweeps of one plan)."""
     g, (rp, col, val) = random_graph(3000, 2500, 60000, R + panel, cuda, heavy_user=2400)
-    x = torch.randn(g.shape[0], 64, generator=torch.Generator().manual_seed(R)) * 0.1
+    x = torch.randn(g.shape[0], d, generator=torch.Generator().manual_seed(R)) * 0.1
     ref = bits(oracle.spmm(rp, col, val, x.numpy()))
     xd = x.to(cuda)
-    plan = g.tiled_plan(64, rows_per_block=R, panel=panel)
-    y = torch.full((g.shape[0], 64), float("nan"), device=cuda)
+    plan = g.tiled_plan(d, rows_per_block=R, panel=panel)
+    y = torch.full((g.shape[0], d), float("nan"), device=cuda)
     F.spmm_tiled_into(g, xd, y, plan)
+    np.testing.assert_array_equal(bits(y.cpu().numpy()), ref)
+    y.fill_(float("nan"))
+    F.spmm_tiled_into(g, xd, y, plan, meet_us=0)        # no pass-start meeting: same bits
     np.testing.assert_array_equal(bits(y.cpu().numpy()), ref)
     F.spmm_tiled_into(g, xd, y, plan)                   # sync words reset per launch
     np.testing.assert_array_equal(bits(y.cpu().numpy()), ref)
@@ -412,10 +419,14 @@ def test_spmm_tiled_epilogues_strides_and_empty_rows(cuda):
 
 def test_spmm_tiled_rejects_bad_arguments(cuda):
     g, _ = random_graph(300, 200, 2000, 1, cuda)
-    plan = g.tiled_plan(32)
-    x = torch.zeros(g.shape[0], 32, device=cuda)
-    with pytest.raises(ValueError, match="d must be 64"):
+    plan = g.tiled_plan(48)
+    x = torch.zeros(g.shape[0], 48, device=cuda)
+    with pytest.raises(ValueError, match="multiple of 32"):
         F.spmm_tiled_into(g, x, torch.empty_like(x), plan)
+    assert F.tiled_plan_for(g, x) is None                # d = 48 stays on the CSR kernel
+    with pytest.raises(ValueError, match="meet_us"):
+        F.spmm_tiled_into(g, x[:, :32], torch.empty(g.shape[0], 32, device=cuda), plan,
+                          meet_us=-1)
 
 
 def test_lightgcn_through_tiled_hop_is_bit_exact(cuda, monkeypatch):

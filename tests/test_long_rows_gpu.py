@@ -61,7 +61,7 @@ def test_csr_hops_bit_exact(case, heavy):
     check_layers(f, hops)
 
 
-@pytest.mark.parametrize("rows_per_block", [600, 97, 8])
+@pytest.mark.parametrize("rows_per_block", [1279, 600, 97, 8])
 def test_tiled_hops_bit_exact(case, rows_per_block):
     """The column-ordered kernel (forced: the operand is below TILED_MIN_ROWS) with the layer
     mean fused as in the headline path."""

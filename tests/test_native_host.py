@@ -100,54 +100,60 @@ def test_partition_covers_rows_and_remaps_columns(world):
 
 def _walk_tiled_plan(plan, n_rows, R, row_bytes=256):
     """Replay gnnrec_spmm_tiled_f32's schedule on the host: per row, the (col, val) sequence
-    its accumulator receives, in kernel order; checks the plan's structural rules on the way."""
+    its accumulator receives, in kernel order; checks the plan's structural rules on the way
+    (include/gnnrec.h: chunks of two 16-slot halves, per-chunk {barriers, chain mask}; a row
+    at most one run per group of 8 slots of a half)."""
     xo = plan["xoff"].numpy().view(np.uint32)
     val = plan["val"].numpy()
     meta = plan["meta"].numpy().view(np.uint16)
+    hdr = plan["hdr"].numpy().view(np.uint32)
     wp = plan["wave_ptr"].numpy()
     ns = plan["n_steps"].numpy()
-    W, CH = 16, 16
+    W, CH, H, GR = _lib.TILED_WAVES, _lib.TILED_CHUNK, _lib.TILED_CHUNK // 2, 8
     seq = [[] for _ in range(n_rows)]
     for b in range(plan["n_blocks"]):
-        owner = {}            # (step, row) -> wave: a row lives on one wave per step
-        events = []           # (step, wave, slot index, row, col, val)
+        owner = {}            # (step, row) -> (wave, half): a row lives on one stream per step
+        events = []           # (step, slot index, row, col, val)
         for w in range(W):
-            s0, s1 = wp[b * W + w], wp[b * W + w + 1]
-            assert (s1 - s0) % CH == 0
             cur = 0
-            for c in range(s0, s1, CH):
-                cur += (int(meta[c]) >> 10) & 31
-                rows_in_chunk = [int(meta[c + t]) & 1023 for t in range(CH)]
-                runs = [r for t, r in enumerate(rows_in_chunk)
-                        if r != R and (t == 0 or rows_in_chunk[t - 1] != r)]
-                assert len(runs) == len(set(runs)), "a row must be one run inside a chunk"
-                for t in range(CH):
-                    m = int(meta[c + t])
-                    row, chain = m & 1023, m >> 15
-                    if t > 0:
-                        assert (m >> 10) & 31 == 0
-                        prev = int(meta[c + t - 1]) & 1023
-                        assert chain == (1 if (row == prev and row != R) else 0) or row == R
-                    if row == R:
-                        assert val[c + t] == 0 and chain == 0
-                        continue
-                    assert owner.setdefault((cur, row), w) == w
-                    assert xo[c + t] % row_bytes == 0
-                    events.append((cur, w, c + t, row, int(xo[c + t]) // row_bytes, val[c + t]))
+            for c in range(wp[b * W + w], wp[b * W + w + 1]):
+                cur += int(hdr[2 * c])
+                cm = int(hdr[2 * c + 1])
+                for h in range(2):
+                    base = c * CH + h * H
+                    rows = [int(meta[base + t]) & 2047 for t in range(H)]
+                    for g0 in range(0, H, GR):
+                        grp = rows[g0:g0 + GR]
+                        runs = [r for t, r in enumerate(grp)
+                                if r != R and (t == 0 or grp[t - 1] != r)]
+                        assert len(runs) == len(set(runs)), "a row must be one run per group"
+                    for t in range(H):
+                        row = rows[t]
+                        chain = (cm >> (16 * h + t)) & 1
+                        if row == R:
+                            assert val[base + t] == 0 and chain == 0
+                            continue
+                        assert row < R
+                        assert chain == (1 if (t > 0 and rows[t - 1] == row) else 0)
+                        assert owner.setdefault((cur, row), (w, h)) == (w, h)
+                        assert xo[base + t] % row_bytes == 0
+                        events.append((cur, base + t, row, int(xo[base + t]) // row_bytes,
+                                       val[base + t]))
             assert cur <= max(ns[b] - 1, 0)
-        events.sort(key=lambda e: (e[0], e[2]))
-        for _, _, _, row, col, v in events:
+        events.sort(key=lambda e: (e[0], e[1]))
+        for _, _, row, col, v in events:
             seq[b * R + row].append((col, v))
     return seq
 
 
-@pytest.mark.parametrize("R,panel,sub", [(600, 32768, 0), (600, 131072, 4096), (37, 5, 2),
-                                         (37, 64, 8), (1, 1, 0), (16, 1 << 30, 64)])
+@pytest.mark.parametrize("R,panel,sub", [(1117, 32768, 0), (1117, 131072, 4096), (37, 5, 2),
+                                         (37, 64, 8), (1, 1, 0), (16, 1 << 30, 64),
+                                         (1279, 4096, 512), (1277, 131072, 4096)])
 def test_tiled_plan_preserves_every_row_chain(R, panel, sub):
     """The column-ordered plan visits each row's neighbours exactly in CSR order (ascending
-    columns: the fmaf order that makes the hop bit-exact), once each, one wave per row and
-    step, a row at most one run of slots per chunk (sub-panel order interleaves rows), with
-    chain flags exactly on run continuations inside a chunk."""
+    columns: the fmaf order that makes the hop bit-exact), once each, one slot stream per row
+    and step, a row at most one run of slots per half-chunk (sub-panel order interleaves
+    rows), with chain bits exactly on run continuations inside a half-chunk."""
     rng = np.random.default_rng(R + panel + sub)
     u = np.concatenate([rng.integers(0, 700, 6000), np.zeros(300, np.int64)])  # a long row
     i = np.concatenate([rng.integers(0, 900, 6000), np.arange(300)])
@@ -155,7 +161,9 @@ def test_tiled_plan_preserves_every_row_chain(R, panel, sub):
     plan = G.tiled_plan(64, rows_per_block=R, panel=panel, sub_panel=sub)
     n = G.shape[0]
     assert plan["n_blocks"] == (n + R - 1) // R
-    assert plan["n_slots"] >= G.nnz and plan["xoff"].numel() == plan["n_slots"] + 16
+    assert plan["n_slots"] >= G.nnz
+    assert plan["xoff"].numel() == (plan["n_chunks"] + _lib.TILED_TAIL) * _lib.TILED_CHUNK
+    assert plan["hdr"].numel() == 2 * (plan["n_chunks"] + _lib.TILED_TAIL)
     seq = _walk_tiled_plan(plan, n, R)
     rp, col, val = G.row_ptr.numpy(), G.col.numpy(), G.val.numpy()
     for r in range(n):

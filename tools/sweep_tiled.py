@@ -2,7 +2,7 @@
 per shape, build the plan, time one hop with HIP events (median of N), and check its bits
 against the row-parallel CSR kernel. One JSON line per shape (not part of the product).
 
-    python tools/sweep_tiled.py R:PANEL:SUB [R:PANEL:SUB ...]
+    python tools/sweep_tiled.py [--d 64] R:PANEL:SUB[:MEET_US] [...]
 """
 import json
 import sys
@@ -16,32 +16,49 @@ sys.path[:0] = [str(ROOT / "gnn-recommendations_amd"), str(ROOT)]
 import bench  # noqa: E402
 from src.ops import functional as F  # noqa: E402
 
+args = sys.argv[1:]
+D, LDX, FOLD = 64, None, 0
+while args and args[0] in ("--d", "--ldx", "--fold"):
+    if args[0] == "--d":
+        D = int(args[1])
+    elif args[0] == "--ldx":
+        LDX = int(args[1])
+    else:   # timing floor: every gather folded into the first FOLD bytes of x (L2-resident)
+        FOLD = int(args[1])
+    args = args[2:]
+LDX = LDX or D
 dev = torch.device("cuda", 0)
 g = bench.build_graph(1_000_000, 1_000_000, 100_000_000, 0, 16).to(dev)
-x = torch.randn(g.shape[0], 64, device=dev, generator=torch.Generator(dev).manual_seed(0)) * 0.1
-ref = torch.empty_like(x)
+x = (torch.randn(g.shape[0], LDX, device=dev, generator=torch.Generator(dev).manual_seed(0))
+     * 0.1)[:, :D]
+ref = torch.empty(x.shape, device=dev)
 F.TILED_HOP = False
 F.spmm_into(g, x, ref)
 torch.cuda.synchronize()
-y = torch.empty_like(x)
-for spec in sys.argv[1:]:
-    R, panel, sub = (int(v) for v in spec.split(":"))
+y = torch.empty(x.shape, device=dev)
+for spec in args:
+    R, panel, sub, *rest = (int(v) for v in spec.split(":"))
+    meet = rest[0] if rest else F.TILED_MEET_US
     t0 = time.time()
-    plan = g.tiled_plan(64, rows_per_block=R, panel=panel, sub_panel=sub)
+    plan = g.tiled_plan(LDX, rows_per_block=R, panel=panel, sub_panel=sub)
     t_plan = time.time() - t0
+    if FOLD:
+        plan = dict(plan)
+        plan["xoff"] = torch.remainder(plan["xoff"].long() & 0xFFFFFFFF, FOLD).int()
     times = []
     for _ in range(12):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        F.spmm_tiled_into(g, x, y, plan)
+        F.spmm_tiled_into(g, x, y, plan, meet_us=meet)
         b.record()
         torch.cuda.synchronize()
         times.append(a.elapsed_time(b))
     exact = bool(torch.equal(y.view(torch.int32), ref.view(torch.int32)))
     times.sort()
-    print(json.dumps({"R": R, "panel": panel, "sub_panel": sub, "n_blocks": plan["n_blocks"],
+    print(json.dumps({"d": D, "ldx": LDX, "fold": FOLD, "R": R, "panel": panel, "sub_panel": sub, "meet_us": meet,
+                      "n_blocks": plan["n_blocks"],
                       "pad": plan["n_slots"] / g.nnz - 1, "ms_median": times[len(times) // 2],
                       "ms_min": times[0], "bit_exact": exact, "plan_s": round(t_plan, 1)}),
           flush=True)
-    g._plans.pop(("tiled", 64, R, panel, sub), None)
+    g._plans.pop(("tiled", LDX, R, panel, sub), None)
     del plan
