@@ -17,7 +17,7 @@ from __future__ import annotations
 import torch
 
 from .graph import CsrGraph, ShardInfo, inv_sqrt_degrees
-from . import functional
+from . import functional, library  # library: registers torch.ops.gnnrec.*
 from .functional import (dense_layer, gas, gat_aggregate, lightgcn_propagate, ngcf_layer,
                          score_topk, spmm, spmm_gas)
 

@@ -37,10 +37,11 @@ from .graph import CsrGraph
 HopFn = Callable[..., None]
 
 
-def _native_hop(adj, x, y, *, epi, self_rows, acc, acc_div, x_mask=None, y_active=None):
+def _native_hop(adj, x, y, *, epi, self_rows, acc, acc_div, x_mask=None, y_active=None,
+                meet_us=None):
     from .functional import spmm_into
     spmm_into(adj, x, y, epi=epi, self_rows=self_rows, acc=acc, acc_div=acc_div,
-              x_mask=x_mask, y_active=y_active)
+              x_mask=x_mask, y_active=y_active, meet_us=meet_us)
 
 
 class DistributedGraph:
@@ -197,11 +198,17 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
     the hop outputs feed the next hop directly (no gather, no copy).
     overlap_chunks > 1 (point-to-point exchange only): the hop runs in that many row chunks
     and each chunk's transfer is posted as soon as its kernel is queued, so the exchange of
-    chunk c overlaps the SpMM of chunk c+1.
+    chunk c overlaps the SpMM of chunk c+1. Each chunk is a cached row view of the shard with
+    its own column-ordered plan (spmm_into picks the tiled kernel for chunks of at least
+    TILED_MIN_ROWS rows), launched without the pass-start meeting (RCCL kernels share the
+    device while it runs).
     masks(k, x_in) -> (x_mask [padded rows], y_active [n_local]) or None: the sparse-input /
     row-subset options of the native hop (spmm_into) for hop k.
     """
     hop = hop_fn or _native_hop
+    # the native hop's pass-start meeting must not wait on workgroups that share the device
+    # with concurrent RCCL kernels (overlapped chunks)
+    chunk_kw = {"meet_us": 0} if hop is _native_hop else {}
 
     def mkw(k, x_in):
         m = masks(k, x_in) if masks is not None else None
@@ -246,7 +253,7 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
                                            "y_active": None if m[1] is None else m[1][c0:r1]}
                 hop(dg.shard.row_slice(c0, r1), x_in, Y[c0:r1], epi=epi,
                     self_rows=self_rows[c0:r1], acc=acc[c0:r1], acc_div=float(n_layers + 1),
-                    **kw)
+                    **kw, **chunk_kw)
             pending += dg.post_chunk(x_next, Y, c0, c1)
         dg.finish(pending)
         x_in = x_next

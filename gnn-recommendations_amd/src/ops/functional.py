@@ -48,13 +48,17 @@ SPMM_HEAVY_THRESHOLD = 256
 
 
 # Column-ordered hop (gnnrec_spmm_tiled_f32): the same bits, used for any d
-# that is a multiple of 32 when the operand fills at least one pass of the persistent grid and
-# has no row longer than TILED_MAX_DEGREE (a long row's panel run stays on one slot stream and
-# would hold its step). Masked / row-subset hops keep the CSR kernel. Rows per block are
-# evened out so every pass of the persistent grid is full (G100M: 14 passes of 1117 rows —
-# 7 per 32-feature slice at d = 64 — not 6 of 1279 plus a tail pass).
+# that is a multiple of 32 when the operand has at least TILED_MIN_ROWS rows, the gathered
+# table is larger than the chip's L2s together (TILED_MIN_TABLE_BYTES; below that the
+# row-parallel gathers hit L2 anyway) and no row is longer than TILED_MAX_DEGREE (a long row's
+# panel run stays on one slot stream and would hold its step). Crossover on G100M row slices
+# (profiles/r02/exp_chunks.jsonl, d = 64): 31K rows CSR 0.124 vs tiled 0.140 ms, 62.5K rows
+# 0.232 vs 0.208, 250K 0.88 vs 0.62. Masked / row-subset hops keep the CSR kernel. Rows per
+# block are evened out so every pass of the persistent grid is full (G100M: 14 passes of 1117
+# rows — 7 per 32-feature slice at d = 64 — not 6 of 1279 plus a tail pass).
 TILED_HOP = True
-TILED_MIN_ROWS = 256 * 600
+TILED_MIN_ROWS = 49152
+TILED_MIN_TABLE_BYTES = 32 << 20
 TILED_MAX_DEGREE = 4096
 TILED_MAX_ROWS = _lib.TILED_MAX_ROWS
 TILED_BALANCE_PASSES = True
@@ -67,15 +71,16 @@ def _tiled_rows_per_block(n_rows: int, device) -> int:
     if not TILED_BALANCE_PASSES:
         return TILED_MAX_ROWS
     cus = torch.cuda.get_device_properties(device).multi_processor_count
-    passes = -(-n_rows // (cus * TILED_MAX_ROWS))
+    passes = max(1, -(-n_rows // (cus * TILED_MAX_ROWS)))
     return min(TILED_MAX_ROWS, -(-n_rows // (passes * cus)))
 
 
 def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None):
     """The column-ordered plan spmm_into would use for (adj, x), or None (CSR kernel)."""
     if (not TILED_HOP or x_mask is not None or y_active is not None or x.shape[1] % 32
-            or adj.n_rows < TILED_MIN_ROWS or adj.nnz == 0
+            or adj.n_rows < max(TILED_MIN_ROWS, 1) or adj.nnz == 0
             or x.shape[0] * x.stride(0) * 4 >= 1 << 32
+            or x.shape[0] * x.shape[1] * 4 < TILED_MIN_TABLE_BYTES
             or adj.max_degree() > TILED_MAX_DEGREE):
         return None
     return adj.tiled_plan(x.stride(0), rows_per_block=_tiled_rows_per_block(adj.n_rows, x.device))
@@ -98,11 +103,12 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
               self_rows: Optional[torch.Tensor] = None, acc: Optional[torch.Tensor] = None,
               acc_div: float = 1.0, heavy_threshold: Optional[int] = None,
               x_mask: Optional[torch.Tensor] = None,
-              y_active: Optional[torch.Tensor] = None) -> None:
+              y_active: Optional[torch.Tensor] = None, meet_us: Optional[int] = None) -> None:
     """y = A x with an optional fused layer-mean epilogue (gnnrec_spmm_csr_masked_f32: rows
     longer than `heavy_threshold` run on the workgroup-per-row kernel; rows of x whose
     `x_mask` byte is 0 are all-zero and are not gathered — same bits; destination rows whose
-    `y_active` byte is 0 are not computed — y is +0 there, or the true value)."""
+    `y_active` byte is 0 are not computed — y is +0 there, or the true value). `meet_us`: the
+    column-ordered kernel's pass-start meeting bound (None: TILED_MEET_US)."""
     _require_device(adj, x, y, self_rows, acc)
     if x_mask is not None and (x_mask.dtype != torch.uint8 or x_mask.device != x.device
                                or x_mask.numel() < adj.shape[1]):
@@ -118,7 +124,8 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
                          "destination row")
     plan = tiled_plan_for(adj, x, x_mask, y_active)
     if plan is not None:
-        spmm_tiled_into(adj, x, y, plan, epi=epi, self_rows=self_rows, acc=acc, acc_div=acc_div)
+        spmm_tiled_into(adj, x, y, plan, epi=epi, self_rows=self_rows, acc=acc, acc_div=acc_div,
+                        meet_us=meet_us)
         return
     check(L.gnnrec_spmm_csr_masked_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(x_mask),
                                        ptr(y_active), ptr(y), y.stride(0) if y is not None else d, d, epi,
@@ -273,48 +280,26 @@ def lightgcn_forward(adj: CsrGraph, x0: torch.Tensor, n_layers: int,
     return out, layers
 
 
-# ---- autograd ------------------------------------------------------------------------------
-class _SpMM(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, adj: CsrGraph, x: torch.Tensor):
-        ctx.adj = adj
-        return spmm_forward(adj, x)
-
-    @staticmethod
-    def backward(ctx, g):
-        adj: CsrGraph = ctx.adj
-        if adj.shard_info is not None:
-            raise NotImplementedError("backward through a row shard: use ops.distributed")
-        return None, spmm_forward(adj.t(), g.contiguous())
-
-
+# ---- autograd: through the registered torch.library ops (src/ops/library.py) --------------
 def spmm(adj: CsrGraph, x: torch.Tensor) -> torch.Tensor:
-    """Drop-in for torch.sparse.mm(adj_matrix, x) with a CsrGraph operand (bit-exact)."""
-    return _SpMM.apply(adj, x)
-
-
-class _LightGCN(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, adj: CsrGraph, x0: torch.Tensor, n_layers: int, need=None):
-        ctx.adj, ctx.n_layers = adj, n_layers
-        if need is not None:
-            return lightgcn_forward_rows(adj, x0, n_layers, need)
-        out, _ = lightgcn_forward(adj, x0, n_layers)
-        return out
-
-    @staticmethod
-    def backward(ctx, g):
-        # d/dx0 of mean_k A^k x0 is mean_k (A^T)^k g: the same propagation over A^T, its
-        # first hops skipping the all-zero rows of the (sparse) incoming gradient.
-        return None, lightgcn_backward(ctx.adj, g, ctx.n_layers), None, None
+    """Drop-in for torch.sparse.mm(adj_matrix, x) with a CsrGraph operand (bit-exact):
+    torch.ops.gnnrec.spmm, differentiable (backward = the same kernel over A^T)."""
+    from . import library
+    library.register(adj)
+    return torch.ops.gnnrec.spmm(adj.row_ptr, adj.col, adj.val, x, adj.shape[1])
 
 
 def lightgcn_propagate(adj: CsrGraph, x0: torch.Tensor, n_layers: int,
                        need: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Fused K-hop LightGCN propagation + layer mean (lightgcn.py:76-95), differentiable.
-    With `need` (uint8 [N]) only those output rows are defined (lightgcn_forward_rows); the
-    gradient must then be zero elsewhere, as it is when only those rows are read."""
-    return _LightGCN.apply(adj, x0, int(n_layers), need)
+    """Fused K-hop LightGCN propagation + layer mean (lightgcn.py:76-95), differentiable:
+    torch.ops.gnnrec.lightgcn_propagate (backward = mean_k (A^T)^k g, its first hops skipping
+    the all-zero rows of the sparse incoming gradient). With `need` (uint8 [N]) only those
+    output rows are defined (lightgcn_forward_rows); the gradient must then be zero
+    elsewhere, as it is when only those rows are read."""
+    from . import library
+    library.register(adj)
+    return torch.ops.gnnrec.lightgcn_propagate(adj.row_ptr, adj.col, adj.val, x0, adj.shape[1],
+                                               int(n_layers), need)
 
 
 # ---- fused inference kernels ----------------------------------------------------------

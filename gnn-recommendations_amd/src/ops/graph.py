@@ -159,8 +159,15 @@ class CsrGraph:
                 row_ptr.ctypes.data, col.ctypes.data, cnt.ctypes.data, N, dis.ctypes.data,
                 0 if normalization == "symmetric" else 1, val.ctypes.data, int(n_threads)),
                 "normalize_values")
+        # D^-1/2 A D^-1/2 is symmetric in exact arithmetic; its fp32 values fl(fl(dis_r a) dis_c)
+        # are bitwise symmetric only when every multiplicity a is a power of two (then
+        # fl(dis_r a) is exact and the two products commute) — otherwise A^T is built
+        # explicitly for backward (t()), as torch.sparse.mm's autograd transposes the stored
+        # values.
+        sym = normalization == "none" or (normalization == "symmetric" and bool(
+            nnz == 0 or np.all(np.frexp(cnt)[0] == 0.5)))
         g = cls(torch.from_numpy(row_ptr), torch.from_numpy(col), torch.from_numpy(val), (N, N),
-                int(n_users), int(n_items), symmetric=normalization in ("symmetric", "none"))
+                int(n_users), int(n_items), symmetric=sym)
         return g.to(device)
 
     @classmethod
@@ -211,9 +218,10 @@ class CsrGraph:
                 _lib.ptr(row_ptr), _lib.ptr(col), _lib.ptr(cnt), N, _lib.ptr(dis),
                 0 if normalization == "symmetric" else 1, _lib.ptr(val), stream),
                 "normalize_values_device")
+        sym = normalization == "none" or (normalization == "symmetric" and bool(
+            nz == 0 or torch.all(torch.frexp(cnt).mantissa == 0.5)))   # as from_interactions
         return cls(row_ptr, col.clone(), val.clone(),
-                   (N, N), int(n_users), int(n_items),
-                   symmetric=normalization in ("symmetric", "none"))
+                   (N, N), int(n_users), int(n_items), symmetric=sym)
 
     @classmethod
     def from_scipy(cls, adj, n_users: Optional[int] = None, n_items: Optional[int] = None,

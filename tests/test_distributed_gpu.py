@@ -35,8 +35,10 @@ def _graph():
 def _model(kind, nu, ni, dev):
     from src.models import GAT, LightGCN, NGCFGroupShuffle
     torch.manual_seed(7)
-    if kind in ("lightgcn", "train"):
+    if kind in ("lightgcn", "train", "lightgcn_tiled"):
         m = LightGCN(nu, ni, 64, 3, 0.1)
+    elif kind == "lightgcn_d128_tiled":
+        m = LightGCN(nu, ni, 128, 3, 0.1)
     elif kind == "ngcf_gs":
         m = NGCFGroupShuffle(nu, ni, 64, [64, 64, 64], 0.1, 0.1, 8, 0.3)
     else:
@@ -45,6 +47,15 @@ def _model(kind, nu, ni, dev):
 
 
 def _worker(rank, world, port, kind, exchange, q):
+    try:
+        _work(rank, world, port, kind, exchange, q)
+    except BaseException as e:   # report instead of leaving the parent waiting on the queue
+        import traceback
+        q.put((rank, None, traceback.format_exc(), None))
+        raise
+
+
+def _work(rank, world, port, kind, exchange, q):
     import sys
     from conftest import PKG, ROOT
     sys.path[:0] = [str(ROOT), str(PKG)]
@@ -55,6 +66,9 @@ def _worker(rank, world, port, kind, exchange, q):
                                          lightgcn_propagate_dist, ngcf_forward_dist)
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
+        if kind.endswith("_tiled"):   # the small test graph through the column-ordered kernel
+            from src.ops import functional as F
+            F.TILED_MIN_ROWS, F.TILED_MIN_TABLE_BYTES = 0, 0
         full, nu, ni = _graph()
         m = _model(kind, nu, ni, dev)
         with torch.no_grad():
@@ -81,6 +95,13 @@ def _worker(rank, world, port, kind, exchange, q):
                 return
             if kind == "lightgcn":
                 mine = lightgcn_propagate_dist(dg, x0p, 3, overlap_chunks=3)
+            elif kind.endswith("_tiled"):
+                from src.ops import functional as F
+                for c0, c1 in dg.chunk_bounds(3):   # every overlap chunk runs the tiled kernel
+                    if min(c1, dg.n_local) > c0:
+                        assert F.tiled_plan_for(dg.shard.row_slice(c0, min(c1, dg.n_local)),
+                                                x0p) is not None
+                mine = lightgcn_propagate_dist(dg, x0p, 3, overlap_chunks=3)
             elif kind == "ngcf_gs":
                 mine = ngcf_forward_dist(dg, m, x0p)
             else:
@@ -93,6 +114,8 @@ def _worker(rank, world, port, kind, exchange, q):
 
 
 @pytest.mark.parametrize("kind,exchange", [("lightgcn", "p2p"), ("lightgcn", "allgather"),
+                                           ("lightgcn_tiled", "p2p"),
+                                           ("lightgcn_d128_tiled", "p2p"),
                                            ("ngcf_gs", "auto"), ("gat", "auto"),
                                            ("train", "auto")])
 def test_two_ranks_native_match_single_device(cuda, kind, exchange):
@@ -103,6 +126,8 @@ def test_two_ranks_native_match_single_device(cuda, kind, exchange):
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in procs]
+    for rank, mine, ref, _ in res:
+        assert mine is not None, f"rank {rank} failed:\n{ref}"
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0

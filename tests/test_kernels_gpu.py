@@ -440,6 +440,7 @@ def test_lightgcn_through_tiled_hop_is_bit_exact(cuda, monkeypatch):
     csr, _ = F.lightgcn_forward(g, xd, 3)
     monkeypatch.setattr(F, "TILED_HOP", True)
     monkeypatch.setattr(F, "TILED_MIN_ROWS", 0)
+    monkeypatch.setattr(F, "TILED_MIN_TABLE_BYTES", 0)
     assert F.tiled_plan_for(g, xd) is not None
     out, _ = F.lightgcn_forward(g, xd, 3)
     np.testing.assert_array_equal(bits(out.cpu().numpy()), ref)
