@@ -45,6 +45,7 @@ constexpr int kTiledTail = GNNREC_TILED_TAIL;
 constexpr int kSlice = 32;                        // features per pass
 constexpr int kRowMask = 2047;
 constexpr int kGroup = 8;                         // steps whose reads precede their writes
+constexpr int kEpiBatch = 8;                      // epilogue rows per wave with loads in flight
 static_assert(kHalf == 16, "a half-chunk is one DPP row of 16 lanes");
 static_assert(kHalf == 2 * kGroup, "a half-chunk is applied as two groups");
 static_assert(GNNREC_TILED_MAX_ROWS < kRowMask, "row field is 11 bits (row R = scratch)");
@@ -191,7 +192,8 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     const int64_t b = wptr[s], e = wptr[s + 1];
     int cur = 0;
     if (b < e) {
-      // slot loads two chunks ahead, gathers one chunk ahead of the LDS chain
+      // slot loads two chunks ahead, gathers one chunk ahead of the LDS chain (a third
+      // chunk of gathers in flight measured the same: profiles/r02/tiled_depth3.jsonl)
       TiledSlots M0, M1, M2;
       float X0[kHalf], X1[kHalf];
       int64_t c = b;
@@ -227,18 +229,35 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
       __syncthreads();
       GNNREC_TILED_STAMP(ev);
     }
+    // epilogue: a wave's rows in batches of kEpiBatch, every load of a batch issued before
+    // the first use (one memory latency per batch, not per row)
     const int64_t r0 = (int64_t)blk * R;
     const int64_t cf = (int64_t)slice * kSlice + f;
-    for (int i = 2 * w + half; i < R; i += 2 * kTiledWaves) {
-      const int64_t r = r0 + i;
-      if (r >= n_rows) break;
-      const float a = acc[i * kSlice + f];
-      if (!(epi & GNNREC_EPI_NO_Y)) y[r * ldy + cf] = a;
-      if (epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) {
-        float bsum = (epi & GNNREC_EPI_ACC_INIT) ? self[r * ld_self + cf] : accg[r * ld_acc + cf];
-        bsum = bsum + a;
-        if (epi & GNNREC_EPI_ACC_DIV) bsum = bsum / acc_div;
-        accg[r * ld_acc + cf] = bsum;
+    const bool acc_on = (epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) != 0;
+    const float* base_src = (epi & GNNREC_EPI_ACC_INIT) ? self : accg;
+    const int64_t ld_base = (epi & GNNREC_EPI_ACC_INIT) ? ld_self : ld_acc;
+    constexpr int kStride = 2 * kTiledWaves;
+    for (int i0 = 2 * w + half; i0 < R; i0 += kStride * kEpiBatch) {
+      float a[kEpiBatch], base[kEpiBatch];
+#pragma unroll
+      for (int q = 0; q < kEpiBatch; ++q) {
+        const int i = i0 + q * kStride;
+        const int64_t r = r0 + i;
+        const bool ok = i < R && r < n_rows;
+        a[q] = ok ? acc[i * kSlice + f] : 0.f;
+        base[q] = (ok && acc_on) ? base_src[r * ld_base + cf] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < kEpiBatch; ++q) {
+        const int i = i0 + q * kStride;
+        const int64_t r = r0 + i;
+        if (i >= R || r >= n_rows) break;
+        if (!(epi & GNNREC_EPI_NO_Y)) y[r * ldy + cf] = a[q];
+        if (acc_on) {
+          float bsum = base[q] + a[q];
+          if (epi & GNNREC_EPI_ACC_DIV) bsum = bsum / acc_div;
+          accg[r * ld_acc + cf] = bsum;
+        }
       }
     }
     __syncthreads();
