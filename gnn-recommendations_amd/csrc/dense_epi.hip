@@ -15,6 +15,8 @@
 //            output tile and store whole rows (float4, coalesced).
 // MFMA 16x16x4 f32 lane maps (cdna_hip_programming.md §3): A[i=l&15][k=l>>4],
 // B[k=l>>4][j=l&15], C/D: col = l&15, row = 4*(l>>4) + reg.
+#include <algorithm>
+
 #include "gather.h"
 
 namespace gnnrec {
@@ -272,6 +274,179 @@ __global__ __launch_bounds__(64 * NW) void spmm_mfma_kernel(DenseParams p) {
   }
 }
 
+// Streaming transform for d = 64 (the split form's second kernel; n = A x is already in HBM):
+// every wave owns 16-row tiles on its own — no workgroup barrier inside the loop. Per tile it
+// stages [n | x (.) n] (MODE 0) or n (MODE 1) in its private LDS rows, runs the 16x16x4 f32
+// MFMA chains of all four 16-column output tiles (8 independent accumulators in MODE 0), the
+// GAS product on the matrix cores, and stores whole rows (float4). The next tile's rows are in
+// flight in registers meanwhile. Same MFMA instructions, fragment maps and k order as
+// spmm_mfma_kernel<64, MODE, 8, false>, so the same bits.
+template <int MODE, int NW>
+__global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
+  constexpr int D = 64;
+  constexpr int KD = MODE == 0 ? 2 * D : D;
+  constexpr int LDA = KD + 2;        // == 2 mod 32: conflict-free A-fragment reads
+  constexpr int LDO = D + 4;
+  constexpr int LDB = D + 16;        // == 16 mod 32: conflict-free B-fragment reads
+  constexpr int STEPS = KD / 4;
+  constexpr int TSZ = 16 * (LDA > LDO ? LDA : LDO);   // the o tile aliases the A tile
+  __shared__ __attribute__((aligned(16))) float b_lds[KD * LDB];
+  __shared__ __attribute__((aligned(16))) float g_lds[MODE == 0 ? D * LDB : 4];
+  __shared__ __attribute__((aligned(16))) float t_lds[NW][TSZ];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i16 = lane & 15, k4 = lane >> 4;
+  float* at = t_lds[wave];
+  for (int e = threadIdx.x; e < KD * D; e += 64 * NW) {
+    const int k = e / D, j = e % D;
+    float v;
+    if (MODE == 0) v = k < D ? p.W1[j * D + k] : p.W2[j * D + (k - D)];
+    else v = p.M[k * D + j];
+    b_lds[k * LDB + j] = v;
+  }
+  const bool gas = MODE == 0 && p.gas_blocks != nullptr;
+  if (gas) {   // G[k][j] = blockdiag(blocks)[k][perm[j]]
+    const int bs = p.gas_bs;
+    for (int e = threadIdx.x; e < D * D; e += 64 * NW) {
+      const int k = e / D, j = e % D;
+      const int c = p.gas_perm[j];
+      const int b = c / bs, col = c - b * bs;
+      g_lds[k * LDB + j] =
+          (k / bs == b) ? p.gas_blocks[(int64_t)(b * bs + (k - b * bs)) * bs + col] : 0.f;
+    }
+  }
+  float bias1[4], bias2[4];
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt) {
+    bias1[nt] = MODE == 0 ? p.b1[16 * nt + i16] : 0.f;
+    bias2[nt] = MODE == 0 ? p.b2[16 * nt + i16] : 0.f;
+  }
+  __syncthreads();
+
+  // row loads: lane covers rows 4 it + (lane >> 4), columns 4 (lane & 15) .. +3, it = 0..3
+  const int lr = lane >> 4, lc = 4 * (lane & 15);
+  const int64_t n_tiles = ceil_div(p.A.n_rows, 16);
+  const int64_t stride = (int64_t)gridDim.x * NW;
+  float4 pn[4], px[4];
+  auto load = [&](int64_t tile) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int64_t r = tile * 16 + 4 * it + lr;
+      pn[it] = px[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (tile < n_tiles && r < p.A.n_rows) {
+        pn[it] = *reinterpret_cast<const float4*>(p.x + r * p.ldx + lc);
+        if (MODE == 0) px[it] = *reinterpret_cast<const float4*>(p.x_self + r * p.ld_self + lc);
+      }
+    }
+  };
+  int64_t tile = (int64_t)blockIdx.x * NW + wave;
+  load(tile);
+  for (; tile < n_tiles; tile += stride) {
+    // stage this tile, then start the next one's loads
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      float* ar = at + (4 * it + lr) * LDA + lc;
+      const float nv[4] = {pn[it].x, pn[it].y, pn[it].z, pn[it].w};
+      const float xv[4] = {px[it].x, px[it].y, px[it].z, px[it].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        ar[q] = nv[q];
+        if (MODE == 0) ar[D + q] = xv[q] * nv[q];
+      }
+    }
+    float4 rs[4];   // MODE 1 residual rows (loaded with the tile, used at the store)
+    if (MODE == 1 && p.resid) {
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int64_t r = tile * 16 + 4 * it + lr;
+        rs[it] = r < p.A.n_rows ? *reinterpret_cast<const float4*>(p.resid + r * p.ld_resid + lc)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    load(tile + stride);
+    // MFMA: c1 over k < D, c2 over k >= D (MODE 0: the reference's two Linear layers)
+    floatx4 c1[4], c2[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) c1[nt] = c2[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const float* arow = at + i16 * LDA + k4;
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s) {
+      const float a = arow[4 * s];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) {
+        const float b = b_lds[(4 * s + k4) * LDB + 16 * nt + i16];
+        if (MODE == 0 && s >= STEPS / 2)
+          c2[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c2[nt], 0, 0, 0);
+        else
+          c1[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c1[nt], 0, 0, 0);
+      }
+    }
+    // o tile (rows 4 k4 + q, column 16 nt + i16) over the A tile (all its reads are done)
+    float* ot = at;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float v;
+        if (MODE == 0) {
+          v = (c1[nt][q] + bias1[nt]) + (c2[nt][q] + bias2[nt]);
+          v = v > 0.f ? v : v * p.slope;
+        } else {
+          v = c1[nt][q];
+        }
+        ot[(4 * k4 + q) * LDO + 16 * nt + i16] = v;
+      }
+    if (gas) {   // out = o @ G on the matrix cores, k ascending (== gas_row_v's chain)
+      floatx4 cg[4];
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) cg[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+      const float* orow = ot + i16 * LDO + k4;
+#pragma unroll
+      for (int st = 0; st < D / 4; ++st) {
+        const float a = orow[4 * st];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt)
+          cg[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+              a, g_lds[(4 * st + k4) * LDB + 16 * nt + i16], cg[nt], 0, 0, 0);
+      }
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ot[(4 * k4 + q) * LDO + 16 * nt + i16] = cg[nt][q];
+    }
+    // whole rows out
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int row = 4 * it + lr;
+      const int64_t r = tile * 16 + row;
+      if (r >= p.A.n_rows) continue;
+      const float* orow = ot + row * LDO + lc;
+      float o[4] = {orow[0], orow[1], orow[2], orow[3]};
+      if (MODE == 1) {
+        const float rv[4] = {rs[it].x, rs[it].y, rs[it].z, rs[it].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = p.resid ? p.c_out * o[q] + p.c_res * rv[q] : p.c_out * o[q];
+        if (p.acc_mode) {
+          float* ar = p.acc + r * p.ld_acc + lc;
+          float bse[4];
+          if (p.acc_mode == 1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) bse[q] = p.w_res * rv[q];
+          } else {
+            const float4 t = *reinterpret_cast<const float4*>(ar);
+            bse[0] = t.x; bse[1] = t.y; bse[2] = t.z; bse[3] = t.w;
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) bse[q] = bse[q] + p.w_out * o[q];
+          *reinterpret_cast<float4*>(ar) = make_float4(bse[0], bse[1], bse[2], bse[3]);
+        }
+      }
+      if (p.y) *reinterpret_cast<float4*>(p.y + r * p.ldy + lc) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+}
+
 }  // namespace gnnrec
 
 using namespace gnnrec;
@@ -287,6 +462,17 @@ namespace {
 // Waves per workgroup: 8 for d <= 64 (weights in LDS), 4 for d = 128 (weights in VGPRs).
 template <int MODE, bool GATHER>
 int launch_dense(const DenseParams& p, int d, hipStream_t s) {
+  if (!GATHER && d == 64) {
+    constexpr int NW = 8;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    const int64_t tiles = ceil_div(p.A.n_rows, 16 * NW);
+    const unsigned grid = (unsigned)std::min<int64_t>(tiles, (int64_t)cus);
+    hipLaunchKernelGGL((transform64_kernel<MODE, NW>), dim3(grid), dim3(64 * NW), 0, s, p);
+    return check_launch(MODE == 0 ? "ngcf_transform" : "dense_transform");
+  }
   auto go = [&](auto kern, int nw) {
     const int64_t tiles = ceil_div(p.A.n_rows, 4 * nw);
     const unsigned grid = (unsigned)(tiles < 2048 ? tiles : 2048);

@@ -76,14 +76,41 @@ class NGCF(BaseRecommender):
                 nn.init.zeros_(lin.bias)
 
     def forward(self, adj_matrix) -> Tuple[torch.Tensor, torch.Tensor]:
-        x = self._initial_table()
-        outs = [x]
-        for layer in self.layers:
-            x = layer(x, adj_matrix)
-            outs.append(x)
-        x_final = torch.cat(outs, dim=1)
+        x_final = self._native_concat_forward(adj_matrix, [None] * self.n_layers)
+        if x_final is None:
+            x = self._initial_table()
+            outs = [x]
+            for layer in self.layers:
+                x = layer(x, adj_matrix)
+                outs.append(x)
+            x_final = torch.cat(outs, dim=1)
         user_emb, item_emb = torch.split(x_final, [self.n_users, self.n_items], dim=0)
         return user_emb, item_emb
+
+    def _native_concat_forward(self, adj_matrix, gs_layers):
+        """Inference on a ROCm operand: every layer's fused kernel reads its input from, and
+        writes its output into, its column block of the final [N, (K+1) d] table, so
+        torch.cat(outs, dim=1) (ngcf.py:186) costs no extra pass over 2 GB at G100M. Same
+        values as the layer-by-layer form (the kernels do not depend on row strides).
+        None when a layer cannot take the fused path."""
+        a = ops.as_operand(adj_matrix)
+        d = self.embedding_dim
+        if not all(layer._fused_ok(self.user_embedding.weight, a) and layer.W1.in_features == d
+                   and (gs is None or gs.fusable())
+                   for layer, gs in zip(self.layers, gs_layers)):
+            return None
+        n = self.n_users + self.n_items
+        w = self.user_embedding.weight
+        out = torch.empty((n, d * (self.n_layers + 1)), dtype=w.dtype, device=w.device)
+        out[:self.n_users, :d].copy_(self.user_embedding.weight.detach())
+        out[self.n_users:, :d].copy_(self.item_embedding.weight.detach())
+        for k, (layer, gs) in enumerate(zip(self.layers, gs_layers)):
+            blocks, perm = (gs.blocks(), gs.perm) if gs is not None else (None, None)
+            ops.ngcf_layer(a, out[:, k * d:(k + 1) * d], layer.W1.weight, layer.W1.bias,
+                           layer.W2.weight, layer.W2.bias, layer.activation.negative_slope,
+                           gas_blocks=blocks, gas_perm=perm, fused=layer.single_kernel,
+                           out=out[:, (k + 1) * d:(k + 2) * d])
+        return out
 
     def predict(self, users, items, adj_matrix=None) -> torch.Tensor:
         if adj_matrix is None:
@@ -112,11 +139,13 @@ class NGCFGroupShuffle(NGCF):
                                        for d in self.layer_sizes)
 
     def forward(self, adj_matrix) -> Tuple[torch.Tensor, torch.Tensor]:
-        x = self._initial_table()
-        outs = [x]
-        for layer, gs in zip(self.layers, self.gs_layers):
-            x = layer(x, adj_matrix, gas=gs)
-            outs.append(x)
-        x_final = torch.cat(outs, dim=1)
+        x_final = self._native_concat_forward(adj_matrix, list(self.gs_layers))
+        if x_final is None:
+            x = self._initial_table()
+            outs = [x]
+            for layer, gs in zip(self.layers, self.gs_layers):
+                x = layer(x, adj_matrix, gas=gs)
+                outs.append(x)
+            x_final = torch.cat(outs, dim=1)
         user_emb, item_emb = torch.split(x_final, [self.n_users, self.n_items], dim=0)
         return user_emb, item_emb

@@ -315,16 +315,19 @@ def ngcf_forward_dist(dg: DistributedGraph, model, x0_pad: torch.Tensor, *,
     gs_layers = list(getattr(model, "gs_layers", [None] * len(model.layers)))
     n = dg.n_local
     x_local = dg.local_slice(x0_pad)
-    outs = [x_local]
+    widths = [x_local.shape[1]] + [layer.W1.out_features for layer in model.layers]
+    # every layer writes its column block of the final cat(x0, ..., xK) table directly
+    local = torch.empty((n, sum(widths)), dtype=torch.float32, device=x0_pad.device)
+    local[:, :widths[0]].copy_(x_local)
+    c0 = widths[0]
     x_in = x0_pad
     for k, (layer, gs) in enumerate(zip(model.layers, gs_layers)):
-        y = torch.empty((n, layer.W1.out_features), dtype=torch.float32, device=x0_pad.device)
+        y = local[:, c0:c0 + widths[k + 1]]
         layer_fn(dg.shard, x_in, x_local, layer, gs, y)
-        outs.append(y)
         x_local = y
+        c0 += widths[k + 1]
         if k + 1 < len(model.layers):
             x_in = _exchanged(dg, y)
-    local = torch.cat(outs, dim=1)
     return gather_rows(dg, local) if gather_output else local
 
 
