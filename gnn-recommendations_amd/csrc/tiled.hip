@@ -43,13 +43,17 @@ constexpr int kTiledChunk = GNNREC_TILED_CHUNK;   // slots per chunk (both halve
 constexpr int kHalf = kTiledChunk / 2;            // slots per half = steps per chunk
 constexpr int kTiledTail = GNNREC_TILED_TAIL;
 constexpr int kSlice = 32;                        // features per pass
-constexpr int kRowMask = 2047;
+constexpr int kRowBits = 11;
+constexpr int kRowMask = (1 << kRowBits) - 1;
+constexpr int kMaxPanel = 1 << 20;                // columns per panel (slot word: 21 bits)
+constexpr int kMaxRowBytes = GNNREC_TILED_MAX_LDX * 4;   // keeps the lane offset 32-bit
 constexpr int kGroup = 8;                         // steps whose reads precede their writes
 constexpr int kEpiBatch = 8;                      // epilogue rows per wave with loads in flight
 static_assert(kHalf == 16, "a half-chunk is one DPP row of 16 lanes");
 static_assert(kHalf == 2 * kGroup, "a half-chunk is applied as two groups");
 static_assert(GNNREC_TILED_MAX_ROWS < kRowMask, "row field is 11 bits (row R = scratch)");
 static_assert((GNNREC_TILED_MAX_ROWS + 1) * kSlice * 4 <= 160 * 1024, "LDS");
+static_assert((int64_t)kMaxPanel * kMaxRowBytes <= ((int64_t)1 << 32), "32-bit lane offsets");
 
 // ---- device -----------------------------------------------------------------------------
 #ifdef GNNREC_TILED_TRACE
@@ -68,9 +72,10 @@ __device__ unsigned long long* g_tiled_trace;
 #endif
 
 struct TiledSlots {   // this lane's slot of the chunk: (half, lane % 16)
-  uint32_t o;         // byte offset of the source row
+  uint32_t o;         // byte offset of the source row from the chunk's panel base
   float v;
   uint32_t r;         // byte offset of the destination row's accumulator in LDS
+  uint32_t h;         // word (lane % 4) of the chunk header
 };
 
 template <int T>
@@ -83,14 +88,36 @@ __device__ __forceinline__ float bcastf(float v) {
                                                                0x150 + T, 0xF, 0xF, true));
 }
 
-__device__ __forceinline__ void tiled_slots(const uint32_t* __restrict__ sx,
+// Slot word: (column - chunk's panel base) << kRowBits | local row. The chunk header {step
+// barriers before the chunk, chain mask, panel base column, 0} is loaded with the slots as a
+// vector load (lane l: word l % 4) and read back with v_readlane: a scalar load would share
+// lgkmcnt with the LDS chain and stall it.
+__device__ __forceinline__ void tiled_slots(const uint32_t* __restrict__ ss,
                                             const float* __restrict__ sv,
-                                            const uint16_t* __restrict__ sm, int64_t c,
-                                            int my_slot, TiledSlots& m) {
+                                            const uint32_t* __restrict__ hdr, int64_t c,
+                                            int my_slot, int lane, uint32_t row_bytes,
+                                            TiledSlots& m) {
   const int64_t i = c * kTiledChunk + my_slot;
-  m.o = sx[i];
+  const uint32_t wd = ss[i];
+  m.o = __umul24(wd >> kRowBits, row_bytes);
   m.v = sv[i];
-  m.r = (uint32_t)(sm[i] & kRowMask) * (kSlice * 4);
+  m.r = (wd & kRowMask) * (kSlice * 4);
+  m.h = hdr[4 * c + (lane & 3)];
+}
+
+template <int W>
+__device__ __forceinline__ uint32_t hdr_word(const TiledSlots& m) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)m.h, W);
+}
+
+// The gathers of a chunk read through a buffer whose base is its panel's first source row, so
+// lane offsets stay 32-bit for any table size.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const char* xs, uint64_t xs_bytes,
+                                                             uint32_t base, uint32_t row_bytes) {
+  const uint64_t off = (uint64_t)base * row_bytes;
+  const uint64_t left = off < xs_bytes ? xs_bytes - off : 0;
+  const uint32_t n = left > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)left;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(xs) + off, 0, (int)n, 0x00020000);
 }
 
 template <int... T>
@@ -149,10 +176,10 @@ __device__ __forceinline__ void tiled_apply(float* acc, uint32_t f4, const Tiled
 }
 
 __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
-    const uint32_t* __restrict__ sx, const float* __restrict__ sv,
-    const uint16_t* __restrict__ sm, const uint32_t* __restrict__ hdr,
-    const int64_t* __restrict__ wptr, const int32_t* __restrict__ nsteps, int n_blocks,
-    int nb_pad, int n_items, int R, const float* __restrict__ x, uint32_t x_bytes,
+    const uint32_t* __restrict__ ss, const float* __restrict__ sv,
+    const uint32_t* __restrict__ hdr, const int64_t* __restrict__ wptr,
+    const int32_t* __restrict__ nsteps, int n_blocks, int nb_pad, int n_items, int R,
+    const float* __restrict__ x, uint64_t x_bytes, uint32_t row_bytes,
     float* __restrict__ y, int64_t ldy, int64_t n_rows, int epi, const float* __restrict__ self,
     int64_t ld_self, float* __restrict__ accg, int64_t ld_acc, float acc_div,
     unsigned* __restrict__ sync, unsigned meet_ticks) {
@@ -186,33 +213,32 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     __syncthreads();
     GNNREC_TILED_STAMP(ev);
     const uint32_t soff = (uint32_t)slice * kSlice * 4;
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(x) + (size_t)slice * kSlice, 0, (int)(x_bytes - soff), 0x00020000);
+    const char* xs = reinterpret_cast<const char*>(x) + soff;
+    const uint64_t xs_bytes = x_bytes - soff;
     const int64_t s = (int64_t)blk * kTiledWaves + w;
     const int64_t b = wptr[s], e = wptr[s + 1];
     int cur = 0;
     if (b < e) {
-      // slot loads two chunks ahead, gathers one chunk ahead of the LDS chain (a third
-      // chunk of gathers in flight measured the same: profiles/r02/tiled_depth3.jsonl)
+      // slot loads (and headers) two chunks ahead, gathers one chunk ahead of the LDS chain (a
+      // third chunk of gathers in flight measured the same: profiles/r02/tiled_depth3.jsonl)
       TiledSlots M0, M1, M2;
       float X0[kHalf], X1[kHalf];
       int64_t c = b;
-      tiled_slots(sx, sv, sm, c, my_slot, M0);
-      tiled_slots(sx, sv, sm, c + 1, my_slot, M1);
-      tiled_gather(kSeq, xr, f4, M0, X0);
-#define GNNREC_TILED_STAGE(MLOAD, MG, XG, MA, XA)                       \
-  {                                                                     \
-    tiled_slots(sx, sv, sm, c + 2, my_slot, MLOAD);                     \
-    tiled_gather(kSeq, xr, f4, MG, XG);                                 \
-    const int bar = __builtin_amdgcn_readfirstlane((int)hdr[2 * c]);    \
-    for (int i = 0; i < bar; ++i) {                                     \
-      __syncthreads();                                                  \
-      GNNREC_TILED_STAMP(ev);                                           \
-    }                                                                   \
-    cur += bar;                                                         \
-    const uint32_t cm = __builtin_amdgcn_readfirstlane((int)hdr[2 * c + 1]); \
-    tiled_apply(acc, f4, MA, XA, cm);                                   \
-    if (++c >= e) break;                                                \
+      tiled_slots(ss, sv, hdr, c, my_slot, lane, row_bytes, M0);
+      tiled_slots(ss, sv, hdr, c + 1, my_slot, lane, row_bytes, M1);
+      tiled_gather(kSeq, chunk_rsrc(xs, xs_bytes, hdr_word<2>(M0), row_bytes), f4, M0, X0);
+#define GNNREC_TILED_STAGE(MLOAD, MG, XG, MA, XA)                                     \
+  {                                                                                   \
+    tiled_slots(ss, sv, hdr, c + 2, my_slot, lane, row_bytes, MLOAD);                 \
+    tiled_gather(kSeq, chunk_rsrc(xs, xs_bytes, hdr_word<2>(MG), row_bytes), f4, MG, XG); \
+    const int bar = (int)hdr_word<0>(MA);                                             \
+    for (int i = 0; i < bar; ++i) {                                                   \
+      __syncthreads();                                                                \
+      GNNREC_TILED_STAMP(ev);                                                         \
+    }                                                                                 \
+    cur += bar;                                                                       \
+    tiled_apply(acc, f4, MA, XA, hdr_word<1>(MA));                                    \
+    if (++c >= e) break;                                                              \
   }
       for (;;) {
         GNNREC_TILED_STAGE(M2, M1, X1, M0, X0)
@@ -285,10 +311,9 @@ struct Run {
 };
 
 struct BlockPlan {
-  std::vector<uint32_t> xoff[kTiledWaves];
+  std::vector<uint32_t> slot[kTiledWaves];
   std::vector<float> val[kTiledWaves];
-  std::vector<uint16_t> meta[kTiledWaves];
-  std::vector<uint32_t> hdr[kTiledWaves];
+  std::vector<uint32_t> hdr[kTiledWaves];   // 4 words per chunk
   int32_t nsteps = 0;
 };
 
@@ -352,7 +377,7 @@ void half_chunks(const std::vector<const Run*>& runs, const int32_t* col, int su
 }
 
 void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_t n_rows,
-                 int R, int panel, int sub_panel, int64_t row_bytes, int64_t b, BlockPlan& out) {
+                 int R, int panel, int sub_panel, int64_t b, BlockPlan& out) {
   const int64_t r0 = b * R, r1 = std::min<int64_t>(n_rows, r0 + R);
   std::vector<Run> runs;
   for (int64_t r = r0; r < r1; ++r) {
@@ -392,6 +417,7 @@ void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_
       load[v] += e->n;
       wl[v].push_back(e);
     }
+    const uint32_t base = (uint32_t)runs[i].p * (uint32_t)panel;   // the step's first column
     for (int w = 0; w < kTiledWaves; ++w) {
       if (wl[2 * w].empty() && wl[2 * w + 1].empty()) continue;
       for (int h = 0; h < 2; ++h) half_chunks(wl[2 * w + h], col, sub_panel, hs[h]);
@@ -404,7 +430,7 @@ void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_
         for (int q = 0; q < kTiledChunk; ++q) {
           const Slot& sl = hs[q / kHalf][c + q % kHalf];
           if (sl.run) {
-            x0 = (uint32_t)(col[sl.run->k + sl.t] * row_bytes);
+            x0 = (uint32_t)col[sl.run->k + sl.t] - base;
             break;
           }
         }
@@ -413,19 +439,16 @@ void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_
           for (int t = 0; t < kHalf; ++t) {
             const Slot& sl = hs[h][c + t];
             if (!sl.run) {
-              out.xoff[w].push_back(x0);
+              out.slot[w].push_back(x0 << kRowBits | (uint32_t)R);
               out.val[w].push_back(0.f);
-              out.meta[w].push_back((uint16_t)R);
               continue;
             }
             const int64_t k = sl.run->k + sl.t;
             if (t > 0 && hs[h][c + t - 1].run == sl.run) cmask |= 1u << (16 * h + t);
-            out.xoff[w].push_back((uint32_t)(col[k] * row_bytes));
+            out.slot[w].push_back(((uint32_t)col[k] - base) << kRowBits | (uint32_t)sl.run->row);
             out.val[w].push_back(val[k]);
-            out.meta[w].push_back((uint16_t)sl.run->row);
           }
-        out.hdr[w].push_back(bar);
-        out.hdr[w].push_back(cmask);
+        out.hdr[w].insert(out.hdr[w].end(), {bar, cmask, base, 0u});
         bar = 0;
       }
       cur[w] = step;
@@ -443,14 +466,13 @@ using namespace gnnrec;
 
 extern "C" int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* col,
                                        const float* val, int64_t n_rows, int32_t rows_per_block,
-                                       int32_t panel, int32_t sub_panel, int64_t row_bytes,
-                                       int32_t n_threads, void** plan, int64_t* n_chunks,
-                                       int64_t* n_blocks) {
+                                       int32_t panel, int32_t sub_panel, int32_t n_threads,
+                                       void** plan, int64_t* n_chunks, int64_t* n_blocks) {
   GNNREC_REQUIRE(row_ptr && plan && n_chunks && n_blocks && n_rows >= 0, "tiled_plan: bad args");
   GNNREC_REQUIRE(rows_per_block >= 1 && rows_per_block <= GNNREC_TILED_MAX_ROWS,
                  "tiled_plan: rows_per_block must be in [1, %d]", GNNREC_TILED_MAX_ROWS);
-  GNNREC_REQUIRE(panel >= 1 && sub_panel >= 0 && row_bytes > 0 && row_bytes % 4 == 0,
-                 "tiled_plan: bad panel / sub_panel / row_bytes");
+  GNNREC_REQUIRE(panel >= 1 && sub_panel >= 0, "tiled_plan: bad panel / sub_panel");
+  panel = std::min(panel, kMaxPanel);   // a slot word holds 20 bits of column offset
   const int64_t nnz = n_rows > 0 ? row_ptr[n_rows] - row_ptr[0] : 0;
   GNNREC_REQUIRE(nnz == 0 || (col && val), "tiled_plan: null col/val");
   auto* pl = new (std::nothrow) TiledPlan;
@@ -465,10 +487,9 @@ extern "C" int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* co
     for (int64_t b; (b = next.fetch_add(1)) < pl->n_blocks;) {
       const int64_t r0 = b * rows_per_block, r1 = std::min<int64_t>(n_rows, r0 + rows_per_block);
       for (int64_t k = row_ptr[r0]; k < row_ptr[r1]; ++k)
-        if (col[k] < 0 || (int64_t)col[k] * row_bytes + row_bytes > (int64_t)UINT32_MAX)
-          bad_col = true;
-      build_block(row_ptr, col, val, n_rows, rows_per_block, panel, sub_panel, row_bytes, b,
-                  pl->blocks[b]);
+        if (col[k] < 0) bad_col = true;
+      if (bad_col) continue;
+      build_block(row_ptr, col, val, n_rows, rows_per_block, panel, sub_panel, b, pl->blocks[b]);
     }
   };
   std::vector<std::thread> pool;
@@ -477,48 +498,45 @@ extern "C" int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* co
   for (auto& th : pool) th.join();
   if (bad_col) {
     delete pl;
-    set_error("tiled_plan: a source row lies beyond 4 GB of the table (col * row_bytes)");
+    set_error("tiled_plan: negative column index");
     return GNNREC_EINVAL;
   }
   int64_t tot = 0;
   for (const auto& bp : pl->blocks)
-    for (int w = 0; w < kTiledWaves; ++w) tot += (int64_t)bp.hdr[w].size() / 2;
+    for (int w = 0; w < kTiledWaves; ++w) tot += (int64_t)bp.hdr[w].size() / 4;
   *n_chunks = tot;
   *n_blocks = pl->n_blocks;
   *plan = pl;
   return GNNREC_OK;
 }
 
-extern "C" int gnnrec_tiled_plan_emit(void* plan, uint32_t* xoff, float* val, uint16_t* meta,
-                                      uint32_t* hdr, int64_t* wave_ptr, int32_t* n_steps) {
-  GNNREC_REQUIRE(plan && xoff && val && meta && hdr && wave_ptr && n_steps,
-                 "tiled_emit: null pointer");
+extern "C" int gnnrec_tiled_plan_emit(void* plan, uint32_t* slot, float* val, uint32_t* hdr,
+                                      int64_t* wave_ptr, int32_t* n_steps) {
+  GNNREC_REQUIRE(plan && slot && val && hdr && wave_ptr && n_steps, "tiled_emit: null pointer");
   auto* pl = static_cast<TiledPlan*>(plan);
   const int64_t nb = pl->n_blocks;
   wave_ptr[0] = 0;
   for (int64_t b = 0; b < nb; ++b)
     for (int w = 0; w < kTiledWaves; ++w)
       wave_ptr[b * kTiledWaves + w + 1] =
-          wave_ptr[b * kTiledWaves + w] + (int64_t)pl->blocks[b].hdr[w].size() / 2;
+          wave_ptr[b * kTiledWaves + w] + (int64_t)pl->blocks[b].hdr[w].size() / 4;
   for (int64_t b = 0; b < nb; ++b) {
     const BlockPlan& bp = pl->blocks[b];
     n_steps[b] = bp.nsteps;
     for (int w = 0; w < kTiledWaves; ++w) {
       const int64_t c = wave_ptr[b * kTiledWaves + w];
-      std::copy(bp.xoff[w].begin(), bp.xoff[w].end(), xoff + c * kTiledChunk);
+      std::copy(bp.slot[w].begin(), bp.slot[w].end(), slot + c * kTiledChunk);
       std::copy(bp.val[w].begin(), bp.val[w].end(), val + c * kTiledChunk);
-      std::copy(bp.meta[w].begin(), bp.meta[w].end(), meta + c * kTiledChunk);
-      std::copy(bp.hdr[w].begin(), bp.hdr[w].end(), hdr + 2 * c);
+      std::copy(bp.hdr[w].begin(), bp.hdr[w].end(), hdr + 4 * c);
     }
   }
-  // tail chunks for the last prefetches: harmless slots (row 0 of x, scratch row)
+  // tail chunks for the last prefetches: harmless slots (row 0 of x, row field all ones)
   const int64_t end = wave_ptr[nb * kTiledWaves];
   for (int64_t s = end * kTiledChunk; s < (end + kTiledTail) * kTiledChunk; ++s) {
-    xoff[s] = 0;
+    slot[s] = (uint32_t)kRowMask;
     val[s] = 0.f;
-    meta[s] = (uint16_t)kRowMask;
   }
-  for (int64_t s = 2 * end; s < 2 * (end + kTiledTail); ++s) hdr[s] = 0;
+  for (int64_t s = 4 * end; s < 4 * (end + kTiledTail); ++s) hdr[s] = 0;
   return GNNREC_OK;
 }
 
@@ -546,7 +564,7 @@ int tiled_lds_attribute(int dev) {
 }
 }  // namespace
 
-extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* xoff, const float* val, const uint16_t* meta,
+extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
                                      const uint32_t* hdr, const int64_t* wave_ptr,
                                      const int32_t* n_steps, int64_t n_blocks,
                                      int32_t rows_per_block, const float* x, int64_t x_rows,
@@ -560,8 +578,8 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* xoff, const float* val, con
                  "spmm_tiled: bad rows_per_block");
   GNNREC_REQUIRE(n_rows >= 0 && n_blocks == (n_rows + rows_per_block - 1) / rows_per_block,
                  "spmm_tiled: n_blocks does not match n_rows / rows_per_block");
-  GNNREC_REQUIRE(ldx >= d && x_rows >= 0 && x_rows * ldx * 4 < ((int64_t)1 << 32),
-                 "spmm_tiled: the x table must be under 4 GB with ldx >= d");
+  GNNREC_REQUIRE(ldx >= d && x_rows >= 0 && ldx * 4 <= kMaxRowBytes,
+                 "spmm_tiled: need d <= ldx <= %d", kMaxRowBytes / 4);
   GNNREC_REQUIRE((epi & GNNREC_EPI_NO_Y) || (y && ldy >= d), "spmm_tiled: null y or ldy < d");
   GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_INIT) || (self && ld_self >= d),
                  "spmm_tiled: ACC_INIT needs self");
@@ -569,7 +587,7 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* xoff, const float* val, con
                  "spmm_tiled: ACC needs acc");
   GNNREC_REQUIRE(meet_us >= 0 && meet_us <= 100000, "spmm_tiled: meet_us must be in [0, 1e5]");
   if (n_rows == 0) return GNNREC_OK;
-  GNNREC_REQUIRE(xoff && val && meta && hdr && wave_ptr && n_steps && x && sync,
+  GNNREC_REQUIRE(slot && val && hdr && wave_ptr && n_steps && x && sync,
                  "spmm_tiled: null pointer");
   hipStream_t s = as_hip(stream);
   int dev = 0, cus = 256;
@@ -588,8 +606,9 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* xoff, const float* val, con
   if (hipMemsetAsync(sync, 0, GNNREC_TILED_SYNC_WORDS * sizeof(uint32_t), s) != hipSuccess)
     return check_launch("spmm_tiled (sync reset)");
   hipLaunchKernelGGL(tiled_hop_kernel, dim3((unsigned)grid), dim3(kTiledWaves * 64), lds, s,
-                     xoff, val, meta, hdr, wave_ptr, n_steps, (int)n_blocks, (int)nb_pad,
-                     (int)n_items, (int)rows_per_block, x, (uint32_t)(x_rows * ldx * 4), y, ldy,
+                     slot, val, hdr, wave_ptr, n_steps,
+                     (int)n_blocks, (int)nb_pad, (int)n_items, (int)rows_per_block, x,
+                     (uint64_t)(x_rows * ldx * 4), (uint32_t)(ldx * 4), y, ldy,
                      n_rows, epi, self, ld_self, acc, ld_acc, acc_div, sync,
                      (unsigned)meet_us * 100u /* wall_clock64 runs at 100 MHz */);
   return check_launch("spmm_tiled");

@@ -61,6 +61,7 @@ TILED_MIN_ROWS = 49152
 TILED_MIN_TABLE_BYTES = 32 << 20
 TILED_MAX_DEGREE = 4096
 TILED_MAX_ROWS = _lib.TILED_MAX_ROWS
+TILED_MAX_LDX = _lib.TILED_MAX_LDX
 TILED_BALANCE_PASSES = True
 # bound of the pass-start meeting of an XCD group's workgroups (µs; 0 = no meeting: use when
 # other kernels share the device, e.g. a concurrent exchange)
@@ -79,11 +80,11 @@ def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None):
     """The column-ordered plan spmm_into would use for (adj, x), or None (CSR kernel)."""
     if (not TILED_HOP or x_mask is not None or y_active is not None or x.shape[1] % 32
             or adj.n_rows < max(TILED_MIN_ROWS, 1) or adj.nnz == 0
-            or x.shape[0] * x.stride(0) * 4 >= 1 << 32
+            or x.stride(0) > TILED_MAX_LDX
             or x.shape[0] * x.shape[1] * 4 < TILED_MIN_TABLE_BYTES
             or adj.max_degree() > TILED_MAX_DEGREE):
         return None
-    return adj.tiled_plan(x.stride(0), rows_per_block=_tiled_rows_per_block(adj.n_rows, x.device))
+    return adj.tiled_plan(rows_per_block=_tiled_rows_per_block(adj.n_rows, x.device))
 
 
 def _heavy_args(adj: CsrGraph, x: torch.Tensor, heavy_threshold: int):
@@ -140,13 +141,13 @@ def spmm_tiled_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], p
                     epi: int = 0, self_rows: Optional[torch.Tensor] = None,
                     acc: Optional[torch.Tensor] = None, acc_div: float = 1.0,
                     meet_us: Optional[int] = None) -> None:
-    """spmm_into through the column-ordered kernel with an explicit plan (adj.tiled_plan(ldx)
-    for this x's row stride); same results, bit for bit. The plan's sync words make
+    """spmm_into through the column-ordered kernel with an explicit plan (adj.tiled_plan());
+    same results, bit for bit. The plan's sync words make
     concurrent launches of one plan on different streams unsafe."""
     _require_device(adj, x, y, self_rows, acc)
     d = x.shape[1]
     check(_lib.lib().gnnrec_spmm_tiled_f32(
-        ptr(plan["xoff"]), ptr(plan["val"]), ptr(plan["meta"]), ptr(plan["hdr"]),
+        ptr(plan["slot"]), ptr(plan["val"]), ptr(plan["hdr"]),
         ptr(plan["wave_ptr"]), ptr(plan["n_steps"]), plan["n_blocks"], plan["rows_per_block"],
         ptr(x), x.shape[0], x.stride(0), ptr(y), y.stride(0) if y is not None else d, adj.n_rows,
         d, epi, ptr(self_rows), self_rows.stride(0) if self_rows is not None else d, ptr(acc),

@@ -362,17 +362,17 @@ class CsrGraph:
             self._plans["max_degree"] = int(deg.max()) if deg.numel() else 0
         return self._plans["max_degree"]
 
-    def tiled_plan(self, ldx: int, rows_per_block: int = 1117, panel: int = 49152,
+    def tiled_plan(self, rows_per_block: int = 1117, panel: int = 49152,
                    sub_panel: int = 4096) -> dict:
         """Column-ordered re-layout of this operand for gnnrec_spmm_tiled_f32 (DESIGN.md
-        §3.1c), for x tables with row stride `ldx` (cached per stride; the same plan serves
-        every d <= ldx that is a multiple of 32): built once on the host from the CSR
+        §3.1c), cached; one plan serves every x table (any d that is a multiple of 32, any row
+        stride up to TILED_MAX_LDX, any size): built once on the host from the CSR
         (gnnrec_tiled_plan_build/emit), uploaded to this graph's device. Defaults from the
         G100M sweep (profiles/r02/tiled_sweep.jsonl): 1117 rows per block fill the LDS with
         32-feature accumulators in 14 full passes, 48K-column panels (steps: a workgroup
         barrier each, which keeps its waves on nearby columns), each stream's slots in
         ascending 4K-column sub-panels inside a step (0: no sub-panel order)."""
-        key = ("tiled", int(ldx), int(rows_per_block), int(panel), int(sub_panel))
+        key = ("tiled", int(rows_per_block), int(panel), int(sub_panel))
         if key not in self._plans:
             import ctypes as C
             L = _lib.lib()
@@ -382,33 +382,32 @@ class CsrGraph:
             h, n_chunks, n_blocks = C.c_void_p(), C.c_int64(), C.c_int64()
             _lib.check(L.gnnrec_tiled_plan_build(rp.ctypes.data, col.ctypes.data, val.ctypes.data,
                                                  self.n_rows, int(rows_per_block), int(panel),
-                                                 int(sub_panel), 4 * int(ldx), 0, C.byref(h),
+                                                 int(sub_panel), 0, C.byref(h),
                                                  C.byref(n_chunks),
                                                  C.byref(n_blocks)), "gnnrec_tiled_plan_build")
             nb = n_blocks.value
             chunks = n_chunks.value + _lib.TILED_TAIL          # + tail chunks (prefetch)
-            xoff = np.empty(chunks * _lib.TILED_CHUNK, np.uint32)
+            slot = np.empty(chunks * _lib.TILED_CHUNK, np.uint32)
             v = np.empty(chunks * _lib.TILED_CHUNK, np.float32)
-            meta = np.empty(chunks * _lib.TILED_CHUNK, np.uint16)
-            hdr = np.empty(chunks * 2, np.uint32)
+            hdr = np.empty(chunks * _lib.TILED_HDR_WORDS, np.uint32)
             wave_ptr = np.empty(nb * _lib.TILED_WAVES + 1, np.int64)
             n_steps = np.empty(max(nb, 1), np.int32)
             try:
-                _lib.check(L.gnnrec_tiled_plan_emit(h, xoff.ctypes.data, v.ctypes.data,
-                                                    meta.ctypes.data, hdr.ctypes.data,
-                                                    wave_ptr.ctypes.data, n_steps.ctypes.data),
+                _lib.check(L.gnnrec_tiled_plan_emit(h, slot.ctypes.data, v.ctypes.data,
+                                                    hdr.ctypes.data, wave_ptr.ctypes.data,
+                                                    n_steps.ctypes.data),
                            "gnnrec_tiled_plan_emit")
             finally:
                 L.gnnrec_tiled_plan_free(h)
             dev = self.device
             self._plans[key] = dict(
-                xoff=torch.from_numpy(xoff.view(np.int32)).to(dev),
+                slot=torch.from_numpy(slot.view(np.int32)).to(dev),
                 val=torch.from_numpy(v).to(dev),
-                meta=torch.from_numpy(meta.view(np.int16)).to(dev),
                 hdr=torch.from_numpy(hdr.view(np.int32)).to(dev),
                 wave_ptr=torch.from_numpy(wave_ptr).to(dev),
                 n_steps=torch.from_numpy(n_steps).to(dev),
-                n_blocks=nb, rows_per_block=int(rows_per_block), panel=int(panel),
+                n_blocks=nb, rows_per_block=int(rows_per_block),
+                panel=min(int(panel), _lib.TILED_MAX_PANEL),
                 sub_panel=int(sub_panel), n_chunks=n_chunks.value,
                 n_slots=n_chunks.value * _lib.TILED_CHUNK,
                 sync=torch.zeros(_lib.TILED_SYNC_WORDS, dtype=torch.int32, device=dev))

@@ -137,40 +137,43 @@ int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col, const
  * neighbour in ascending column order: bit-exact.
  *
  * The operand is re-laid out once on the host from the CSR (gnnrec_tiled_plan_build, then
- * gnnrec_tiled_plan_emit into caller buffers, then gnnrec_tiled_plan_free); the plan does not
- * depend on d. Per (block, wave) the plan is a run of chunks; a chunk is GNNREC_TILED_CHUNK
- * slots, the first half for lanes 0-31, the second for lanes 32-63 (a slot stream each); slot
- * = xoff (byte offset col * row_bytes of the source row), val, meta (uint16 local row; row
- * rows_per_block = a padding slot); per chunk hdr[2] = {step barriers before the chunk, chain
- * mask: bit t (first half) / 16 + t (second half) = slot t continues slot t-1's row}. Inside
- * a half, a row appears in each group of 8 slots as at most one run of consecutive slots.
- * Slot arrays hold (n_chunks + GNNREC_TILED_TAIL) * GNNREC_TILED_CHUNK entries, hdr 2 *
- * (n_chunks + GNNREC_TILED_TAIL) (tail chunks read by the last prefetches); wave_ptr
- * [n_blocks * GNNREC_TILED_WAVES + 1] are chunk offsets; n_steps [n_blocks]. rows_per_block
- * <= GNNREC_TILED_MAX_ROWS. gnnrec_spmm_tiled_f32 needs d % 32 == 0, ldx * 4 == the plan's
- * row_bytes, x_rows * ldx * 4 < 2^32, `sync`: a device scratch of GNNREC_TILED_SYNC_WORDS
- * uint32 (zeroed per call), and meet_us: the bound of the pass-start meeting in microseconds
- * (0: no meeting — e.g. when other kernels share the device). */
+ * gnnrec_tiled_plan_emit into caller buffers, then gnnrec_tiled_plan_free); the plan depends
+ * on neither d nor the x table's stride. Per (block, wave) the plan is a run of chunks; a
+ * chunk is GNNREC_TILED_CHUNK slots, the first half for lanes 0-31, the second for lanes 32-63
+ * (a slot stream each); a slot is one uint32 word ((col - panel base) << 11 | local row; row
+ * rows_per_block = a padding slot) and one fp32 value; per chunk hdr[4] = {step barriers
+ * before the chunk, chain mask: bit t (first half) / 16 + t (second half) = slot t continues
+ * slot t-1's row, panel base column (every slot of a chunk lies in one panel of at most 2^20
+ * columns), 0}. Inside a half, a row appears in each group of 8 slots as at most one run of
+ * consecutive slots. Slot arrays hold (n_chunks + GNNREC_TILED_TAIL) * GNNREC_TILED_CHUNK
+ * entries, hdr 4 * (n_chunks + GNNREC_TILED_TAIL) (tail chunks read by the last prefetches);
+ * wave_ptr [n_blocks * GNNREC_TILED_WAVES + 1] are chunk offsets; n_steps [n_blocks].
+ * rows_per_block <= GNNREC_TILED_MAX_ROWS. gnnrec_spmm_tiled_f32 needs d % 32 == 0,
+ * d <= ldx <= GNNREC_TILED_MAX_LDX (any table size), `sync`: a device scratch of
+ * GNNREC_TILED_SYNC_WORDS uint32 (zeroed per call), and meet_us: the bound of the pass-start
+ * meeting in microseconds (0: no meeting — e.g. when other kernels share the device). */
 #define GNNREC_TILED_WAVES 16
 #define GNNREC_TILED_CHUNK 32
 #define GNNREC_TILED_TAIL 2
 #define GNNREC_TILED_MAX_ROWS 1279
 #define GNNREC_TILED_SYNC_WORDS 256
+#define GNNREC_TILED_HDR_WORDS 4
+#define GNNREC_TILED_MAX_LDX 1024
 
 int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* col, const float* val,
                             int64_t n_rows, int32_t rows_per_block, int32_t panel,
-                            int32_t sub_panel, int64_t row_bytes, int32_t n_threads, void** plan,
+                            int32_t sub_panel, int32_t n_threads, void** plan,
                             int64_t* n_chunks, int64_t* n_blocks);
-int gnnrec_tiled_plan_emit(void* plan, uint32_t* xoff, float* val, uint16_t* meta,
-                           uint32_t* hdr, int64_t* wave_ptr, int32_t* n_steps);
+int gnnrec_tiled_plan_emit(void* plan, uint32_t* slot, float* val, uint32_t* hdr,
+                           int64_t* wave_ptr, int32_t* n_steps);
 int gnnrec_tiled_plan_free(void* plan);
 
-int gnnrec_spmm_tiled_f32(const uint32_t* xoff, const float* val, const uint16_t* meta,
-                          const uint32_t* hdr, const int64_t* wave_ptr, const int32_t* n_steps,
-                          int64_t n_blocks, int32_t rows_per_block, const float* x,
-                          int64_t x_rows, int64_t ldx, float* y, int64_t ldy, int64_t n_rows,
-                          int32_t d, int32_t epi, const float* self, int64_t ld_self, float* acc,
-                          int64_t ld_acc, float acc_div, uint32_t* sync, int32_t meet_us,
+int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val, const uint32_t* hdr,
+                          const int64_t* wave_ptr, const int32_t* n_steps, int64_t n_blocks,
+                          int32_t rows_per_block, const float* x, int64_t x_rows, int64_t ldx,
+                          float* y, int64_t ldy, int64_t n_rows, int32_t d, int32_t epi,
+                          const float* self, int64_t ld_self, float* acc, int64_t ld_acc,
+                          float acc_div, uint32_t* sync, int32_t meet_us,
                           gnnrec_stream_t stream);
 
 int gnnrec_row_nonzero_f32(const float* x, int64_t ldx, int64_t n_rows, int32_t d,

@@ -384,7 +384,7 @@ def test_spmm_tiled_bit_exact(cuda, R, panel, d):
     x = torch.randn(g.shape[0], d, generator=torch.Generator().manual_seed(R)) * 0.1
     ref = bits(oracle.spmm(rp, col, val, x.numpy()))
     xd = x.to(cuda)
-    plan = g.tiled_plan(d, rows_per_block=R, panel=panel)
+    plan = g.tiled_plan(rows_per_block=R, panel=panel)
     y = torch.full((g.shape[0], d), float("nan"), device=cuda)
     F.spmm_tiled_into(g, xd, y, plan)
     np.testing.assert_array_equal(bits(y.cpu().numpy()), ref)
@@ -403,7 +403,7 @@ def test_spmm_tiled_epilogues_strides_and_empty_rows(cuda):
     x = big[:, 16:80]                                    # ldx = 96
     xs = x.contiguous().cpu().numpy()
     yr = oracle.spmm(rp, col, val, xs)
-    plan = g.tiled_plan(96, rows_per_block=100, panel=512)
+    plan = g.tiled_plan(rows_per_block=100, panel=512)
     acc = torch.empty(n, 64, device=cuda)
     y = torch.full((n, 128), 7.0, device=cuda)
     F.spmm_tiled_into(g, x, y[:, 32:96], plan, epi=_lib.EPI_ACC_INIT, self_rows=x, acc=acc)
@@ -419,7 +419,7 @@ def test_spmm_tiled_epilogues_strides_and_empty_rows(cuda):
 
 def test_spmm_tiled_rejects_bad_arguments(cuda):
     g, _ = random_graph(300, 200, 2000, 1, cuda)
-    plan = g.tiled_plan(48)
+    plan = g.tiled_plan()
     x = torch.zeros(g.shape[0], 48, device=cuda)
     with pytest.raises(ValueError, match="multiple of 32"):
         F.spmm_tiled_into(g, x, torch.empty_like(x), plan)
@@ -427,6 +427,32 @@ def test_spmm_tiled_rejects_bad_arguments(cuda):
     with pytest.raises(ValueError, match="meet_us"):
         F.spmm_tiled_into(g, x[:, :32], torch.empty(g.shape[0], 32, device=cuda), plan,
                           meet_us=-1)
+    wide = torch.zeros(g.shape[0], _lib.TILED_MAX_LDX + 32, device=cuda)[:, :32]
+    with pytest.raises(ValueError, match="ldx"):
+        F.spmm_tiled_into(g, wide, torch.empty(g.shape[0], 32, device=cuda), plan)
+
+
+def test_spmm_tiled_table_over_4gb(cuda):
+    """Gathers beyond the first 4 GB of the x table: each chunk's buffer is based at its
+    panel's first source row, so lane offsets stay 32-bit (4.6 GB table, ldx = 1024)."""
+    n_users, n_items = 1000, 1_130_000
+    rng = np.random.default_rng(11)
+    u = rng.integers(0, n_users, 40000)
+    i = np.concatenate([rng.integers(0, n_items, 30000),
+                        rng.integers(n_items - 100_000, n_items, 10000)])   # rows > 4 GB
+    g = CsrGraph.from_interactions(u, i, n_users, n_items).to(cuda)
+    n = g.shape[0]
+    big = torch.empty(n, _lib.TILED_MAX_LDX, device=cuda)
+    assert big.numel() * 4 > 1 << 32
+    x = big[:, 64:128]
+    x.copy_(torch.randn(n, 64, device=cuda, generator=torch.Generator(cuda).manual_seed(3)))
+    rp, col, val = g.row_ptr.cpu().numpy(), g.col.cpu().numpy(), g.val.cpu().numpy()
+    ref = bits(oracle.spmm(rp, col, val, x.cpu().numpy()))
+    plan = g.tiled_plan(rows_per_block=500, panel=49152)
+    y = torch.full((n, 64), float("nan"), device=cuda)
+    F.spmm_tiled_into(g, x, y, plan)
+    np.testing.assert_array_equal(bits(y.cpu().numpy()), ref)
+    del big
 
 
 def test_lightgcn_through_tiled_hop_is_bit_exact(cuda, monkeypatch):

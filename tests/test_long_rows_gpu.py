@@ -66,7 +66,7 @@ def test_tiled_hops_bit_exact(case, rows_per_block):
     """The column-ordered kernel (forced: the operand is below TILED_MIN_ROWS) with the layer
     mean fused as in the headline path."""
     f, g, x0, _, _ = case
-    plan = g.tiled_plan(x0.stride(0), rows_per_block=rows_per_block)
+    plan = g.tiled_plan(rows_per_block=rows_per_block)
     acc = torch.empty_like(x0)
     hops, x = [], x0
     for k in range(1, 4):

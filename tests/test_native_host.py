@@ -98,15 +98,16 @@ def test_partition_covers_rows_and_remaps_columns(world):
         np.testing.assert_array_equal(glob, G.col.numpy()[k0:k0 + s.nnz])
 
 
-def _walk_tiled_plan(plan, n_rows, R, row_bytes=256):
+def _walk_tiled_plan(plan, n_rows, R):
     """Replay gnnrec_spmm_tiled_f32's schedule on the host: per row, the (col, val) sequence
     its accumulator receives, in kernel order; checks the plan's structural rules on the way
-    (include/gnnrec.h: chunks of two 16-slot halves, per-chunk {barriers, chain mask}; a row
-    at most one run per group of 8 slots of a half)."""
-    xo = plan["xoff"].numpy().view(np.uint32)
+    (include/gnnrec.h: chunks of two 16-slot halves, per-chunk {barriers, chain mask, panel
+    base, 0}; slot word = (col - base) << 11 | row; a row at most one run per group of 8
+    slots of a half; every slot of a chunk inside its panel)."""
+    sw = plan["slot"].numpy().view(np.uint32)
     val = plan["val"].numpy()
-    meta = plan["meta"].numpy().view(np.uint16)
     hdr = plan["hdr"].numpy().view(np.uint32)
+    panel = plan["panel"]
     wp = plan["wave_ptr"].numpy()
     ns = plan["n_steps"].numpy()
     W, CH, H, GR = _lib.TILED_WAVES, _lib.TILED_CHUNK, _lib.TILED_CHUNK // 2, 8
@@ -117,11 +118,13 @@ def _walk_tiled_plan(plan, n_rows, R, row_bytes=256):
         for w in range(W):
             cur = 0
             for c in range(wp[b * W + w], wp[b * W + w + 1]):
-                cur += int(hdr[2 * c])
-                cm = int(hdr[2 * c + 1])
+                cur += int(hdr[4 * c])
+                cm = int(hdr[4 * c + 1])
+                pbase = int(hdr[4 * c + 2])
+                assert pbase % panel == 0 and hdr[4 * c + 3] == 0
                 for h in range(2):
                     base = c * CH + h * H
-                    rows = [int(meta[base + t]) & 2047 for t in range(H)]
+                    rows = [int(sw[base + t]) & 2047 for t in range(H)]
                     for g0 in range(0, H, GR):
                         grp = rows[g0:g0 + GR]
                         runs = [r for t, r in enumerate(grp)
@@ -136,9 +139,9 @@ def _walk_tiled_plan(plan, n_rows, R, row_bytes=256):
                         assert row < R
                         assert chain == (1 if (t > 0 and rows[t - 1] == row) else 0)
                         assert owner.setdefault((cur, row), (w, h)) == (w, h)
-                        assert xo[base + t] % row_bytes == 0
-                        events.append((cur, base + t, row, int(xo[base + t]) // row_bytes,
-                                       val[base + t]))
+                        rel = int(sw[base + t]) >> 11
+                        assert rel < panel
+                        events.append((cur, base + t, row, pbase + rel, val[base + t]))
             assert cur <= max(ns[b] - 1, 0)
         events.sort(key=lambda e: (e[0], e[1]))
         for _, _, row, col, v in events:
@@ -158,12 +161,12 @@ def test_tiled_plan_preserves_every_row_chain(R, panel, sub):
     u = np.concatenate([rng.integers(0, 700, 6000), np.zeros(300, np.int64)])  # a long row
     i = np.concatenate([rng.integers(0, 900, 6000), np.arange(300)])
     G = CsrGraph.from_interactions(u, i, 701, 900)     # user 700: an empty row
-    plan = G.tiled_plan(64, rows_per_block=R, panel=panel, sub_panel=sub)
+    plan = G.tiled_plan(rows_per_block=R, panel=panel, sub_panel=sub)
     n = G.shape[0]
     assert plan["n_blocks"] == (n + R - 1) // R
     assert plan["n_slots"] >= G.nnz
-    assert plan["xoff"].numel() == (plan["n_chunks"] + _lib.TILED_TAIL) * _lib.TILED_CHUNK
-    assert plan["hdr"].numel() == 2 * (plan["n_chunks"] + _lib.TILED_TAIL)
+    assert plan["slot"].numel() == (plan["n_chunks"] + _lib.TILED_TAIL) * _lib.TILED_CHUNK
+    assert plan["hdr"].numel() == 4 * (plan["n_chunks"] + _lib.TILED_TAIL)
     seq = _walk_tiled_plan(plan, n, R)
     rp, col, val = G.row_ptr.numpy(), G.col.numpy(), G.val.numpy()
     for r in range(n):
@@ -173,10 +176,20 @@ def test_tiled_plan_preserves_every_row_chain(R, panel, sub):
                                       val[rp[r]:rp[r + 1]])
 
 
-def test_tiled_plan_rejects_tables_over_4gb():
-    G = CsrGraph.from_interactions([0, 1], [0, 1], 2, 2)
-    with pytest.raises(ValueError, match="4 GB"):
-        G.tiled_plan(1 << 30)
+def test_tiled_plan_clamps_panels_to_the_slot_word():
+    """A slot word holds 20 bits of column offset from its panel's base: wider panels are cut
+    to 2^20 columns, and the chains are still exact across the cut."""
+    n_users, n_items = 3, (1 << 20) + 50
+    u = np.array([0, 0, 0, 1, 2, 2])
+    i = np.array([1, (1 << 20) - 1, (1 << 20) + 40, 5, (1 << 20) + 1, 7])
+    G = CsrGraph.from_interactions(u, i, n_users, n_items)
+    plan = G.tiled_plan(rows_per_block=8, panel=1 << 30, sub_panel=0)
+    assert plan["panel"] == 1 << 20
+    n = G.shape[0]
+    seq = _walk_tiled_plan(plan, n, 8)
+    rp, col = G.row_ptr.numpy(), G.col.numpy()
+    for r in range(n):
+        assert [c for c, _ in seq[r]] == col[rp[r]:rp[r + 1]].tolist(), r
 
 
 def test_heavy_row_plan_segments_cover_heavy_rows():

@@ -41,7 +41,7 @@ for n in sizes:
     F.TILED_HOP = False
     t_csr = timed(lambda: F.spmm_into(s, x, y1))
     R = F._tiled_rows_per_block(n, dev)
-    plan = s.tiled_plan(64, rows_per_block=R)
+    plan = s.tiled_plan(rows_per_block=R)
     t_tiled = timed(lambda: F.spmm_tiled_into(s, x, y2, plan))
     t_tiled0 = timed(lambda: F.spmm_tiled_into(s, x, y2, plan, meet_us=0))
     print(json.dumps({"rows": n, "nnz": s.nnz, "R": R, "csr_ms": t_csr, "tiled_ms": t_tiled,

@@ -40,11 +40,16 @@ for spec in args:
     R, panel, sub, *rest = (int(v) for v in spec.split(":"))
     meet = rest[0] if rest else F.TILED_MEET_US
     t0 = time.time()
-    plan = g.tiled_plan(LDX, rows_per_block=R, panel=panel, sub_panel=sub)
+    plan = g.tiled_plan(rows_per_block=R, panel=panel, sub_panel=sub)
     t_plan = time.time() - t0
     if FOLD:
         plan = dict(plan)
-        plan["xoff"] = torch.remainder(plan["xoff"].long() & 0xFFFFFFFF, FOLD).int()
+        rows = FOLD // (4 * LDX)     # slot words re-pointed into the first FOLD bytes
+        w = plan["slot"].long() & 0xFFFFFFFF
+        plan["slot"] = ((torch.remainder(w >> 11, rows) << 11) | (w & 2047)).int()
+        hdr = plan["hdr"].clone().view(-1, 4)
+        hdr[:, 2] = 0
+        plan["hdr"] = hdr.view(-1)
     times = []
     for _ in range(12):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -60,5 +65,5 @@ for spec in args:
                       "pad": plan["n_slots"] / g.nnz - 1, "ms_median": times[len(times) // 2],
                       "ms_min": times[0], "bit_exact": exact, "plan_s": round(t_plan, 1)}),
           flush=True)
-    g._plans.pop(("tiled", LDX, R, panel, sub), None)
+    g._plans.pop(("tiled", R, panel, sub), None)
     del plan

@@ -55,7 +55,7 @@ def main(specs):
     for spec in specs:
         R, panel, sub, *rest = (int(v) for v in spec.split(":"))
         meet = rest[0] if rest else F.TILED_MEET_US
-        plan = g.tiled_plan(64, rows_per_block=R, panel=panel, sub_panel=sub)
+        plan = g.tiled_plan(rows_per_block=R, panel=panel, sub_panel=sub)
         assert L.gnnrec_debug_tiled_trace(0) == 0
         F.spmm_tiled_into(g, x, y, plan, meet_us=meet)
         buf.zero_()
