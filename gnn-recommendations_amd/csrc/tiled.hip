@@ -48,7 +48,10 @@ constexpr int kRowMask = (1 << kRowBits) - 1;
 constexpr int kMaxPanel = 1 << 20;                // columns per panel (slot word: 21 bits)
 constexpr int kMaxRowBytes = GNNREC_TILED_MAX_LDX * 4;   // keeps the lane offset 32-bit
 constexpr int kGroup = 8;                         // steps whose reads precede their writes
-constexpr int kEpiBatch = 8;                      // epilogue rows per wave with loads in flight
+#ifndef GNNREC_TILED_EPI_BATCH
+#define GNNREC_TILED_EPI_BATCH 20
+#endif
+constexpr int kEpiBatch = GNNREC_TILED_EPI_BATCH;   // epilogue rows per half-wave, loads in flight
 static_assert(kHalf == 16, "a half-chunk is one DPP row of 16 lanes");
 static_assert(kHalf == 2 * kGroup, "a half-chunk is applied as two groups");
 static_assert(GNNREC_TILED_MAX_ROWS < kRowMask, "row field is 11 bits (row R = scratch)");
@@ -120,6 +123,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const char* xs, uin
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(xs) + off, 0, (int)n, 0x00020000);
 }
 
+// Rows [r0, r0 + rows) of a row-major fp32 table (row stride ld), from column slice * 32: the
+// range ends right after the last row's slice, so offsets of later rows are out of range.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* p, int64_t r0,
+                                                            int64_t ld, int slice, int rows) {
+  const float* b = p ? p + r0 * ld + (int64_t)slice * kSlice : p;
+  const uint32_t n = p ? (uint32_t)(rows - 1) * (uint32_t)ld * 4u + kSlice * 4u : 0u;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(b), 0, (int)n, 0x00020000);
+}
+
 template <int... T>
 __device__ __forceinline__ void tiled_gather(std::integer_sequence<int, T...>,
                                              __amdgpu_buffer_rsrc_t xr, uint32_t f4,
@@ -173,6 +185,50 @@ __device__ __forceinline__ void tiled_apply(float* acc, uint32_t f4, const Tiled
   float prev = 0.f;
   tiled_apply8<0>(k8, base, f4, m, x, cm, prev);
   tiled_apply8<kGroup>(k8, base, f4, m, x, cm, prev);
+}
+
+// Pass-end epilogue of one half-wave: its rows i = rl + 32q of the block (rl = 2 * wave +
+// half), kEpiBatch at a time with every load of a batch issued before the first use. All
+// offsets are 32-bit rows of buffers based at the block's first row whose ranges end at the
+// last valid row: loads past it return 0 and stores are dropped, so there is no branch (a
+// branch around a load makes the compiler wait for it in place). A null ry: no y output.
+// ACC: acc_out = (base + y) [/ div] with base = x0 (ACC_INIT) or the running sum.
+template <bool ACC>
+__device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, uint32_t f4,
+                                               __amdgpu_buffer_rsrc_t ry, uint32_t ly,
+                                               __amdgpu_buffer_rsrc_t rb, uint32_t lb,
+                                               __amdgpu_buffer_rsrc_t ra, uint32_t la,
+                                               bool div, float acc_div) {
+  constexpr int kStride = 2 * kTiledWaves;
+  for (int i0 = rl; i0 - (rl & 1) < R; i0 += kStride * kEpiBatch) {
+    // per-row offsets advance by a stride; the opaque copy keeps the compiler from hoisting
+    // kEpiBatch x 3 of them out of the persistent loop (they would spill)
+    uint32_t ol = (uint32_t)i0, ob = (uint32_t)i0 * lb + f4;
+    asm volatile("" : "+v"(ol), "+v"(ob));
+    float a[kEpiBatch], base[kEpiBatch];
+#pragma unroll
+    for (int q = 0; q < kEpiBatch; ++q) {
+      a[q] = acc[min(ol, (uint32_t)R) * kSlice + (f4 >> 2)];
+      ol += kStride;
+      if (ACC) {
+        base[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, ob, 0, 0));
+        ob += kStride * lb;
+      }
+    }
+    uint32_t oy = (uint32_t)i0 * ly + f4, oa = (uint32_t)i0 * la + f4;
+    asm volatile("" : "+v"(oy), "+v"(oa));
+#pragma unroll
+    for (int q = 0; q < kEpiBatch; ++q) {
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, a[q]), ry, oy, 0, 0);
+      oy += kStride * ly;
+      if (ACC) {
+        float bsum = base[q] + a[q];
+        if (div) bsum = bsum / acc_div;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, bsum), ra, oa, 0, 0);
+        oa += kStride * la;
+      }
+    }
+  }
 }
 
 __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
@@ -255,36 +311,22 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
       __syncthreads();
       GNNREC_TILED_STAMP(ev);
     }
-    // epilogue: a wave's rows in batches of kEpiBatch, every load of a batch issued before
-    // the first use (one memory latency per batch, not per row)
+    // epilogue: half-wave h of wave w owns rows i = 2w + h + 32q (see tiled_epilogue)
     const int64_t r0 = (int64_t)blk * R;
-    const int64_t cf = (int64_t)slice * kSlice + f;
-    const bool acc_on = (epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) != 0;
-    const float* base_src = (epi & GNNREC_EPI_ACC_INIT) ? self : accg;
-    const int64_t ld_base = (epi & GNNREC_EPI_ACC_INIT) ? ld_self : ld_acc;
-    constexpr int kStride = 2 * kTiledWaves;
-    for (int i0 = 2 * w + half; i0 < R; i0 += kStride * kEpiBatch) {
-      float a[kEpiBatch], base[kEpiBatch];
-#pragma unroll
-      for (int q = 0; q < kEpiBatch; ++q) {
-        const int i = i0 + q * kStride;
-        const int64_t r = r0 + i;
-        const bool ok = i < R && r < n_rows;
-        a[q] = ok ? acc[i * kSlice + f] : 0.f;
-        base[q] = (ok && acc_on) ? base_src[r * ld_base + cf] : 0.f;
-      }
-#pragma unroll
-      for (int q = 0; q < kEpiBatch; ++q) {
-        const int i = i0 + q * kStride;
-        const int64_t r = r0 + i;
-        if (i >= R || r >= n_rows) break;
-        if (!(epi & GNNREC_EPI_NO_Y)) y[r * ldy + cf] = a[q];
-        if (acc_on) {
-          float bsum = base[q] + a[q];
-          if (epi & GNNREC_EPI_ACC_DIV) bsum = bsum / acc_div;
-          accg[r * ld_acc + cf] = bsum;
-        }
-      }
+    const int nv = (int)min((int64_t)R, n_rows - r0);
+    const int rl = 2 * w + half;
+    const __amdgpu_buffer_rsrc_t ry = rows_rsrc((epi & GNNREC_EPI_NO_Y) ? nullptr : y, r0, ldy,
+                                                slice, nv);
+    if (epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) {
+      const bool init = (epi & GNNREC_EPI_ACC_INIT) != 0;
+      const float* bsrc = init ? self : accg;
+      const int64_t ldb = init ? ld_self : ld_acc;
+      tiled_epilogue<true>(acc, R, rl, f4, ry, (uint32_t)ldy * 4,
+                           rows_rsrc(bsrc, r0, ldb, slice, nv), (uint32_t)ldb * 4,
+                           rows_rsrc(accg, r0, ld_acc, slice, nv), (uint32_t)ld_acc * 4,
+                           (epi & GNNREC_EPI_ACC_DIV) != 0, acc_div);
+    } else {
+      tiled_epilogue<false>(acc, R, rl, f4, ry, (uint32_t)ldy * 4, ry, 0, ry, 0, false, 1.f);
     }
     __syncthreads();
   }
@@ -586,6 +628,10 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
   GNNREC_REQUIRE(!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) || (acc && ld_acc >= d),
                  "spmm_tiled: ACC needs acc");
   GNNREC_REQUIRE(meet_us >= 0 && meet_us <= 100000, "spmm_tiled: meet_us must be in [0, 1e5]");
+  constexpr int64_t kMaxLd = ((int64_t)1 << 32) / (4 * 4096);   // epilogue row offsets: 32-bit
+  GNNREC_REQUIRE(ldy <= kMaxLd && ld_self <= kMaxLd && ld_acc <= kMaxLd,
+                 "spmm_tiled: output / self / acc row strides must be <= %lld",
+                 (long long)kMaxLd);
   if (n_rows == 0) return GNNREC_OK;
   GNNREC_REQUIRE(slot && val && hdr && wave_ptr && n_steps && x && sync,
                  "spmm_tiled: null pointer");
