@@ -202,15 +202,19 @@ def lightgcn_backward(adj: CsrGraph, g: torch.Tensor, n_layers: int,
                       masked_hops: Optional[int] = None, active_hops: int = 1) -> torch.Tensor:
     """d/dx0 of mean_k A^k x0 applied to g: mean_k (A^T)^k g — the same launches and epilogue
     order as lightgcn_forward over A^T (so the same bits). The BPR gradient touches a few
-    thousand rows, so the first `masked_hops` hops (default K-1) skip the all-zero rows of
-    their input, and the first `active_hops` also skip the output rows no non-zero row reaches.
-    G100M, batch 2048 (tools/exp_masked.py): hop 1 1.9 ms masked+active vs 7.0 dense; hop 2
-    (a quarter of the rows live) 5.9 ms masked, 6.0 + 0.4 (marking) masked+active."""
+    thousand rows, so the first `masked_hops` hops skip the all-zero rows of their input, and
+    the first `active_hops` also skip the output rows no non-zero row reaches. G100M, batch
+    2048 (tools/exp_masked.py): hop 1 1.9 ms masked+active vs 7.0 dense (row-parallel); hop 2
+    (a quarter of the rows live) 5.9 ms masked, 6.0 + 0.4 (marking) masked+active, but 4.2 ms
+    dense through the column-ordered kernel. Default: only hop 1 masked where that kernel
+    takes the operand, K-1 hops otherwise (a skipped row adds fmaf(v, 0, acc) = acc: the
+    same bits as the dense hop, which is the reference's own arithmetic)."""
     at = adj.t()
     g = g.contiguous()
     _require_device(at, g)
     K = int(n_layers)
-    masked_hops = K - 1 if masked_hops is None else masked_hops
+    if masked_hops is None:
+        masked_hops = 1 if tiled_plan_for(at, g) is not None else K - 1
 
     def masks(k, x_in):
         if k > masked_hops:

@@ -113,11 +113,13 @@ def lightgcn_train_step_dist(dg: DistributedGraph, emb_local: torch.nn.Parameter
         # index_add_'s atomics: repeated batch rows sum in a fixed order
         dy.index_put_((ids[mine] - b0,), rb.grad[mine], accumulate=True)
         bwd_masks = None
-        if native:   # hops 1..K-1 skip the zero rows; hop 1 also the rows none reaches
-            from ..ops.functional import row_nonzero
+        if native:   # hop 1 skips the zero rows and the rows none reaches; hops 2..K-1 skip
+            # the zero rows unless the column-ordered kernel takes the shard (its dense hop is
+            # faster there: ops.functional.lightgcn_backward)
+            from ..ops.functional import row_nonzero, tiled_plan_for
 
             def bwd_masks(k, x_in):
-                if k >= K:
+                if k >= K or (k > 1 and tiled_plan_for(dg.shard, x_in) is not None):
                     return None
                 xm = row_nonzero(x_in)
                 ya = dg.local_slice(_reach(dg, dg.local_slice(xm))) if k == 1 else None
