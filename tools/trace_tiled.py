@@ -73,7 +73,14 @@ def main(specs):
         n_ev = int((t[0] > 0).sum())
         passes = n_ev // per_pass
         t0 = t[t > 0].min()
-        spreads, steps, meets = [], [], []
+        spreads, steps, meets, trans, first = [], [], [], [], []
+        for blk in range(grid):   # per block: pass transition and first step of a pass
+            nsb = int(plan["n_steps"][blk].item())
+            for p in range(passes - 1):
+                last, nxt = t[blk, p * per_pass + nsb], t[blk, (p + 1) * per_pass]
+                if nsb == ns and last > 0 and nxt > 0:
+                    trans.append(int(nxt - last))
+                    first.append(int(t[blk, (p + 1) * per_pass + 1] - nxt))
         for grp in range(8):
             blocks = list(range(grp, grid, 8))
             for p in range(passes):
@@ -91,6 +98,9 @@ def main(specs):
                "group_spread_at_step_us_median": float(np.median(spreads)) / 100,
                "group_spread_at_step_us_p90": float(np.percentile(spreads, 90)) / 100,
                "group_spread_at_pass_start_us_median": float(np.median(meets)) / 100,
+               # last step barrier of a pass -> next pass start (epilogue, meeting, zeroing)
+               "pass_transition_us_median": float(np.median(trans)) / 100 if trans else None,
+               "first_step_us_median": float(np.median(first)) / 100 if first else None,
                "kernel_span_us": float(t[t > 0].max() - t0) / 100}
         print(json.dumps(res), flush=True)
         np.save(ROOT / "gpurun_out" / f"trace_{R}_{panel}_{sub}_{meet}.npy", t)
