@@ -346,13 +346,15 @@ class CsrGraph:
         return self._plans[key]
 
     def heavy_rows(self, threshold: int) -> Optional[torch.Tensor]:
-        """int64 ids of the rows with more than `threshold` neighbours on this device, or None
-        (cached): the SpMM's workgroup-per-row bucket."""
+        """int64 ids of the rows with more than `threshold` neighbours on this device, longest
+        first (they start first and finish last), or None (cached): the SpMM's
+        workgroup-per-row bucket."""
         key = ("heavy_rows", threshold)
         if key not in self._plans:
             deg = self.row_ptr[1:] - self.row_ptr[:-1]
-            rows = torch.nonzero(deg > threshold).flatten().to(torch.int64).contiguous()
-            self._plans[key] = rows if rows.numel() else None
+            rows = torch.nonzero(deg > threshold).flatten().to(torch.int64)
+            rows = rows[torch.argsort(deg[rows], descending=True, stable=True)]
+            self._plans[key] = rows.contiguous() if rows.numel() else None
         return self._plans[key]
 
     def max_degree(self) -> int:
