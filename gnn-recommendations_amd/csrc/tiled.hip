@@ -19,13 +19,15 @@
 // sweeps of the same plan; the work items are (slice, block) pairs, slice-major.
 //
 // The two 32-lane halves of a wave take two slot streams (lane = half * 32 + feature). A chunk
-// holds 16 slots per half. Every lane loads ITS slot's (offset, value, row) once per chunk
-// (lane l: slot (l / 32, l % 16)) and step t broadcasts slot t of each half to that half with
-// DPP row_newbcast:t (a 16-lane row reads its lane t), fused into the address add where the
-// compiler can; per-chunk header words (scalar loads) carry the step barriers and the chain
-// mask (slot t continues slot t-1's row in the same half: take the register value, not LDS).
-// Pipeline per wave: chunk c+2's slot loads, chunk c+1's gathers and chunk c's LDS
-// read-fmaf-write in flight together.
+// holds 16 slots per half. Every lane loads ITS slot's word (column offset from the chunk's
+// panel base | local row), value and one word of the chunk header once per chunk (lane l:
+// slot (l / 32, l % 16)), and step t broadcasts slot t of each half to that half with DPP
+// row_newbcast:t (a 16-lane row reads its lane t), fused into the address add where the
+// compiler can; the header words (v_readlane) carry the step barriers, the chain mask (slot t
+// continues slot t-1's row in the same half: take the register value, not LDS) and the panel
+// base the chunk's buffer resource starts at. Pipeline per wave: chunk c+2's slot loads,
+// chunk c+1's gathers and chunk c's LDS read-fmaf-write in flight together. What bounds it:
+// the per-CU L1 miss path (one L2 request per gathered 128-B line).
 #include <algorithm>
 #include <atomic>
 #include <mutex>
