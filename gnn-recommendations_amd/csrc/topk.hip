@@ -12,8 +12,9 @@
 //   * seen items are masked lazily: only a candidate that would enter the list is looked up,
 //     through a per-user cursor into its sorted seen list that only moves forward (the
 //     candidates of a user arrive in ascending item order), and, if seen, re-scored as -inf.
-// Workgroup = 4 waves = 64 users (16 per wave); item tiles of 64 rows are staged in LDS
-// ([64][d+2]: d+2 == 2 mod 32 makes the B-fragment reads conflict-free) and reused by the
+// Workgroup = 4 waves = 64 * UF users (16 * UF per wave: UF user fragments share every B
+// fragment a wave reads, UF MFMA chains per item block); item tiles of 64 rows are staged in
+// LDS ([64][d+2]: d+2 == 2 mod 32 makes the B-fragment reads conflict-free) and reused by the
 // four waves.
 #include <math.h>
 
@@ -72,12 +73,14 @@ __device__ __forceinline__ void heap_replace_root(float* hs, int* hi, float cs, 
   hi[pos] = ci;
 }
 
-template <int D, int KM>
+template <int D, int KM, int UF>
 __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
   constexpr int STEPS = D / 4;
   constexpr int TI = D <= 128 ? 64 : 32;  // items per LDS tile
   constexpr int LDV = D + 2;
-  constexpr int UPB = 64;      // users per workgroup
+  constexpr int UPW = 16 * UF;  // users per wave
+  constexpr int UPB = 4 * UPW;  // users per workgroup
+  static_assert(UF * 4 * (TI / 16) <= 32, "candidate mask bits");
   constexpr int PIECES = TI * (D / 4) / kBlock;  // float4 per thread per tile
   __shared__ __attribute__((aligned(16))) float v_lds[2][TI * LDV];
   __shared__ float l_score[UPB][KM];
@@ -88,16 +91,19 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int i16 = lane & 15, k4 = lane >> 4;
   const int64_t ub = (int64_t)blockIdx.x * UPB;
+  const int wu = UPW * wave;   // this wave's first user in the workgroup
   // this workgroup's item range (a multiple of TI, so tiles never straddle two ranges)
   const int64_t per = ((p.n_items + p.n_split - 1) / p.n_split + TI - 1) / TI * TI;
   const int64_t i_beg = (int64_t)blockIdx.y * per;
   const int64_t i_end = min<int64_t>(p.n_items, i_beg + per);
-  // A fragments: this wave's 16 users, k = 4s + k4 (ascending k per MFMA chain)
-  float af[STEPS];
-  {
-    const int64_t user = ub + 16 * wave + i16;
+  // A fragments: this wave's 16 * UF users, k = 4s + k4 (ascending k per MFMA chain)
+  float af[UF][STEPS];
 #pragma unroll
-    for (int s = 0; s < STEPS; ++s) af[s] = user < p.nb ? p.u[user * p.ldu + 4 * s + k4] : 0.f;
+  for (int f = 0; f < UF; ++f) {
+    const int64_t user = ub + wu + 16 * f + i16;
+#pragma unroll
+    for (int s = 0; s < STEPS; ++s)
+      af[f][s] = user < p.nb ? p.u[user * p.ldu + 4 * s + k4] : 0.f;
   }
   for (int e = threadIdx.x; e < UPB * KM; e += kBlock) {
     l_score[e / KM][e % KM] = -INFINITY;
@@ -149,58 +155,68 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
     if (t0 + TI < i_end) load_tile(t0 + TI);
     // all B fragments of the tile first (LDS latency paid once), then the MFMAs with the
     // TI/16 independent accumulator chains interleaved; each chain still runs k ascending
-    floatx4_t acc[TI / 16];
+    floatx4_t acc[UF][TI / 16];
     float bf[TI / 16][STEPS];
 #pragma unroll
     for (int nt = 0; nt < TI / 16; ++nt) {
       const float* brow = &v_lds[buf][(16 * nt + i16) * LDV + k4];
 #pragma unroll
       for (int s = 0; s < STEPS; ++s) bf[nt][s] = brow[4 * s];
-      acc[nt] = floatx4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int f = 0; f < UF; ++f) acc[f][nt] = floatx4_t{0.f, 0.f, 0.f, 0.f};
     }
     __builtin_amdgcn_sched_barrier(0);  // keep every LDS read ahead of the MFMA stream
 #pragma unroll
     for (int s = 0; s < STEPS; ++s)
 #pragma unroll
       for (int nt = 0; nt < TI / 16; ++nt)
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[s], bf[nt][s], acc[nt], 0, 0, 0);
-    // candidates: lane holds users 16*wave + 4*k4 + q (q = reg) x items t0 + 16*nt + i16.
-    // Fast filter against register copies of the four users' current worst entries (a list's
+#pragma unroll
+        for (int f = 0; f < UF; ++f)
+          acc[f][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[f][s], bf[nt][s], acc[f][nt], 0,
+                                                            0, 0);
+    // candidates: lane holds users wu + 16*f + 4*k4 + q (q = reg) x items t0 + 16*nt + i16.
+    // Fast filter against register copies of the users' current worst entries (a list's
     // worst only rises, so a score that fails the copy fails the list); the wave leaves the
     // tile after one ballot unless some lane has a candidate.
-    float ws[4];
-    int wi[4];
-    unsigned cmask = 0;   // bit 4*nt + q: (item, user q) passes the register filter
+    float ws[UF][4];
+    int wi[UF][4];
+    unsigned cmask = 0;   // bit (f * TI/16 + nt) * 4 + q: (item, user) passes the filter
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      ws[q] = l_score[16 * wave + 4 * k4 + q][0];   // heap roots = current worst
-      wi[q] = l_item[16 * wave + 4 * k4 + q][0];
-    }
-#pragma unroll
-    for (int nt = 0; nt < TI / 16; ++nt)
+    for (int f = 0; f < UF; ++f)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        float sc = acc[nt][q];
-        if (sc != sc) sc = -INFINITY;  // NaN scores rank last
-        acc[nt][q] = sc;
-        const int64_t item64 = t0 + 16 * nt + i16;
-        // >= : a superset of better() (ties are settled by the leader's exact check)
-        if (sc >= ws[q] && item64 < i_end && ub + 16 * wave + 4 * k4 + q < p.nb &&
-            (sc > ws[q] || (int)item64 < wi[q]))
-          cmask |= 1u << (4 * nt + q);
+        ws[f][q] = l_score[wu + 16 * f + 4 * k4 + q][0];   // heap roots = current worst
+        wi[f][q] = l_item[wu + 16 * f + 4 * k4 + q][0];
       }
+#pragma unroll
+    for (int f = 0; f < UF; ++f)
+#pragma unroll
+      for (int nt = 0; nt < TI / 16; ++nt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float sc = acc[f][nt][q];
+          if (sc != sc) sc = -INFINITY;  // NaN scores rank last
+          acc[f][nt][q] = sc;
+          const int64_t item64 = t0 + 16 * nt + i16;
+          // >= : a superset of better() (ties are settled by the leader's exact check)
+          if (sc >= ws[f][q] && item64 < i_end && ub + wu + 16 * f + 4 * k4 + q < p.nb &&
+              (sc > ws[f][q] || (int)item64 < wi[f][q]))
+            cmask |= 1u << ((f * (TI / 16) + nt) * 4 + q);
+        }
     if (__ballot(cmask != 0) == 0) continue;
+#pragma unroll
+    for (int f = 0; f < UF; ++f)
 #pragma unroll
     for (int nt = 0; nt < TI / 16; ++nt) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int ul = 16 * wave + 4 * k4 + q;
+        const int ul = wu + 16 * f + 4 * k4 + q;
         const int64_t user = ub + ul;
         const int64_t item64 = t0 + 16 * nt + i16;
-        const float s = acc[nt][q];
+        const float s = acc[f][nt][q];
         const int item = (int)item64;
         // (the leader re-checks each candidate against the heap root, which only rises)
-        const unsigned long long m = __ballot((cmask >> (4 * nt + q)) & 1u);
+        const unsigned long long m = __ballot((cmask >> ((f * (TI / 16) + nt) * 4 + q)) & 1u);
         if (m == 0) continue;
         // the 16 lanes of group k4 share user ul; group leader (i16 == 0) inserts the group's
         // candidates into that user's heap one by one — the four groups work in parallel
@@ -238,7 +254,7 @@ __global__ __launch_bounds__(kBlock) void score_topk_kernel(TopkParams p) {
   }
   __syncthreads();
   // emit each user's list sorted by (score desc, item asc): rank by counting
-  for (int ul = 16 * wave; ul < 16 * wave + 16; ++ul) {
+  for (int ul = wu; ul < wu + UPW; ++ul) {
     const int64_t user = ub + ul;
     if (user >= p.nb) break;
     for (int e = lane; e < KM; e += 64) {
@@ -297,10 +313,13 @@ __global__ __launch_bounds__(kBlock) void topk_merge_kernel(const int64_t* __res
 using namespace gnnrec;
 
 namespace {
+// Two user fragments per wave where the A fragments and the lists fit (d <= 64, k <= 64).
 template <int D, int KM>
 void launch_topk(const TopkParams& p, hipStream_t s) {
-  hipLaunchKernelGGL((score_topk_kernel<D, KM>), dim3((unsigned)ceil_div(p.nb, 64), (unsigned)p.n_split),
-                     dim3(kBlock), 0, s, p);
+  constexpr int UF = (D <= 64 && KM <= 64) ? 2 : 1;
+  hipLaunchKernelGGL((score_topk_kernel<D, KM, UF>),
+                     dim3((unsigned)ceil_div(p.nb, 64 * UF), (unsigned)p.n_split), dim3(kBlock), 0,
+                     s, p);
 }
 template <int D>
 int dispatch_k(const TopkParams& p, hipStream_t s) {

@@ -493,7 +493,7 @@ def score_topk(user_emb: torch.Tensor, item_emb: torch.Tensor, k: int,
     if seen_ptr is not None:
         seen_ptr = seen_ptr.to(u.device, torch.int64).contiguous()
         seen_col = seen_col.to(u.device, torch.int32).contiguous()
-    n_split = topk_splits(B, v.shape[0], d) if n_split is None else int(n_split)
+    n_split = topk_splits(B, v.shape[0], d, k) if n_split is None else int(n_split)
     wi = ws = None
     if n_split > 1:
         wi = torch.empty((B, n_split, k), dtype=torch.int64, device=u.device)
@@ -506,9 +506,16 @@ def score_topk(user_emb: torch.Tensor, item_emb: torch.Tensor, k: int,
     return idx, sc
 
 
-def topk_splits(n_users: int, n_items: int, d: int, target_wg: int = 1024) -> int:
-    """Item ranges for gnnrec_score_topk_split_f32: enough workgroups (64 users each) to fill
-    the 256 CUs a few times over, each range at least 16 tiles long."""
-    wg = max(1, -(-n_users // 64))
+def topk_splits(n_users: int, n_items: int, d: int, k: int = 20,
+                target_wg: Optional[int] = None) -> int:
+    """Item ranges for gnnrec_score_topk_split_f32: enough workgroups to fill the 256 CUs in
+    one round — 512 of 128 users for d <= 64 and k <= 64 (two per CU: 68 KB LDS, 240
+    registers per lane; csrc/topk.hip launch_topk), else 1024 of 64 — each range at least 16
+    tiles long. Measured (profiles/r02/config8_uf2_splits.jsonl): 16K users 35.7 ms at 512
+    workgroups vs 43.6 at 1024; 2K users 10.5 ms at 512 vs 16.8 at 1024."""
+    two = d <= 64 and k <= 64
+    upb = 128 if two else 64
+    target_wg = target_wg or (512 if two else 1024)
+    wg = max(1, -(-n_users // upb))
     tile = 64 if d <= 128 else 32
     return int(max(1, min(-(-target_wg // wg), n_items // (16 * tile), 65535)))

@@ -123,6 +123,8 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--g1b", action="store_true", help="config 5 at full size (10M x 10M, 1B pairs)")
     ap.add_argument("--verify", action="store_true")
+    ap.add_argument("--topk-splits", type=int, nargs="*", default=[],
+                    help="config 8: item-range splits timed besides 1 and the default")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
     a = ap.parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -254,7 +256,7 @@ def main(argv=None):
                 seen_ptr = torch.arange(0, nb * 100 + 1, 100, dtype=torch.int64)
                 seen_col = seen.flatten().to(torch.int32).cpu()
                 res = {}
-                for ns in sorted({1, topk_splits(nb, ni, dd)}):
+                for ns in sorted({1, topk_splits(nb, ni, dd, 20)} | set(a.topk_splits)):
                     f = lambda: score_topk(U, V, 20, seen_ptr, seen_col, n_split=ns)
                     t, _ = timed(f, max(2, a.steps // 5), 1, 1, device)
                     res[ns] = t
