@@ -16,6 +16,10 @@
 // MFMA 16x16x4 f32 lane maps (cdna_hip_programming.md §3): A[i=l&15][k=l>>4],
 // B[k=l>>4][j=l&15], C/D: col = l&15, row = 4*(l>>4) + reg.
 #include <algorithm>
+#include <mutex>
+#include <type_traits>
+#include <utility>
+#include <vector>
 
 #include "gather.h"
 
@@ -447,6 +451,86 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
   }
 }
 
+// Streaming row GEMM y[r, :P] = x[r, :K] @ B[K, P] for tall-skinny operands (GAT's fused
+// projection [N, 64] x [64, H*o + 2H] and head-mean [N, H*in] x [H*in, o]; hipBLASLt ran these
+// at 1-3 TB/s). Every wave owns 16-row tiles on its own (no barrier in the loop) and feeds the
+// A operand of v_mfma_f32_16x16x4f32 straight from registers: lane (i, g) = (lane & 15,
+// lane >> 4) loads row i's float4 at columns 16 t + 4 g (t < K/16: the 4 lanes of a row read
+// 64 contiguous bytes per instruction), and MFMA step 4 t + q contracts k = 16 t + 4 g + q
+// (a permutation of the k order; GAT is an fp32-tolerance path). B sits in LDS for the launch
+// (row stride PN + 4: the k rows of lanes g and g + 1 land 16 banks apart), NT 16-column output
+// tiles, the o tile goes through a small private LDS tile so whole rows are stored, and the
+// next tile's rows are in flight in registers meanwhile.
+template <int K, int NT, int NW>
+__global__ __launch_bounds__(64 * NW) void rows_gemm_kernel(int64_t n_rows, const float* __restrict__ x,
+                                                            int64_t ldx, const float* __restrict__ B,
+                                                            int P, float* __restrict__ y, int64_t ldy) {
+  constexpr int PN = NT * 16;
+  constexpr int LDB = PN + 4;
+  constexpr int LDO = PN + 4;
+  constexpr int T = K / 16;            // float4 per lane per tile
+  static_assert(K % 16 == 0 && NT >= 1, "rows_gemm: K % 16 == 0");
+  // dynamic LDS (rows_gemm_lds): B [K][LDB] then NW o tiles [16][LDO]
+  extern __shared__ __attribute__((aligned(16))) float rg_lds[];
+  float* b_lds = rg_lds;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int i16 = lane & 15, g = lane >> 4;
+  for (int e = threadIdx.x; e < K * PN; e += 64 * NW) {
+    const int k = e / PN, j = e % PN;
+    b_lds[k * LDB + j] = j < P ? B[(int64_t)k * P + j] : 0.f;
+  }
+  __syncthreads();
+  float* ot = rg_lds + K * LDB + wave * 16 * LDO;
+  const int64_t n_tiles = ceil_div(n_rows, 16);
+  const int64_t stride = (int64_t)gridDim.x * NW;
+  float4 pa[T], pn[T];
+  auto load = [&](int64_t tile, float4 (&v)[T]) {
+    const int64_t r = tile * 16 + i16;
+    const bool ok = tile < n_tiles && r < n_rows;
+    const float* xr = x + (ok ? r : 0) * ldx + 4 * g;
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+      v[t] = ok ? *reinterpret_cast<const float4*>(xr + 16 * t) : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  int64_t tile = (int64_t)blockIdx.x * NW + wave;
+  load(tile, pa);
+  const int P4 = P / 4;
+  const float* brow = b_lds + (4 * g) * LDB + i16;
+  for (; tile < n_tiles; tile += stride) {
+    load(tile + stride, pn);
+    floatx4 c[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) c[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // fully unrolled (a rolled k loop made the compiler rotate the accumulators through
+    // partially overlapping AGPR ranges, v_mfma a[10:13], ..., a[12:15]: wrong on gfx950)
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const float av[4] = {pa[t].x, pa[t].y, pa[t].z, pa[t].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          c[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+              av[q], brow[(16 * t + q) * LDB + 16 * nt], c[nt], 0, 0, 0);
+    }
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ot[(4 * g + q) * LDO + 16 * nt + i16] = c[nt][q];
+    for (int e = lane; e < 16 * P4; e += 64) {
+      const int row = e / P4, c4 = e - row * P4;
+      const int64_t r = tile * 16 + row;
+      if (r < n_rows) {
+        const float* o = ot + row * LDO + 4 * c4;
+        *reinterpret_cast<float4*>(y + r * ldy + 4 * c4) = make_float4(o[0], o[1], o[2], o[3]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) pa[t] = pn[t];
+  }
+}
+
 }  // namespace gnnrec
 
 using namespace gnnrec;
@@ -603,4 +687,84 @@ extern "C" int gnnrec_dense_transform_f32(int64_t n_rows, const float* n, int64_
   p.M = M; p.c_out = c_out; p.c_res = c_res; p.resid = resid; p.ld_resid = ld_resid;
   p.acc = acc; p.ld_acc = ld_acc; p.acc_mode = acc_mode; p.w_out = w_out; p.w_res = w_res;
   return launch_dense<1, false>(p, d, as_hip(stream));
+}
+
+namespace {
+template <int K, int NT, int NW>
+constexpr size_t rows_gemm_lds() {
+  constexpr int PN = NT * 16;
+  return sizeof(float) * ((size_t)K * (PN + 4) + (size_t)NW * 16 * (PN + 4));
+}
+
+// Dynamic LDS past 64 KB needs the kernel attribute, set once per (kernel, device); a
+// refusal is reported, not ignored.
+bool big_lds_ok(const void* kern, int dev, size_t bytes) {
+  static std::mutex mu;
+  static std::vector<std::pair<std::pair<const void*, int>, int>> done;
+  std::lock_guard<std::mutex> lock(mu);
+  for (auto& e : done)
+    if (e.first.first == kern && e.first.second == dev) return e.second > 0;
+  const bool ok = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)bytes) == hipSuccess;
+  if (!ok) (void)hipGetLastError();
+  done.push_back({{kern, dev}, ok ? 1 : -1});
+  return ok;
+}
+}  // namespace
+
+// y[r, :p] = x[r, :k] @ B[k, p] (B row-major [k][p]) on the matrix cores, fp32 in / fp32
+// accumulate, k ascending per output. k in {64, 128, 256}, p % 4 == 0, p <= 80 (k = 64),
+// 64 (k = 128, 256); x and y rows 16-B aligned.
+extern "C" int gnnrec_rows_gemm_f32(int64_t n_rows, const float* x, int64_t ldx, int32_t k,
+                                    const float* B, int32_t p, float* y, int64_t ldy,
+                                    gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(n_rows >= 0 && k > 0 && p > 0 && p % 4 == 0, "rows_gemm: bad sizes");
+  if (n_rows == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(B && rows_ok(x, ldx) && ldx >= k && rows_ok(y, ldy) && ldy >= p,
+                 "rows_gemm: x/y must be 16-B aligned with ld %% 4 == 0 and ld >= k / p");
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  hipStream_t s = as_hip(stream);
+  auto go = [&](auto kern, auto kk, auto ntc, auto nwc, int per_cu) -> int {
+    constexpr int K = decltype(kk)::value, NT = decltype(ntc)::value, NW = decltype(nwc)::value;
+    const size_t lds = rows_gemm_lds<K, NT, NW>();
+    if (lds > 64 * 1024 && !big_lds_ok((const void*)kern, dev, lds)) {
+      set_error("rows_gemm: the device refused %zu bytes of dynamic LDS", lds);
+      return GNNREC_EHIP;
+    }
+    const int64_t tiles = ceil_div(n_rows, 16 * NW);
+    const unsigned grid = (unsigned)std::min<int64_t>(tiles, (int64_t)cus * per_cu);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NW), lds, s, n_rows, x, ldx, B, (int)p, y,
+                       ldy);
+    return check_launch("rows_gemm");
+  };
+  using I = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  using I3 = std::integral_constant<int, 3>;
+  using I4 = std::integral_constant<int, 4>;
+  using I5 = std::integral_constant<int, 5>;
+  using I8 = std::integral_constant<int, 8>;
+  using K64 = std::integral_constant<int, 64>;
+  using K128 = std::integral_constant<int, 128>;
+  using K256 = std::integral_constant<int, 256>;
+  const int nt = (p + 15) / 16;
+  if (k == 64) {
+    switch (nt) {
+      case 1: return go(rows_gemm_kernel<64, 1, 8>, K64{}, I{}, I8{}, 2);
+      case 2: return go(rows_gemm_kernel<64, 2, 8>, K64{}, I2{}, I8{}, 2);
+      case 3: return go(rows_gemm_kernel<64, 3, 8>, K64{}, I3{}, I8{}, 2);
+      case 4: return go(rows_gemm_kernel<64, 4, 8>, K64{}, I4{}, I8{}, 2);
+      case 5: return go(rows_gemm_kernel<64, 5, 8>, K64{}, I5{}, I8{}, 2);
+      default: break;
+    }
+  } else if (k == 128 && nt <= 4) {
+    return go(rows_gemm_kernel<128, 4, 8>, K128{}, I4{}, I8{}, 1);
+  } else if (k == 256 && nt <= 4) {
+    return go(rows_gemm_kernel<256, 4, 8>, K256{}, I4{}, I8{}, 1);
+  }
+  set_error("rows_gemm: (k=%d, p=%d) unsupported (k 64: p <= 80; k 128/256: p <= 64)", (int)k,
+            (int)p);
+  return GNNREC_EUNSUPPORTED;
 }

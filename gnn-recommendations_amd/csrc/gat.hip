@@ -70,11 +70,51 @@ __device__ __forceinline__ void gat_finish(const GatParams& p, int64_t r, float4
   acc_epilogue(p.epi, o, p.self + r * p.ld_self + 4 * gl, p.acc + r * p.ld_acc + 4 * gl, p.acc_div);
 }
 
-// Online-softmax accumulation of neighbours [beg, end) of row r (head of this lane).
+// Online softmax in blocks of kSoftBlock neighbours, base 2: E_j = LeakyReLU(s_self + s_neigh[j])
+// * log2(e); per block the running max moves once (m' = max(m, max_j E_j)), the sums are
+// rescaled once by 2^(m - m'), and each neighbour costs ONE v_exp_f32 (2^(E_j - m')) and its
+// fmaf. softmax = sum_j 2^(E_j - m) h_j / sum_j 2^(E_j - m) is the reference's
+// exp(e_j - max) / sum (gat.py:135-141) reassociated — fp32 tolerance, as the reference's
+// own dense softmax. Neighbours past the row end get E = -inf (p = 0: the sums are unchanged,
+// no branch). Every kernel below uses the same blocks from the row's (or segment's) first
+// neighbour, so the shared-row and the head-major kernels agree bit for bit.
+constexpr int kSoftBlock = 8;
+constexpr float kLog2e = 1.4426950408889634f;
+
+__device__ __forceinline__ float gat_exp2(float v) { return __builtin_amdgcn_exp2f(v); }
+
+__device__ __forceinline__ float gat_logit2(float ss, float sn, float slope, bool valid) {
+  float e = ss + sn;
+  e = e > 0.f ? e : e * slope;
+  return valid ? e * kLog2e : -INFINITY;
+}
+
+// One softmax block of one head: logits E[0..kSoftBlock), rows xv[0..kSoftBlock).
+__device__ __forceinline__ void gat_block(const float (&E)[kSoftBlock], const float4* xv,
+                                          float& m, float& l, float4& a) {
+  float bm = E[0];
+#pragma unroll
+  for (int t = 1; t < kSoftBlock; ++t) bm = fmaxf(bm, E[t]);
+  const float mn = fmaxf(m, bm);
+  const float sc = gat_exp2(m - mn);   // m = -inf on the first block: sc = 0
+  l *= sc;
+  a = make_float4(a.x * sc, a.y * sc, a.z * sc, a.w * sc);
+#pragma unroll
+  for (int t = 0; t < kSoftBlock; ++t) {
+    const float pe = gat_exp2(E[t] - mn);
+    l += pe;
+    a = fma4(pe, xv[t], a);
+  }
+  m = mn;
+}
+
+// Online-softmax accumulation of neighbours [beg, end) of row r (head of this lane); m is in
+// the base-2 logit domain.
 template <int GROUP>
 __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, int64_t beg,
                                                int64_t end, int gl, float& m, float& l,
                                                float4& a) {
+  static_assert(kChunk % kSoftBlock == 0, "a gather step holds whole softmax blocks");
   const int hl = p.o_dim / 4;
   const int head = gl / hl;
   const float ss = p.s_self[r * p.heads + head];
@@ -96,20 +136,13 @@ __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, in
       sn[t] = p.s_neigh[(int64_t)c * p.heads + head];
     }
 #pragma unroll
-    for (int t = 0; t < kChunk; ++t) {
-      if (k0 + t < end) {
-        float e = ss + sn[t];
-        e = e > 0.f ? e : e * p.slope;
-        const float mn = fmaxf(m, e);
-        const float sc = expf(m - mn);  // m = -inf on the first neighbour: sc = 0
-        const float pe = expf(e - mn);
-        l = l * sc + pe;
-        a.x = __builtin_fmaf(pe, xv[t].x, a.x * sc);
-        a.y = __builtin_fmaf(pe, xv[t].y, a.y * sc);
-        a.z = __builtin_fmaf(pe, xv[t].z, a.z * sc);
-        a.w = __builtin_fmaf(pe, xv[t].w, a.w * sc);
-        m = mn;
-      }
+    for (int b = 0; b < kChunk / kSoftBlock; ++b) {
+      if (k0 + b * kSoftBlock >= end) break;
+      float E[kSoftBlock];
+#pragma unroll
+      for (int t = 0; t < kSoftBlock; ++t)
+        E[t] = gat_logit2(ss, sn[b * kSoftBlock + t], p.slope, k0 + b * kSoftBlock + t < end);
+      gat_block(E, xv + b * kSoftBlock, m, l, a);
     }
   }
 }
@@ -155,6 +188,7 @@ __global__ __launch_bounds__(kBlock) void gat_shared_kernel(GatParams p) {
     l[h] = 0.f;
     a[h] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  static_assert(CH == kSoftBlock, "one softmax block per gather step (same blocks as gat_kernel)");
   for (int64_t k0 = beg; k0 < end; k0 += CH) {
     constexpr int PER = (GROUP >= CH) ? 1 : CH / GROUP;
     int cm[PER];
@@ -179,23 +213,11 @@ __global__ __launch_bounds__(kBlock) void gat_shared_kernel(GatParams p) {
       }
     }
 #pragma unroll
-    for (int t = 0; t < CH; ++t) {
-      if (k0 + t < end) {
+    for (int h = 0; h < H; ++h) {
+      float E[CH];
 #pragma unroll
-        for (int h = 0; h < H; ++h) {
-          float e = ss[h] + sn[t][h];
-          e = e > 0.f ? e : e * p.slope;
-          const float mn = fmaxf(m[h], e);
-          const float sc = expf(m[h] - mn);
-          const float pe = expf(e - mn);
-          l[h] = l[h] * sc + pe;
-          a[h].x = __builtin_fmaf(pe, xv[t].x, a[h].x * sc);
-          a[h].y = __builtin_fmaf(pe, xv[t].y, a[h].y * sc);
-          a[h].z = __builtin_fmaf(pe, xv[t].z, a[h].z * sc);
-          a[h].w = __builtin_fmaf(pe, xv[t].w, a[h].w * sc);
-          m[h] = mn;
-        }
-      }
+      for (int t = 0; t < CH; ++t) E[t] = gat_logit2(ss[h], sn[t][h], p.slope, k0 + t < end);
+      gat_block(E, xv, m[h], l[h], a[h]);
     }
   }
 #pragma unroll
@@ -254,7 +276,7 @@ __global__ __launch_bounds__(kBlock) void gat_merge_kernel(GatParams p, GatSplit
   float L = 0.f;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   for (int64_t s = s0; s < s1; ++s) {
-    const float w = expf(mm[s * p.heads + head] - M);
+    const float w = gat_exp2(mm[s * p.heads + head] - M);   // base-2 maxima (gat_block)
     const float4 t = ld4(sp.work + s * F + 4 * gl);
     L = __builtin_fmaf(ll[s * p.heads + head], w, L);
     a = make_float4(__builtin_fmaf(t.x, w, a.x), __builtin_fmaf(t.y, w, a.y),

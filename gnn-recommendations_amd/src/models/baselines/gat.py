@@ -62,11 +62,18 @@ class GATLayer(nn.Module):
             self._fused_w, self._fused_key = out.detach(), key
         return out
 
+    @staticmethod
+    def _project(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        """x @ w^T; on a ROCm device the streaming MFMA row GEMM (gnnrec_rows_gemm_f32)."""
+        if x.is_cuda:
+            return ops.functional.rows_gemm(x, w.t())
+        return x @ w.t()
+
     def projections(self, x: torch.Tensor):
         """h = [W_0 x | ... | W_H x] and the per-head attention halves s_self, s_neigh, all
         from one GEMM (h is a strided view of its output)."""
         ho = self.n_heads * self.out_dim
-        out = x @ self.fused_weight().t()                                  # [N, H*o + 2H]
+        out = self._project(x, self.fused_weight())                        # [N, H*o + 2H]
         return out[:, :ho], out[:, ho:ho + self.n_heads], out[:, ho + self.n_heads:]
 
     def shares_input(self) -> bool:
@@ -85,7 +92,7 @@ class GATLayer(nn.Module):
         """(table gathered per neighbour, s_self, s_neigh) for the rows of x."""
         if self.shares_input():
             H = self.n_heads
-            s = x @ self.fused_weight()[H * self.out_dim:].t()            # [N, 2H]
+            s = self._project(x, self.fused_weight()[H * self.out_dim:])    # [N, 2H]
             return x, s[:, :H], s[:, H:]
         return self.projections(x)
 
@@ -99,7 +106,7 @@ class GATLayer(nn.Module):
                                      acc_div=acc_div)
         z = ops.gat_aggregate(a, feat, s_self, s_neigh, self.n_heads, self.in_dim, self.alpha,
                               mean_heads=False, apply_elu=False, shared_rows=True)
-        y = z @ self.head_mean_weight()
+        y = ops.functional.rows_gemm(z, self.head_mean_weight())
         if apply_elu:
             y = F.elu(y)
         if epi & (EPI_ACC_INIT | EPI_ACC_ADD):      # the kernel epilogue's order

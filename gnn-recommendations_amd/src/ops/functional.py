@@ -467,6 +467,27 @@ def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh:
     return out
 
 
+def rows_gemm(x: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x [n, k] @ B [k, p] on the matrix cores (gnnrec_rows_gemm_f32): the tall-skinny GAT
+    projections, streamed at HBM rate instead of hipBLASLt's 1-3 TB/s. fp32, k ascending per
+    output (fp32-tolerance equal to torch.matmul). Shapes the kernel does not take go to
+    torch.matmul on the same device."""
+    n, k = x.shape
+    p = B.shape[1]
+    ok = (x.is_cuda and x.dtype == torch.float32 and B.dtype == torch.float32
+          and k in (64, 128, 256) and p % 4 == 0 and (p <= 80 if k == 64 else p <= 64)
+          and x.stride(1) == 1 and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0)
+    if not ok:
+        return torch.matmul(x, B, out=out) if out is not None else torch.matmul(x, B)
+    Bc = B.contiguous()
+    if out is None:
+        out = torch.empty((n, p), dtype=torch.float32, device=x.device)
+    check(_lib.lib().gnnrec_rows_gemm_f32(n, ptr(x), x.stride(0), k, ptr(Bc), p, ptr(out),
+                                          out.stride(0), _lib.stream_of(x.device)),
+          "gnnrec_rows_gemm_f32")
+    return out
+
+
 def score_topk(user_emb: torch.Tensor, item_emb: torch.Tensor, k: int,
                seen_ptr: Optional[torch.Tensor] = None,
                seen_col: Optional[torch.Tensor] = None,

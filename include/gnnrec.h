@@ -255,7 +255,8 @@ int gnnrec_dense_transform_f32(int64_t n_rows, const float* n, int64_t ldn, floa
  * for every head h and destination row r with neighbours j (CSR pattern; values ignored):
  *   e_j = LeakyReLU_slope(s_self[r, h] + s_neigh[j, h]);  a = softmax_j(e)
  *   o[r, h, :] = sum_j a_j * hfeat[j, h, :]
- * (single pass, online max/sum rescaling, fp32). hfeat[j, h, :] starts at
+ * (single pass, online max/sum rescaling per block of 8 neighbours in base 2, fp32).
+ * hfeat[j, h, :] starts at
  * hfeat + j*ldh + h*head_stride: head_stride = o_dim for the head-major [N, heads*o_dim]
  * table of the per-head W_h x; head_stride = 0 lets every head aggregate the same row (the
  * layer input x, with W_h applied by the caller afterwards: sum_j a_j W_h x_j =
@@ -291,6 +292,15 @@ int gnnrec_gat_heavy_f32(const int32_t* col, const int64_t* seg_row, const int64
                          float* out, int64_t ldo, int32_t epi, const float* self,
                          int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
                          gnnrec_stream_t stream);
+
+/* Dense projections of the GAT layer (gat.py:113-118 W_h x and the attention halves, one
+ * fused weight; and the head-averaged last layer's W_h applied after the aggregation,
+ * gat.py:149): y[r, :p] = x[r, :k] @ B[k, p], B row-major [k][p], on the matrix cores
+ * (fp32, k ascending). Replaces the tall-skinny torch.matmul / hipBLASLt calls.
+ * k in {64, 128, 256}; p % 4 == 0; p <= 80 for k = 64, p <= 64 otherwise; x, y rows 16-B
+ * aligned (ld % 4 == 0). */
+int gnnrec_rows_gemm_f32(int64_t n_rows, const float* x, int64_t ldx, int32_t k, const float* B,
+                         int32_t p, float* y, int64_t ldy, gnnrec_stream_t stream);
 
 /* ---- a13: scoring + seen-item mask + top-K ------------------------------------------
  * Replaces evaluator.py:96-105 / trainer.py:327-336 for one batch of users:

@@ -473,3 +473,21 @@ def test_lightgcn_through_tiled_hop_is_bit_exact(cuda, monkeypatch):
     np.testing.assert_array_equal(bits(csr.cpu().numpy()), ref)
     m = torch.zeros(g.shape[0], dtype=torch.uint8, device=cuda)
     assert F.tiled_plan_for(g, xd, x_mask=m) is None     # masked hops keep the CSR kernel
+
+
+@pytest.mark.parametrize("k,p", [(64, 72), (64, 8), (64, 64), (64, 80), (128, 64), (256, 64),
+                                 (256, 12)])
+def test_rows_gemm_matches_fp32_matmul(cuda, k, p):
+    """gnnrec_rows_gemm_f32 (GAT projections) vs a float64 product: fp32-accumulation
+    tolerance, ragged tile tails, a strided x view, and no write past p columns."""
+    gen = torch.Generator().manual_seed(k + p)
+    n = 16 * 37 + 5
+    xb = torch.randn(n, k + 8, generator=gen)
+    B = torch.randn(k, p, generator=gen) * 0.1
+    ref = (xb[:, :k].double() @ B.double()).float()
+    x = xb.to(cuda)[:, :k]                       # ld = k + 8
+    out = torch.full((n, p + 4), 7.0, device=cuda)
+    F.rows_gemm(x, B.to(cuda), out=out[:, :p])
+    torch.testing.assert_close(out[:, :p].cpu(), ref, rtol=1e-5, atol=1e-5)
+    assert bool((out[:, p:] == 7.0).all())
+    assert F.rows_gemm(x[:0], B.to(cuda)).shape == (0, p)
