@@ -461,10 +461,21 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
 // (row stride PN + 4: the k rows of lanes g and g + 1 land 16 banks apart), NT 16-column output
 // tiles, the o tile goes through a small private LDS tile so whole rows are stored, and the
 // next tile's rows are in flight in registers meanwhile.
+struct RowsGemmEpi {   // optional epilogue of gnnrec_rows_gemm_f32 (GAT's last layer)
+  int apply_elu;
+  int epi;             // GNNREC_EPI_ACC_* flags, as gnnrec_gat_aggregate_f32
+  const float* self;
+  int64_t ld_self;
+  float* acc;
+  int64_t ld_acc;
+  float acc_div;
+};
+
 template <int K, int NT, int NW>
 __global__ __launch_bounds__(64 * NW) void rows_gemm_kernel(int64_t n_rows, const float* __restrict__ x,
                                                             int64_t ldx, const float* __restrict__ B,
-                                                            int P, float* __restrict__ y, int64_t ldy) {
+                                                            int P, float* __restrict__ y, int64_t ldy,
+                                                            RowsGemmEpi ep) {
   constexpr int PN = NT * 16;
   constexpr int LDB = PN + 4;
   constexpr int LDO = PN + 4;
@@ -518,12 +529,44 @@ __global__ __launch_bounds__(64 * NW) void rows_gemm_kernel(int64_t n_rows, cons
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
       for (int q = 0; q < 4; ++q) ot[(4 * g + q) * LDO + 16 * nt + i16] = c[nt][q];
-    for (int e = lane; e < 16 * P4; e += 64) {
+    // whole rows out; the accumulator rows (ACC epilogue) are all loaded before the first use
+    constexpr int MAXIT = (16 * PN / 4 + 63) / 64;
+    const bool has_acc = (ep.epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) != 0;
+    const bool init = (ep.epi & GNNREC_EPI_ACC_INIT) != 0;
+    float4 bse[MAXIT];
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) {
+      const int e = lane + 64 * it;
       const int row = e / P4, c4 = e - row * P4;
       const int64_t r = tile * 16 + row;
-      if (r < n_rows) {
+      bse[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (has_acc && e < 16 * P4 && r < n_rows)
+        bse[it] = init ? ld4(ep.self + r * ep.ld_self + 4 * c4) : ld4(ep.acc + r * ep.ld_acc + 4 * c4);
+    }
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) {
+      const int e = lane + 64 * it;
+      const int row = e / P4, c4 = e - row * P4;
+      const int64_t r = tile * 16 + row;
+      if (e < 16 * P4 && r < n_rows) {
         const float* o = ot + row * LDO + 4 * c4;
-        *reinterpret_cast<float4*>(y + r * ldy + 4 * c4) = make_float4(o[0], o[1], o[2], o[3]);
+        float4 v = make_float4(o[0], o[1], o[2], o[3]);
+        if (ep.apply_elu) {   // F.elu (gat.py:283), as gat_finish
+          v.x = v.x > 0.f ? v.x : expm1f(v.x);
+          v.y = v.y > 0.f ? v.y : expm1f(v.y);
+          v.z = v.z > 0.f ? v.z : expm1f(v.z);
+          v.w = v.w > 0.f ? v.w : expm1f(v.w);
+        }
+        if (y) *reinterpret_cast<float4*>(y + r * ldy + 4 * c4) = v;
+        if (has_acc) {   // acc_epilogue's order: (base + y) [/ div]
+          float4 b = bse[it];
+          b.x = b.x + v.x; b.y = b.y + v.y; b.z = b.z + v.z; b.w = b.w + v.w;
+          if (ep.epi & GNNREC_EPI_ACC_DIV) {
+            b.x = b.x / ep.acc_div; b.y = b.y / ep.acc_div;
+            b.z = b.z / ep.acc_div; b.w = b.w / ep.acc_div;
+          }
+          st4(ep.acc + r * ep.ld_acc + 4 * c4, b);
+        }
       }
     }
 #pragma unroll
@@ -717,11 +760,19 @@ bool big_lds_ok(const void* kern, int dev, size_t bytes) {
 // 64 (k = 128, 256); x and y rows 16-B aligned.
 extern "C" int gnnrec_rows_gemm_f32(int64_t n_rows, const float* x, int64_t ldx, int32_t k,
                                     const float* B, int32_t p, float* y, int64_t ldy,
+                                    int32_t apply_elu, int32_t epi, const float* self,
+                                    int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
                                     gnnrec_stream_t stream) {
   GNNREC_REQUIRE(n_rows >= 0 && k > 0 && p > 0 && p % 4 == 0, "rows_gemm: bad sizes");
   if (n_rows == 0) return GNNREC_OK;
-  GNNREC_REQUIRE(B && rows_ok(x, ldx) && ldx >= k && rows_ok(y, ldy) && ldy >= p,
+  const bool has_acc = (epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) != 0;
+  GNNREC_REQUIRE(B && rows_ok(x, ldx) && ldx >= k && (y ? rows_ok(y, ldy) && ldy >= p : has_acc),
                  "rows_gemm: x/y must be 16-B aligned with ld %% 4 == 0 and ld >= k / p");
+  GNNREC_REQUIRE(!has_acc || (rows_ok(acc, ld_acc) && ld_acc >= p),
+                 "rows_gemm: ACC needs 16-B aligned acc rows");
+  GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_INIT) || (rows_ok(self, ld_self) && ld_self >= p),
+                 "rows_gemm: ACC_INIT needs 16-B aligned self rows");
+  const RowsGemmEpi ep{apply_elu, has_acc ? epi : 0, self, ld_self, acc, ld_acc, acc_div};
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -737,7 +788,7 @@ extern "C" int gnnrec_rows_gemm_f32(int64_t n_rows, const float* x, int64_t ldx,
     const int64_t tiles = ceil_div(n_rows, 16 * NW);
     const unsigned grid = (unsigned)std::min<int64_t>(tiles, (int64_t)cus * per_cu);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * NW), lds, s, n_rows, x, ldx, B, (int)p, y,
-                       ldy);
+                       ldy, ep);
     return check_launch("rows_gemm");
   };
   using I = std::integral_constant<int, 1>;

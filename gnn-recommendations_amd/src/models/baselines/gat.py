@@ -19,7 +19,7 @@ import torch.nn.functional as F
 
 from ..base import BaseRecommender
 from ... import ops
-from ...ops._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT
+from ...ops._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT, EPI_NO_Y
 from ...ops.graph import CsrGraph
 
 
@@ -106,15 +106,9 @@ class GATLayer(nn.Module):
                                      acc_div=acc_div)
         z = ops.gat_aggregate(a, feat, s_self, s_neigh, self.n_heads, self.in_dim, self.alpha,
                               mean_heads=False, apply_elu=False, shared_rows=True)
-        y = ops.functional.rows_gemm(z, self.head_mean_weight())
-        if apply_elu:
-            y = F.elu(y)
-        if epi & (EPI_ACC_INIT | EPI_ACC_ADD):      # the kernel epilogue's order
-            b = (self_rows if epi & EPI_ACC_INIT else acc) + y
-            if epi & EPI_ACC_DIV:
-                b = b / acc_div
-            acc.copy_(b)
-        return y
+        # W_h, ELU and the layer-mean accumulator in one pass (the aggregation epilogue's order)
+        return ops.functional.rows_gemm(z, self.head_mean_weight(), apply_elu=apply_elu, epi=epi,
+                                        self_rows=self_rows, acc=acc, acc_div=acc_div)
 
     def forward(self, x: torch.Tensor, adj_matrix, *, apply_elu: bool = False, epi: int = 0,
                 self_rows=None, acc=None, acc_div: float = 1.0) -> torch.Tensor:
@@ -184,7 +178,7 @@ class GAT(BaseRecommender):
             for k, layer in enumerate(self.layers, start=1):
                 epi = EPI_ACC_INIT if k == 1 else EPI_ACC_ADD
                 if k == L:
-                    epi |= EPI_ACC_DIV
+                    epi |= EPI_ACC_DIV | EPI_NO_Y   # only the layer mean is read after it
                 x = layer(x, a, apply_elu=True, epi=epi, self_rows=x, acc=acc,
                           acc_div=float(L + 1))
             x_final = acc

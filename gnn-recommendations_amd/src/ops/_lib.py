@@ -70,7 +70,8 @@ _SIGNATURES = {
                                   _f32, _p, _p, _i32, _p],
     "gnnrec_dense_transform_f32": [_i64, _p, _i64, _p, _i64, _i32, _p, _f32, _p, _i64, _f32,
                                    _p, _i64, _i32, _f32, _f32, _p],
-    "gnnrec_rows_gemm_f32": [_i64, _p, _i64, _i32, _p, _i32, _p, _i64, _p],
+    "gnnrec_rows_gemm_f32": [_i64, _p, _i64, _i32, _p, _i32, _p, _i64, _i32, _i32, _p, _i64,
+                             _p, _i64, _f32, _p],
     "gnnrec_gat_aggregate_f32": [_p, _p, _i64, _p, _i64, _i64, _p, _p, _i32, _i32, _f32, _i32,
                                  _i32, _p, _i64, _i32, _p, _i64, _p, _i64, _f32, _i64, _p],
     "gnnrec_gat_heavy_f32": [_p, _p, _p, _p, _i64, _p, _p, _i64, _p, _p, _i64, _i64, _p, _p,

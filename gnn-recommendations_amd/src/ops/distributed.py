@@ -347,7 +347,6 @@ def gat_forward_dist(dg: DistributedGraph, model, x0_pad: torch.Tensor, *,
     values a neighbour reads), and runs the sparse edge-softmax aggregation over its shard
     with ELU and the layer mean fused (gnnrec_gat_aggregate_f32 + heavy-row split). Returns
     this rank's rows of the layer mean (or the full table)."""
-    from ._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT
     layer_fn = layer_fn or _native_gat_layer
     x_local = dg.local_slice(x0_pad)
     acc = torch.empty_like(x_local)
@@ -357,7 +356,7 @@ def gat_forward_dist(dg: DistributedGraph, model, x0_pad: torch.Tensor, *,
         featp, snp = _exchanged(dg, feat), _exchanged(dg, sn.contiguous())
         epi = EPI_ACC_INIT if k == 1 else EPI_ACC_ADD
         if k == L:
-            epi |= EPI_ACC_DIV
+            epi |= EPI_ACC_DIV | EPI_NO_Y   # only the layer mean is read after it
         x_local = layer_fn(dg.shard, featp, ss, snp, layer, apply_elu=True, epi=epi,
                            self_rows=x_local, acc=acc, acc_div=float(L + 1))
     return gather_rows(dg, acc) if gather_output else acc

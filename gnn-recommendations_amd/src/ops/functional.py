@@ -467,25 +467,46 @@ def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh:
     return out
 
 
-def rows_gemm(x: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def rows_gemm(x: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None, *,
+              apply_elu: bool = False, epi: int = 0, self_rows: Optional[torch.Tensor] = None,
+              acc: Optional[torch.Tensor] = None, acc_div: float = 1.0) -> Optional[torch.Tensor]:
     """x [n, k] @ B [k, p] on the matrix cores (gnnrec_rows_gemm_f32): the tall-skinny GAT
-    projections, streamed at HBM rate instead of hipBLASLt's 1-3 TB/s. fp32, k ascending per
-    output (fp32-tolerance equal to torch.matmul). Shapes the kernel does not take go to
-    torch.matmul on the same device."""
+    projections, streamed at HBM rate instead of hipBLASLt's 1-3 TB/s, with GAT's epilogue
+    optionally fused (ELU, then the layer-mean accumulator acc = (self_rows | acc) + y
+    [/ acc_div], as gat_aggregate). fp32 (tolerance-equal to torch.matmul). Shapes the kernel
+    does not take run the same arithmetic through torch on the same device."""
     n, k = x.shape
     p = B.shape[1]
+    no_y = bool(epi & EPI_NO_Y)
+    rows = [t for t in (out, self_rows, acc) if t is not None]
     ok = (x.is_cuda and x.dtype == torch.float32 and B.dtype == torch.float32
           and k in (64, 128, 256) and p % 4 == 0 and (p <= 80 if k == 64 else p <= 64)
-          and x.stride(1) == 1 and x.stride(0) % 4 == 0 and x.data_ptr() % 16 == 0)
+          and all(t.stride(-1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
+                  for t in [x] + rows))
     if not ok:
-        return torch.matmul(x, B, out=out) if out is not None else torch.matmul(x, B)
+        y = torch.matmul(x, B)
+        if apply_elu:
+            y = torch.nn.functional.elu(y)
+        if epi & (EPI_ACC_INIT | EPI_ACC_ADD):
+            b = (self_rows if epi & EPI_ACC_INIT else acc) + y
+            acc.copy_(b / acc_div if epi & EPI_ACC_DIV else b)
+        if no_y:
+            return None
+        if out is not None:
+            out.copy_(y)
+            return out
+        return y
     Bc = B.contiguous()
-    if out is None:
+    if out is None and not no_y:
         out = torch.empty((n, p), dtype=torch.float32, device=x.device)
-    check(_lib.lib().gnnrec_rows_gemm_f32(n, ptr(x), x.stride(0), k, ptr(Bc), p, ptr(out),
-                                          out.stride(0), _lib.stream_of(x.device)),
-          "gnnrec_rows_gemm_f32")
-    return out
+    y = None if no_y else out
+    check(_lib.lib().gnnrec_rows_gemm_f32(
+        n, ptr(x), x.stride(0), k, ptr(Bc), p, ptr(y), y.stride(0) if y is not None else p,
+        int(apply_elu), int(epi), ptr(self_rows),
+        self_rows.stride(0) if self_rows is not None else p, ptr(acc),
+        acc.stride(0) if acc is not None else p, float(acc_div), _lib.stream_of(x.device)),
+        "gnnrec_rows_gemm_f32")
+    return y
 
 
 def score_topk(user_emb: torch.Tensor, item_emb: torch.Tensor, k: int,

@@ -296,11 +296,15 @@ int gnnrec_gat_heavy_f32(const int32_t* col, const int64_t* seg_row, const int64
 /* Dense projections of the GAT layer (gat.py:113-118 W_h x and the attention halves, one
  * fused weight; and the head-averaged last layer's W_h applied after the aggregation,
  * gat.py:149): y[r, :p] = x[r, :k] @ B[k, p], B row-major [k][p], on the matrix cores
- * (fp32, k ascending). Replaces the tall-skinny torch.matmul / hipBLASLt calls.
- * k in {64, 128, 256}; p % 4 == 0; p <= 80 for k = 64, p <= 64 otherwise; x, y rows 16-B
- * aligned (ld % 4 == 0). */
+ * (fp32 accumulate; the k order is a fixed permutation: an fp32-tolerance path). Replaces the
+ * tall-skinny torch.matmul / hipBLASLt calls. Then, as gnnrec_gat_aggregate_f32's epilogue:
+ * apply_elu: y = ELU(y); epi: the ACC_* flags (acc = (self or acc) + y [/ acc_div]). y may be
+ * NULL when epi writes acc. k in {64, 128, 256}; p % 4 == 0; p <= 80 for k = 64, p <= 64
+ * otherwise; x, y, self, acc rows 16-B aligned (ld % 4 == 0). */
 int gnnrec_rows_gemm_f32(int64_t n_rows, const float* x, int64_t ldx, int32_t k, const float* B,
-                         int32_t p, float* y, int64_t ldy, gnnrec_stream_t stream);
+                         int32_t p, float* y, int64_t ldy, int32_t apply_elu, int32_t epi,
+                         const float* self, int64_t ld_self, float* acc, int64_t ld_acc,
+                         float acc_div, gnnrec_stream_t stream);
 
 /* ---- a13: scoring + seen-item mask + top-K ------------------------------------------
  * Replaces evaluator.py:96-105 / trainer.py:327-336 for one batch of users:

@@ -491,3 +491,22 @@ def test_rows_gemm_matches_fp32_matmul(cuda, k, p):
     torch.testing.assert_close(out[:, :p].cpu(), ref, rtol=1e-5, atol=1e-5)
     assert bool((out[:, p:] == 7.0).all())
     assert F.rows_gemm(x[:0], B.to(cuda)).shape == (0, p)
+
+
+def test_rows_gemm_fused_gat_epilogue(cuda):
+    """rows_gemm's ELU + layer-mean epilogue == the same steps in torch (GAT's last layer)."""
+    from src.ops._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT, EPI_NO_Y
+    gen = torch.Generator().manual_seed(5)
+    n = 1000
+    z = torch.randn(n, 256, generator=gen).to(cuda)
+    W = (torch.randn(256, 64, generator=gen) * 0.05).to(cuda)
+    base = torch.randn(n, 64, generator=gen).to(cuda)
+    y_ref = torch.nn.functional.elu((z.double() @ W.double()).float())
+    for epi, div in [(EPI_ACC_INIT, 1.0), (EPI_ACC_ADD | EPI_ACC_DIV, 4.0)]:
+        acc = base.clone() if epi & EPI_ACC_ADD else torch.empty_like(base)
+        y = F.rows_gemm(z, W, apply_elu=True, epi=epi, self_rows=base, acc=acc, acc_div=div)
+        torch.testing.assert_close(y, y_ref, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(acc, (base + y) / div, rtol=0, atol=0)
+    acc = base.clone()
+    assert F.rows_gemm(z, W, epi=EPI_ACC_ADD | EPI_NO_Y, acc=acc) is None
+    torch.testing.assert_close(acc, base + (z.double() @ W.double()).float(), rtol=1e-5, atol=1e-5)
