@@ -17,7 +17,7 @@ import torch  # noqa: F401  (load order: torch's HIP runtime first)
 
 _PKG_ROOT = Path(__file__).resolve().parents[2]
 LIB_PATH = Path(os.environ.get("GNNREC_LIB", _PKG_ROOT / "lib" / "libgnnrec.so"))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # gnnrec.h epilogue flags
 EPI_ACC_INIT = 1

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GNNREC_ABI_VERSION 3
+#define GNNREC_ABI_VERSION 4
 
 typedef struct ihipStream_t* gnnrec_stream_t;
 

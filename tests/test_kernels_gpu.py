@@ -475,7 +475,7 @@ def test_lightgcn_through_tiled_hop_is_bit_exact(cuda, monkeypatch):
     assert F.tiled_plan_for(g, xd, x_mask=m) is None     # masked hops keep the CSR kernel
 
 
-@pytest.mark.parametrize("k,p", [(64, 72), (64, 8), (64, 64), (64, 80), (128, 64), (256, 64),
+@pytest.mark.parametrize("k,p", [(64, 72), (64, 8), (64, 48), (64, 64), (64, 80), (128, 64), (256, 64),
                                  (256, 12)])
 def test_rows_gemm_matches_fp32_matmul(cuda, k, p):
     """gnnrec_rows_gemm_f32 (GAT projections) vs a float64 product: fp32-accumulation

@@ -209,3 +209,33 @@ def test_heavy_row_plan_segments_cover_heavy_rows():
         assert b[0] == rp[r] and e[-1] == rp[r + 1] and np.all(b[1:] == e[:-1])
         assert np.all(e - b <= 16) and np.all(plan["seg_row"].numpy()[list(segs)] == r)
     assert G.heavy_plan(10 ** 6, 16) is None
+
+
+def test_mfma_accumulators_never_partially_overlap():
+    """Every MFMA in the shipped kernels either accumulates in place or into disjoint
+    registers. A rolled k loop once made the compiler rotate accumulators through partially
+    overlapping AGPR ranges (v_mfma a[10:13], ..., a[12:15]) and rows_gemm's results were
+    wrong on gfx950; this guards the compiled ISA against that pattern."""
+    import shutil
+    import subprocess
+    import tempfile
+    import build_native
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not __import__("os").path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    pat = re.compile(r"v_mfma\w*\s+([av])\[(\d+):(\d+)\],\s*[^,]+,\s*[^,]+,\s*([av])\[(\d+):(\d+)\]")
+    checked = 0
+    for src in ("dense_epi.hip", "topk.hip"):
+        with tempfile.TemporaryDirectory() as tmp:
+            out = f"{tmp}/k.s"
+            r = subprocess.run([hipcc, *build_native.CFLAGS, "--cuda-device-only", "-S",
+                                str(build_native.CSRC / src), "-o", out],
+                               capture_output=True, text=True)
+            assert r.returncode == 0, r.stderr[-2000:]
+            for m in pat.finditer(open(out).read()):
+                checked += 1
+                d0, d1, c0, c1 = map(int, (m[2], m[3], m[5], m[6]))
+                same_file = m[1] == m[4]
+                assert not (same_file and (d0, d1) != (c0, c1) and d0 <= c1 and c0 <= d1), \
+                    f"{src}: partially overlapping MFMA accumulators: {m[0]}"
+    assert checked > 500
