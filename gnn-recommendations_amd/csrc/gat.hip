@@ -15,6 +15,8 @@
 // layer-mean accumulator (gat.py:287-288, GNNREC_EPI_* flags).
 #include <math.h>
 
+#include <utility>
+
 #include "gather.h"
 
 namespace gnnrec {
@@ -164,6 +166,72 @@ __global__ __launch_bounds__(kBlock) void gat_kernel(GatParams p) {
   gat_finish<GROUP>(p, r, make_float4(a.x / l, a.y / l, a.z / l, a.w / l), gl);
 }
 
+template <int T>
+__device__ __forceinline__ float row_bcast(float v) {   // DPP row_newbcast: lane T of each 16
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                               0x150 + T, 0xF, 0xF, true));
+}
+
+// One block of 8 neighbours for a 16-lane row group with 4 heads: lane gl computes the logits
+// and weights of ONE neighbour (gl & 7) for TWO heads (2 (gl >> 3), +1) instead of every lane
+// computing all 32, and the weights reach the other lanes by DPP row broadcasts. Every value
+// is produced by the same operations on the same inputs as gat_block's, and each lane applies
+// them in gat_block's order, so the results are bit-identical to the generic path.
+template <int... T>
+__device__ __forceinline__ void gat_apply16(std::integer_sequence<int, T...>, float pa, float pb,
+                                            const float4 (&xv)[8], float (&l)[4],
+                                            float4 (&a)[4]) {
+  // neighbour t = T: head 0/1 weights from lane t, head 2/3 weights from lane t + 8
+  ((l[0] += row_bcast<T>(pa), a[0] = fma4(row_bcast<T>(pa), xv[T], a[0]),
+    l[1] += row_bcast<T>(pb), a[1] = fma4(row_bcast<T>(pb), xv[T], a[1]),
+    l[2] += row_bcast<T + 8>(pa), a[2] = fma4(row_bcast<T + 8>(pa), xv[T], a[2]),
+    l[3] += row_bcast<T + 8>(pb), a[3] = fma4(row_bcast<T + 8>(pb), xv[T], a[3])), ...);
+}
+
+__device__ __forceinline__ void gat_shared_rows16(const GatParams& p, int64_t r, int64_t beg,
+                                                  int64_t end, int gl, const float (&ss)[4],
+                                                  float (&m)[4], float (&l)[4],
+                                                  float4 (&a)[4]) {
+  const int tl = gl & 7;
+  const bool hi = gl >= 8;                       // heads 2, 3 (else 0, 1)
+  const float ssa = hi ? ss[2] : ss[0], ssb = hi ? ss[3] : ss[1];
+  for (int64_t k0 = beg; k0 < end; k0 += 8) {
+    int64_t k = k0 + gl;
+    k = k < end ? k : end - 1;
+    const int cm = p.A.col[k];
+    float4 xv[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int c = __shfl(cm, t, 16);
+      xv[t] = ld4(p.h + (int64_t)c * p.ldh + 4 * gl);
+    }
+    const int co = __shfl(cm, tl, 16);
+    const float4 s4 = ld4(p.s_neigh + (int64_t)co * 4);
+    const bool valid = k0 + tl < end;
+    const float ea = gat_logit2(ssa, hi ? s4.z : s4.x, p.slope, valid);
+    const float eb = gat_logit2(ssb, hi ? s4.w : s4.y, p.slope, valid);
+    float ma = ea, mb = eb;   // block max per head over the 8 lanes of the half-row
+#pragma unroll
+    for (int d = 1; d < 8; d <<= 1) {
+      ma = fmaxf(ma, __shfl_xor(ma, d, 8));
+      mb = fmaxf(mb, __shfl_xor(mb, d, 8));
+    }
+    const float bm[4] = {row_bcast<0>(ma), row_bcast<0>(mb), row_bcast<8>(ma), row_bcast<8>(mb)};
+    float mn[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      mn[h] = fmaxf(m[h], bm[h]);
+      const float sc = gat_exp2(m[h] - mn[h]);
+      l[h] *= sc;
+      a[h] = make_float4(a[h].x * sc, a[h].y * sc, a[h].z * sc, a[h].w * sc);
+      m[h] = mn[h];
+    }
+    const float pa = gat_exp2(ea - (hi ? mn[2] : mn[0]));
+    const float pb = gat_exp2(eb - (hi ? mn[3] : mn[1]));
+    gat_apply16(std::make_integer_sequence<int, 8>{}, pa, pb, xv, l, a);
+  }
+}
+
 // Shared-row mode (head_stride 0, no epilogue: the caller applies W_h afterwards): every
 // head aggregates the same O-wide row, so a row is owned by O/4 lanes that each load ONE
 // float4 of x per neighbour and keep H heads' online-softmax state for it (the generic
@@ -189,6 +257,9 @@ __global__ __launch_bounds__(kBlock) void gat_shared_kernel(GatParams p) {
     a[h] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   static_assert(CH == kSoftBlock, "one softmax block per gather step (same blocks as gat_kernel)");
+  if constexpr (GROUP == 16 && H == 4 && CH == 8) {
+    gat_shared_rows16(p, r, beg, end, gl, ss, m, l, a);
+  } else {
   for (int64_t k0 = beg; k0 < end; k0 += CH) {
     constexpr int PER = (GROUP >= CH) ? 1 : CH / GROUP;
     int cm[PER];
@@ -219,6 +290,7 @@ __global__ __launch_bounds__(kBlock) void gat_shared_kernel(GatParams p) {
       for (int t = 0; t < CH; ++t) E[t] = gat_logit2(ss[h], sn[t][h], p.slope, k0 + t < end);
       gat_block(E, xv, m[h], l[h], a[h]);
     }
+  }
   }
 #pragma unroll
   for (int h = 0; h < H; ++h)
