@@ -95,6 +95,8 @@ class HopTimer:
         e.record()
         self.pairs.append((s, e))
 
+    hop.native_hop = True   # lightgcn_propagate_dist passes the chunk options through it
+
     def durations_ms(self):
         return [s.elapsed_time(e) for s, e in self.pairs]
 
@@ -328,24 +330,29 @@ def main(argv=None) -> int:
     del full
 
     timer = HopTimer()
-    chunks = 1
+    chunks, reserve = 1, 0
 
     def step():
         return lightgcn_propagate_dist(dg, x0_pad, K, hop_fn=timer.hop, work=work,
-                                       overlap_chunks=chunks)
+                                       overlap_chunks=chunks, reserve_cus=reserve)
 
     # Exchange form (N > 1): time whole steps of each candidate before the timed region and
     # keep the fastest (same decision on every rank: max over ranks).
     exchange_info = {"mode": dg.exchange_mode, "overlap_chunks": 1}
     if world > 1:
-        cands = [("allgather", 1)]
+        # (mode, overlap chunks, CUs a chunk kernel leaves to the concurrent RCCL kernels)
+        cands = [("allgather", 1, 0)]
         if not bool(dg.needs.all()) and a.exchange in ("auto", "p2p"):
-            cands = ([] if a.exchange == "p2p" else cands) + [("p2p", 1), ("p2p", 4), ("p2p", 8)]
+            cands = ([] if a.exchange == "p2p" else cands) + [
+                ("p2p", 1, 0), ("p2p", 4, 0), ("p2p", 8, 0), ("p2p", 4, 16), ("p2p", 8, 16)]
         elif a.exchange == "p2p":
-            cands = [("p2p", 1)]
+            cands = [("p2p", 1, 0)]
+
+        def cname(c):
+            return f"{c[0]}_x{c[1]}" + (f"_r{c[2]}" if c[2] else "") + "_ms"
         tried = {}
-        for mode, ch in cands:
-            dg.exchange_mode, chunks = mode, ch
+        for cand in cands:
+            dg.exchange_mode, chunks, reserve = cand
             step()
             torch.cuda.synchronize()
             dist.barrier()
@@ -355,10 +362,11 @@ def main(argv=None) -> int:
             torch.cuda.synchronize()
             tt = torch.tensor([(time.perf_counter() - t0) / 3 * 1e3], dtype=torch.float64, device=device)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            tried[f"{mode}_x{ch}_ms"] = float(tt.item())
-        best = min(cands, key=lambda c: tried[f"{c[0]}_x{c[1]}_ms"])
-        dg.exchange_mode, chunks = best
-        exchange_info = {"mode": best[0], "overlap_chunks": best[1], "candidates_ms_per_step": tried}
+            tried[cname(cand)] = float(tt.item())
+        best = min(cands, key=lambda c: tried[cname(c)])
+        dg.exchange_mode, chunks, reserve = best
+        exchange_info = {"mode": best[0], "overlap_chunks": best[1], "reserved_cus": best[2],
+                         "candidates_ms_per_step": tried}
 
     for _ in range(a.warmup):
         step()
@@ -444,7 +452,10 @@ def main(argv=None) -> int:
                 "nnz": int(nnz_total), "n_nodes": N, "n_layers": K, "dim": d,
                 "parallelism": f"dst-row shards x{world}" + (
                     f" + per-hop RCCL exchange ({exchange_info['mode']}, "
-                    f"{exchange_info['overlap_chunks']} overlap chunks)" if world > 1 else ""),
+                    f"{exchange_info['overlap_chunks']} overlap chunks"
+                    + (f", {exchange_info['reserved_cus']} CUs left to RCCL"
+                       if exchange_info.get('reserved_cus') else "") + ")"
+                    if world > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm",

@@ -68,15 +68,24 @@ TILED_BALANCE_PASSES = True
 TILED_MEET_US = 200
 
 
-def _tiled_rows_per_block(n_rows: int, device) -> int:
+def _tiled_rows_per_block(n_rows: int, device, reserve_cus: int = 0) -> int:
+    """Rows per block so every pass of the persistent grid is full. reserve_cus > 0: size a
+    single-pass operand for cus - reserve_cus blocks, so the launch grid (one workgroup per
+    block, at most one per CU) leaves that many CUs free for kernels that run beside it
+    (the exchange of overlapped multi-GPU chunks)."""
     if not TILED_BALANCE_PASSES:
         return TILED_MAX_ROWS
     cus = torch.cuda.get_device_properties(device).multi_processor_count
+    if 0 < reserve_cus < cus:
+        eff = cus - int(reserve_cus)
+        if n_rows <= eff * TILED_MAX_ROWS:
+            return max(1, -(-n_rows // eff))
     passes = max(1, -(-n_rows // (cus * TILED_MAX_ROWS)))
     return min(TILED_MAX_ROWS, -(-n_rows // (passes * cus)))
 
 
-def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None):
+def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None,
+                   reserve_cus: int = 0):
     """The column-ordered plan spmm_into would use for (adj, x), or None (CSR kernel)."""
     if (not TILED_HOP or x_mask is not None or y_active is not None or x.shape[1] % 32
             or adj.n_rows < max(TILED_MIN_ROWS, 1) or adj.nnz == 0
@@ -84,7 +93,8 @@ def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None):
             or x.shape[0] * x.shape[1] * 4 < TILED_MIN_TABLE_BYTES
             or adj.max_degree() > TILED_MAX_DEGREE):
         return None
-    return adj.tiled_plan(rows_per_block=_tiled_rows_per_block(adj.n_rows, x.device))
+    return adj.tiled_plan(rows_per_block=_tiled_rows_per_block(adj.n_rows, x.device,
+                                                               reserve_cus))
 
 
 def _heavy_args(adj: CsrGraph, x: torch.Tensor, heavy_threshold: int):
@@ -104,12 +114,14 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
               self_rows: Optional[torch.Tensor] = None, acc: Optional[torch.Tensor] = None,
               acc_div: float = 1.0, heavy_threshold: Optional[int] = None,
               x_mask: Optional[torch.Tensor] = None,
-              y_active: Optional[torch.Tensor] = None, meet_us: Optional[int] = None) -> None:
+              y_active: Optional[torch.Tensor] = None, meet_us: Optional[int] = None,
+              reserve_cus: int = 0) -> None:
     """y = A x with an optional fused layer-mean epilogue (gnnrec_spmm_csr_masked_f32: rows
     longer than `heavy_threshold` run on the workgroup-per-row kernel; rows of x whose
     `x_mask` byte is 0 are all-zero and are not gathered — same bits; destination rows whose
     `y_active` byte is 0 are not computed — y is +0 there, or the true value). `meet_us`: the
-    column-ordered kernel's pass-start meeting bound (None: TILED_MEET_US)."""
+    column-ordered kernel's pass-start meeting bound (None: TILED_MEET_US); `reserve_cus`: its
+    single-pass grid leaves that many CUs free (_tiled_rows_per_block)."""
     _require_device(adj, x, y, self_rows, acc)
     if x_mask is not None and (x_mask.dtype != torch.uint8 or x_mask.device != x.device
                                or x_mask.numel() < adj.shape[1]):
@@ -123,7 +135,7 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
                                  or y_active.numel() < adj.n_rows):
         raise ValueError("y_active must be a uint8 tensor on x's device with a byte per "
                          "destination row")
-    plan = tiled_plan_for(adj, x, x_mask, y_active)
+    plan = tiled_plan_for(adj, x, x_mask, y_active, reserve_cus)
     if plan is not None:
         spmm_tiled_into(adj, x, y, plan, epi=epi, self_rows=self_rows, acc=acc, acc_div=acc_div,
                         meet_us=meet_us)

@@ -102,6 +102,13 @@ def _work(rank, world, port, kind, exchange, q):
                         assert F.tiled_plan_for(dg.shard.row_slice(c0, min(c1, dg.n_local)),
                                                 x0p) is not None
                 mine = lightgcn_propagate_dist(dg, x0p, 3, overlap_chunks=3)
+                # chunks sized to leave 16 CUs to the exchange: one pass of <= cus - 16 blocks,
+                # the same bits
+                cus = torch.cuda.get_device_properties(dev).multi_processor_count
+                sl = dg.shard.row_slice(0, min(dg.chunk_bounds(3)[0][1], dg.n_local))
+                assert F.tiled_plan_for(sl, x0p, reserve_cus=16)["n_blocks"] <= cus - 16
+                again = lightgcn_propagate_dist(dg, x0p, 3, overlap_chunks=3, reserve_cus=16)
+                assert torch.equal(again, mine), "reserve_cus changed the result"
             elif kind == "ngcf_gs":
                 mine = ngcf_forward_dist(dg, m, x0p)
             else:
