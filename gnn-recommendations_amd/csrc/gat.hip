@@ -330,27 +330,49 @@ __global__ __launch_bounds__(kBlock) void gat_partial_kernel(GatParams p, GatSpl
   }
 }
 
-// Heavy rows, pass 2: merge the segments of each heavy row (max-rescaled sums), finish.
+// Heavy rows, pass 2: merge the segments of each heavy row (max-rescaled sums), finish. One
+// workgroup per heavy row: its NG = 256 / GROUP row groups each merge a strided subset of
+// the row's segments, then group 0 merges the NG partials (the longest power-law rows have
+// hundreds of segments; one group walking them all was the serial tail of the launch).
 template <int F>
 __global__ __launch_bounds__(kBlock) void gat_merge_kernel(GatParams p, GatSplit sp) {
   constexpr int GROUP = F / 4;
-  constexpr int RPW = 64 / GROUP;
-  const int lane = threadIdx.x & 63;
-  const int gl = lane % GROUP;
-  const int64_t h = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
-  if (h >= sp.n_heavy) return;
+  constexpr int NG = kBlock / GROUP;
+  __shared__ float s_m[NG][GROUP], s_l[NG][GROUP];
+  __shared__ float4 s_a[NG][GROUP];
+  const int64_t h = blockIdx.x;
+  const int g = threadIdx.x / GROUP, gl = threadIdx.x % GROUP;
   const int hl = p.o_dim / 4, head = gl / hl;
   const float* mm = sp.work + sp.n_seg * F;
   const float* ll = mm + sp.n_seg * p.heads;
   const int64_t s0 = sp.heavy_seg_ptr[h], s1 = sp.heavy_seg_ptr[h + 1];
   float M = -INFINITY;
-  for (int64_t s = s0; s < s1; ++s) M = fmaxf(M, mm[s * p.heads + head]);
+  for (int64_t s = s0 + g; s < s1; s += NG) M = fmaxf(M, mm[s * p.heads + head]);
   float L = 0.f;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int64_t s = s0; s < s1; ++s) {
+  for (int64_t s = s0 + g; s < s1; s += NG) {
     const float w = gat_exp2(mm[s * p.heads + head] - M);   // base-2 maxima (gat_block)
     const float4 t = ld4(sp.work + s * F + 4 * gl);
     L = __builtin_fmaf(ll[s * p.heads + head], w, L);
+    a = make_float4(__builtin_fmaf(t.x, w, a.x), __builtin_fmaf(t.y, w, a.y),
+                    __builtin_fmaf(t.z, w, a.z), __builtin_fmaf(t.w, w, a.w));
+  }
+  s_m[g][gl] = M;
+  s_l[g][gl] = L;
+  s_a[g][gl] = a;
+  __syncthreads();
+  if (g != 0) return;
+  M = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < NG; ++q) M = fmaxf(M, s_m[q][gl]);
+  L = 0.f;
+  a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    // a group without segments holds (-inf, 0, 0): weight 0
+    const float w = s_m[q][gl] == -INFINITY ? 0.f : gat_exp2(s_m[q][gl] - M);
+    const float4 t = s_a[q][gl];
+    L = __builtin_fmaf(s_l[q][gl], w, L);
     a = make_float4(__builtin_fmaf(t.x, w, a.x), __builtin_fmaf(t.y, w, a.y),
                     __builtin_fmaf(t.z, w, a.z), __builtin_fmaf(t.w, w, a.w));
   }
@@ -436,7 +458,7 @@ extern "C" int gnnrec_gat_heavy_f32(const int32_t* col, const int64_t* seg_row,
 #define GAT_HEAVY(FF)                                                                          \
   case FF:                                                                                     \
     hipLaunchKernelGGL(gat_partial_kernel<FF>, g(n_seg, FF), dim3(kBlock), 0, s, p, sp);       \
-    hipLaunchKernelGGL(gat_merge_kernel<FF>, g(n_heavy, FF), dim3(kBlock), 0, s, p, sp);       \
+    hipLaunchKernelGGL(gat_merge_kernel<FF>, dim3((unsigned)n_heavy), dim3(kBlock), 0, s, p, sp); \
     break;
     GAT_HEAVY(16) GAT_HEAVY(32) GAT_HEAVY(64) GAT_HEAVY(128) GAT_HEAVY(256)
 #undef GAT_HEAVY
