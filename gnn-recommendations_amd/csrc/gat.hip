@@ -29,6 +29,7 @@ struct GatParams {
                         // head-major; 0: every head reads the same o_dim-wide row)
   const float* s_self;
   const float* s_neigh;
+  int64_t ld_ss, ld_sn;  // row strides of s_self / s_neigh (>= heads)
   int heads, o_dim;
   float slope;
   int mean_heads, apply_elu;
@@ -119,7 +120,7 @@ __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, in
   static_assert(kChunk % kSoftBlock == 0, "a gather step holds whole softmax blocks");
   const int hl = p.o_dim / 4;
   const int head = gl / hl;
-  const float ss = p.s_self[r * p.heads + head];
+  const float ss = p.s_self[r * p.ld_ss + head];
   for (int64_t k0 = beg; k0 < end; k0 += kChunk) {
     constexpr int PER = (GROUP >= kChunk) ? 1 : kChunk / GROUP;
     int cm[PER];
@@ -135,7 +136,7 @@ __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, in
     for (int t = 0; t < kChunk; ++t) {
       const int c = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
       xv[t] = ld4(p.h + (int64_t)c * p.ldh + head * p.head_stride + 4 * (gl - head * hl));
-      sn[t] = p.s_neigh[(int64_t)c * p.heads + head];
+      sn[t] = p.s_neigh[(int64_t)c * p.ld_sn + head];
     }
 #pragma unroll
     for (int b = 0; b < kChunk / kSoftBlock; ++b) {
@@ -206,7 +207,7 @@ __device__ __forceinline__ void gat_shared_rows16(const GatParams& p, int64_t r,
       xv[t] = ld4(p.h + (int64_t)c * p.ldh + 4 * gl);
     }
     const int co = __shfl(cm, tl, 16);
-    const float4 s4 = ld4(p.s_neigh + (int64_t)co * 4);
+    const float4 s4 = ld4(p.s_neigh + (int64_t)co * p.ld_sn);
     const bool valid = k0 + tl < end;
     const float ea = gat_logit2(ssa, hi ? s4.z : s4.x, p.slope, valid);
     const float eb = gat_logit2(ssb, hi ? s4.w : s4.y, p.slope, valid);
@@ -251,7 +252,7 @@ __global__ __launch_bounds__(kBlock) void gat_shared_kernel(GatParams p) {
   float4 a[H];
 #pragma unroll
   for (int h = 0; h < H; ++h) {
-    ss[h] = p.s_self[r * H + h];
+    ss[h] = p.s_self[r * p.ld_ss + h];
     m[h] = -INFINITY;
     l[h] = 0.f;
     a[h] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -276,11 +277,11 @@ __global__ __launch_bounds__(kBlock) void gat_shared_kernel(GatParams p) {
       const int c = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
       xv[t] = ld4(p.h + (int64_t)c * p.ldh + 4 * gl);
       if constexpr (H == 4) {
-        const float4 s4 = ld4(p.s_neigh + (int64_t)c * 4);
+        const float4 s4 = ld4(p.s_neigh + (int64_t)c * p.ld_sn);
         sn[t][0] = s4.x; sn[t][1] = s4.y; sn[t][2] = s4.z; sn[t][3] = s4.w;
       } else {
 #pragma unroll
-        for (int h = 0; h < H; ++h) sn[t][h] = p.s_neigh[(int64_t)c * H + h];
+        for (int h = 0; h < H; ++h) sn[t][h] = p.s_neigh[(int64_t)c * p.ld_sn + h];
       }
     }
 #pragma unroll
@@ -385,7 +386,8 @@ using namespace gnnrec;
 
 extern "C" int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* col, int64_t n_rows,
                                         const float* hfeat, int64_t ldh, int64_t head_stride,
-                                        const float* s_self, const float* s_neigh, int32_t heads,
+                                        const float* s_self, const float* s_neigh, int64_t ld_ss,
+                                        int64_t ld_sn, int32_t heads,
                                         int32_t o_dim,
                                         float slope, int32_t mean_heads, int32_t apply_elu,
                                         float* out, int64_t ldo, int32_t epi, const float* self,
@@ -396,6 +398,7 @@ extern "C" int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* c
   const int F = heads * o_dim;
   const int width = mean_heads ? o_dim : F;
   GNNREC_REQUIRE(row_ptr && col && hfeat && s_self && s_neigh, "gat: null operand");
+  GNNREC_REQUIRE(ld_ss >= heads && ld_sn >= heads, "gat: score row strides must be >= heads");
   GNNREC_REQUIRE(head_stride >= 0 && !(head_stride & 3), "gat: head_stride must be >= 0 and %% 4 == 0");
   GNNREC_REQUIRE(aligned16(hfeat) && !(ldh & 3) && ldh >= (heads - 1) * head_stride + o_dim,
                  "gat: hfeat must be 16-B aligned, ld %% 4 == 0, ld >= (heads-1)*head_stride + o_dim");
@@ -406,12 +409,12 @@ extern "C" int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* c
   GNNREC_REQUIRE(!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) ||
                      (acc && aligned16(acc) && !(ld_acc & 3) && ld_acc >= width),
                  "gat: ACC needs 16-B aligned acc");
-  GatParams p{Csr{row_ptr, col, nullptr, n_rows}, hfeat, ldh, head_stride, s_self, s_neigh, heads, o_dim, slope,
+  GatParams p{Csr{row_ptr, col, nullptr, n_rows}, hfeat, ldh, head_stride, s_self, s_neigh, ld_ss, ld_sn, heads, o_dim, slope,
               mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, max_row_len};
   hipStream_t s = as_hip(stream);
   auto grid = [&](int f) { return dim3((unsigned)ceil_div(n_rows, (64 / (f / 4)) * (kBlock / 64))); };
   const bool shared_fast = head_stride == 0 && heads == 4 && !mean_heads && !apply_elu && epi == 0 &&
-                           (o_dim == 16 || o_dim == 32 || o_dim == 64) && aligned16(s_neigh) &&
+                           (o_dim == 16 || o_dim == 32 || o_dim == 64) && aligned16(s_neigh) && !(ld_sn & 3) &&
                            aligned16(out);
   if (shared_fast) {
     switch (o_dim) {
@@ -436,7 +439,8 @@ extern "C" int gnnrec_gat_heavy_f32(const int32_t* col, const int64_t* seg_row,
                                     const int64_t* seg_beg, const int64_t* seg_end, int64_t n_seg,
                                     const int64_t* heavy_rows, const int64_t* heavy_seg_ptr,
                                     int64_t n_heavy, float* work, const float* hfeat, int64_t ldh,
-                                    int64_t head_stride, const float* s_self, const float* s_neigh, int32_t heads,
+                                    int64_t head_stride, const float* s_self, const float* s_neigh,
+                                    int64_t ld_ss, int64_t ld_sn, int32_t heads,
                                     int32_t o_dim, float slope, int32_t mean_heads,
                                     int32_t apply_elu, float* out, int64_t ldo, int32_t epi,
                                     const float* self, int64_t ld_self, float* acc, int64_t ld_acc,
@@ -448,8 +452,9 @@ extern "C" int gnnrec_gat_heavy_f32(const int32_t* col, const int64_t* seg_row,
                      hfeat && s_self && s_neigh && aligned16(work) && aligned16(hfeat) && !(ldh & 3) &&
                      head_stride >= 0 && !(head_stride & 3),
                  "gat_heavy: null or misaligned operand");
+  GNNREC_REQUIRE(ld_ss >= heads && ld_sn >= heads, "gat_heavy: score row strides must be >= heads");
   const int F = heads * o_dim;
-  GatParams p{Csr{nullptr, col, nullptr, 0}, hfeat, ldh, head_stride, s_self, s_neigh, heads, o_dim, slope,
+  GatParams p{Csr{nullptr, col, nullptr, 0}, hfeat, ldh, head_stride, s_self, s_neigh, ld_ss, ld_sn, heads, o_dim, slope,
               mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, 0};
   GatSplit sp{seg_row, seg_beg, seg_end, n_seg, heavy_rows, heavy_seg_ptr, n_heavy, work};
   hipStream_t s = as_hip(stream);

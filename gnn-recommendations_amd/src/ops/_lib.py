@@ -17,7 +17,7 @@ import torch  # noqa: F401  (load order: torch's HIP runtime first)
 
 _PKG_ROOT = Path(__file__).resolve().parents[2]
 LIB_PATH = Path(os.environ.get("GNNREC_LIB", _PKG_ROOT / "lib" / "libgnnrec.so"))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # gnnrec.h epilogue flags
 EPI_ACC_INIT = 1
@@ -72,11 +72,12 @@ _SIGNATURES = {
                                    _p, _i64, _i32, _f32, _f32, _p],
     "gnnrec_rows_gemm_f32": [_i64, _p, _i64, _i32, _p, _i32, _p, _i64, _i32, _i32, _p, _i64,
                              _p, _i64, _f32, _p],
-    "gnnrec_gat_aggregate_f32": [_p, _p, _i64, _p, _i64, _i64, _p, _p, _i32, _i32, _f32, _i32,
-                                 _i32, _p, _i64, _i32, _p, _i64, _p, _i64, _f32, _i64, _p],
+    "gnnrec_gat_aggregate_f32": [_p, _p, _i64, _p, _i64, _i64, _p, _p, _i64, _i64, _i32, _i32,
+                                 _f32, _i32, _i32, _p, _i64, _i32, _p, _i64, _p, _i64, _f32, _i64,
+                                 _p],
     "gnnrec_gat_heavy_f32": [_p, _p, _p, _p, _i64, _p, _p, _i64, _p, _p, _i64, _i64, _p, _p,
-                             _i32, _i32, _f32, _i32, _i32, _p, _i64, _i32, _p, _i64, _p, _i64,
-                             _f32, _p],
+                             _i64, _i64, _i32, _i32, _f32, _i32, _i32, _p, _i64, _i32, _p, _i64,
+                             _p, _i64, _f32, _p],
     "gnnrec_score_topk_f32": [_p, _i64, _i64, _p, _i64, _i64, _i32, _p, _p, _i32, _p, _p, _p],
     "gnnrec_score_topk_split_f32": [_p, _i64, _i64, _p, _i64, _i64, _i32, _p, _p, _i32, _i32,
                                     _p, _p, _p, _p, _p],

@@ -448,8 +448,10 @@ def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh:
     shared_rows: `h` is ONE [N, o_dim] table every head aggregates (head_stride 0), e.g. the
     layer input x when W_h is applied after the aggregation."""
     h = _rowmajor(h)
-    s_self = s_self.contiguous()
-    s_neigh = s_neigh.contiguous()
+    # score tables are read in place with their row strides (e.g. columns of the projection
+    # output); only a column-strided view is compacted
+    s_self = s_self if s_self.stride(1) == 1 else s_self.contiguous()
+    s_neigh = s_neigh if s_neigh.stride(1) == 1 else s_neigh.contiguous()
     _require_device(adj, h, self_rows, acc)
     if h.shape[1] < (o_dim if shared_rows else heads * o_dim):
         raise ValueError("h is narrower than the aggregated rows")
@@ -458,7 +460,8 @@ def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh:
     if out is None and not (epi & EPI_NO_Y):
         out = torch.empty((adj.n_rows, width), dtype=torch.float32, device=h.device)
     plan = adj.heavy_plan(heavy_threshold, GAT_SEGMENT) if heavy_threshold > 0 else None
-    common = (ptr(h), h.stride(0), head_stride, ptr(s_self), ptr(s_neigh), int(heads),
+    common = (ptr(h), h.stride(0), head_stride, ptr(s_self), ptr(s_neigh), s_self.stride(0),
+              s_neigh.stride(0), int(heads),
               int(o_dim), float(slope), int(mean_heads), int(apply_elu), ptr(out),
               out.stride(0) if out is not None else width, int(epi), ptr(self_rows),
               self_rows.stride(0) if self_rows is not None else width, ptr(acc),

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GNNREC_ABI_VERSION 4
+#define GNNREC_ABI_VERSION 5
 
 typedef struct ihipStream_t* gnnrec_stream_t;
 
@@ -261,7 +261,8 @@ int gnnrec_dense_transform_f32(int64_t n_rows, const float* n, int64_t ldn, floa
  * table of the per-head W_h x; head_stride = 0 lets every head aggregate the same row (the
  * layer input x, with W_h applied by the caller afterwards: sum_j a_j W_h x_j =
  * W_h sum_j a_j x_j — the head-averaged last layer then gathers o_dim instead of heads*o_dim
- * floats per neighbour). s_self / s_neigh: [N, heads] (ld = heads).
+ * floats per neighbour). s_self / s_neigh: [N, heads] with row strides ld_ss / ld_sn
+ * (>= heads; e.g. columns of the projection's [N, heads*o_dim + 2*heads] output in place).
  * mean_heads = 0: out[r] = cat_h o[r,h,:] ([n_rows, heads*o_dim]); 1: out[r] = mean_h
  * o[r,h,:] ([n_rows, o_dim]). apply_elu: out = ELU(out) (alpha 1). epi: the ACC_* flags of
  * gnnrec_spmm_csr_f32 applied to the (ELU'd) output with `self` = the layer input rows.
@@ -271,8 +272,8 @@ int gnnrec_dense_transform_f32(int64_t n_rows, const float* n, int64_t ldn, floa
  * gnnrec_gat_heavy_f32 (power-law degree buckets; 0 = every row here). */
 int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* col, int64_t n_rows,
                              const float* hfeat, int64_t ldh, int64_t head_stride,
-                             const float* s_self,
-                             const float* s_neigh, int32_t heads, int32_t o_dim, float slope,
+                             const float* s_self, const float* s_neigh, int64_t ld_ss,
+                             int64_t ld_sn, int32_t heads, int32_t o_dim, float slope,
                              int32_t mean_heads, int32_t apply_elu, float* out, int64_t ldo,
                              int32_t epi, const float* self, int64_t ld_self, float* acc,
                              int64_t ld_acc, float acc_div, int64_t max_row_len,
@@ -287,8 +288,9 @@ int gnnrec_gat_heavy_f32(const int32_t* col, const int64_t* seg_row, const int64
                          const int64_t* seg_end, int64_t n_seg, const int64_t* heavy_rows,
                          const int64_t* heavy_seg_ptr, int64_t n_heavy, float* work,
                          const float* hfeat, int64_t ldh, int64_t head_stride,
-                         const float* s_self, const float* s_neigh, int32_t heads,
-                         int32_t o_dim, float slope, int32_t mean_heads, int32_t apply_elu,
+                         const float* s_self, const float* s_neigh, int64_t ld_ss,
+                         int64_t ld_sn, int32_t heads, int32_t o_dim, float slope,
+                         int32_t mean_heads, int32_t apply_elu,
                          float* out, int64_t ldo, int32_t epi, const float* self,
                          int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
                          gnnrec_stream_t stream);

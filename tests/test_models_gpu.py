@@ -220,3 +220,24 @@ def test_edge_specific_transport_native(cuda):
                              torch.from_numpy(f["edge_type"]).to(cuda))
     assert out.is_cuda
     np.testing.assert_allclose(out.cpu().numpy(), f["y"], rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("shared", [False, True])
+def test_gat_scores_read_in_place_with_row_strides(cuda, shared):
+    """s_self / s_neigh as column views of a wider table (the projection's output) give the
+    same bits as compacted copies, on the normal and the heavy-row path."""
+    from src.ops import functional as F
+    rng = np.random.default_rng(4)
+    u = rng.integers(0, 300, 6000)
+    i = np.minimum(rng.zipf(1.3, 6000) - 1, 199)
+    g = CsrGraph.from_interactions(u, i, 300, 200).to(cuda)
+    n, H, o = g.shape[0], 4, (64 if shared else 16)
+    feat = torch.randn(n, o if shared else H * o, device=cuda)
+    wide = torch.randn(n, 72, device=cuda)
+    ss, sn = wide[:, 64:68], wide[:, 68:72]
+    for heavy in (0, 64):
+        got = F.gat_aggregate(g, feat, ss, sn, H, o, 0.2, shared_rows=shared, heavy_threshold=heavy)
+        ref = F.gat_aggregate(g, feat, ss.contiguous(), sn.contiguous(), H, o, 0.2,
+                              shared_rows=shared, heavy_threshold=heavy)
+        np.testing.assert_array_equal(got.cpu().numpy().view(np.uint32),
+                                      ref.cpu().numpy().view(np.uint32))
