@@ -359,7 +359,9 @@ def gat_forward_dist(dg: DistributedGraph, model, x0_pad: torch.Tensor, *,
     L = len(model.layers)
     for k, layer in enumerate(model.layers, start=1):
         feat, ss, sn = layer.native_inputs(x_local)
-        featp, snp = _exchanged(dg, feat), _exchanged(dg, sn.contiguous())
+        # scores travel as their (strided) projection columns: no compaction copy, and on one
+        # device the kernel reads them next to the gathered rows
+        featp, snp = _exchanged(dg, feat), _exchanged(dg, sn)
         epi = EPI_ACC_INIT if k == 1 else EPI_ACC_ADD
         if k == L:
             epi |= EPI_ACC_DIV | EPI_NO_Y   # only the layer mean is read after it
