@@ -45,6 +45,7 @@ sys.path.insert(0, str(ROOT))
 
 from src.ops import CsrGraph  # noqa: E402
 from src.ops import functional as F  # noqa: E402
+from src.ops._lib import EPI_ACC_ADD, EPI_ACC_INIT, EPI_ACC_X, EPI_NO_Y  # noqa: E402
 from src.ops.distributed import (DistributedGraph, lightgcn_propagate_dist,  # noqa: E402
                                  make_work, _native_hop)
 
@@ -108,19 +109,25 @@ def hop_bytes_alg(nnz: int, rows: int, src: int, d: int) -> int:
     return 8 * nnz + 8 * (rows + 1) + 4 * d * src + 4 * d * rows
 
 
-def hop_bytes(nnz: int, rows: int, src: int, d: int, K: int, world: int) -> list:
+def hop_bytes(nnz: int, rows: int, src: int, d: int, K: int, world: int,
+              deferred: bool = False) -> list:
     """Bytes of each hop launch as the kernel is used here, fused layer-mean epilogue
-    included: CSR once, every distinct source row once, the hop output written once (not
-    on the last hop), the layer-mean accumulator written every hop and read from hop 2 on;
-    rank-local self rows read on hop 1 when sharded (with one GPU they are part of the
-    gathered table already)."""
+    included: CSR once, every distinct source row once, then the epilogue's row transfers of
+    the hop schedule (F.lightgcn_hop_schedule): the hop output unless NO_Y, the layer-mean
+    inputs it reads (x0 on INIT, the acc rows on ADD, its own input rows on ACC_X) and the acc
+    write. Eager (N > 1): y, acc written every hop and read from hop 2 on, rank-local x0 rows
+    read on hop 1 when sharded (with one GPU they are part of the gathered table already,
+    unless the deferred hop 3 reads them again as its self rows)."""
     out = []
-    for k in range(1, K + 1):
+    row = 4 * d * rows
+    for k, (_, _, epi) in enumerate(F.lightgcn_hop_schedule(K, deferred), start=1):
         b = 8 * nnz + 8 * (rows + 1) + 4 * d * src
-        b += 4 * d * rows * (k < K)          # y
-        b += 4 * d * rows * (k >= 2)         # acc read
-        b += 4 * d * rows                    # acc write
-        b += 4 * d * rows * (k == 1 and world > 1)  # x0 self rows
+        b += row * (not (epi & EPI_NO_Y))
+        if epi & (EPI_ACC_INIT | EPI_ACC_ADD):
+            b += row                                           # acc write
+            b += row * bool(epi & EPI_ACC_ADD)
+            b += row * bool(epi & EPI_ACC_X)
+            b += row * bool((epi & EPI_ACC_INIT) and (world > 1 or k > 1))
         out.append(b)
     return out
 
@@ -391,7 +398,9 @@ def main(argv=None) -> int:
 
     durs = timer.durations_ms()
     alg_bytes = float(hop_bytes_alg(dg.shard.nnz, dg.n_local, src, d))
-    per_hop = hop_bytes(dg.shard.nnz, dg.n_local, src, d, K, world)
+    # one device + column-ordered kernel: the deferred layer mean (lightgcn_propagate_dist)
+    per_hop = hop_bytes(dg.shard.nnz, dg.n_local, src, d, K, world,
+                        deferred=(world == 1 and tiled and K >= 2))
     launch_bytes = float(np.mean(per_hop))
     # kernel time per hop (= per launch at N=1; the sum of its chunk launches when the hop is
     # split into overlap chunks)
@@ -475,6 +484,8 @@ def main(argv=None) -> int:
                            f"spmm_vec_kernel<{d}> (one launch per hop)"),
                 "launch_ms": launch_ms,
                 "bytes_per_launch_with_fused_epilogue": launch_bytes,
+                "layer_mean_schedule": "deferred (hop K forms the mean)"
+                if (world == 1 and tiled and K >= 2) else "eager (every hop's epilogue)",
                 # the same launch priced by its MEASURED memory-side traffic (PMC): how close
                 # the random row gather runs to the fabric/HBM rate
                 "traffic_gbps": (traffic / (launch_ms * 1e-3) / 1e9) if traffic else None,

@@ -386,6 +386,11 @@ extern "C" int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t*
                  "spmm: ACC needs acc");
   GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_DIV) || (epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)),
                  "spmm: ACC_DIV without ACC_INIT/ACC_ADD");
+  if ((epi & GNNREC_EPI_ACC_X) ||
+      ((epi & GNNREC_EPI_ACC_INIT) && (epi & GNNREC_EPI_ACC_ADD))) {
+    set_error("spmm: ACC_X and ACC_INIT|ACC_ADD are epilogues of gnnrec_spmm_tiled_f32 only");
+    return GNNREC_EUNSUPPORTED;
+  }
   GNNREC_REQUIRE(heavy_threshold >= 0 && n_heavy >= 0, "spmm: negative heavy_threshold/n_heavy");
   const bool split = heavy_threshold > 0;
   if (split) {

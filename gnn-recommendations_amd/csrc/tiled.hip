@@ -54,6 +54,7 @@ constexpr int kGroup = 8;                         // steps whose reads precede t
 #define GNNREC_TILED_EPI_BATCH 20
 #endif
 constexpr int kEpiBatch = GNNREC_TILED_EPI_BATCH;   // epilogue rows per half-wave, loads in flight
+constexpr int kEpiBatch3 = 10;   // the same with two or three base inputs per row (VGPRs)
 static_assert(kHalf == 16, "a half-chunk is one DPP row of 16 lanes");
 static_assert(kHalf == 2 * kGroup, "a half-chunk is applied as two groups");
 static_assert(GNNREC_TILED_MAX_ROWS < kRowMask, "row field is 11 bits (row R = scratch)");
@@ -190,41 +191,58 @@ __device__ __forceinline__ void tiled_apply(float* acc, uint32_t f4, const Tiled
 }
 
 // Pass-end epilogue of one half-wave: its rows i = rl + 32q of the block (rl = 2 * wave +
-// half), kEpiBatch at a time with every load of a batch issued before the first use. All
-// offsets are 32-bit rows of buffers based at the block's first row whose ranges end at the
-// last valid row: loads past it return 0 and stores are dropped, so there is no branch (a
-// branch around a load makes the compiler wait for it in place). A null ry: no y output.
-// ACC: acc_out = (base + y) [/ div] with base = x0 (ACC_INIT) or the running sum.
-template <bool ACC>
+// half), B at a time with every load of a batch issued before the first use. All offsets are
+// 32-bit rows of buffers based at the block's first row whose ranges end at the last valid
+// row: loads past it return 0 and stores are dropped, so there is no branch (a branch around
+// a load makes the compiler wait for it in place). A null ry: no y output.
+// NB base inputs (the layer-mean terms before this hop, in layer order): acc_out =
+// (((b0 [+ b1]) [+ b2]) + y) [/ div] — b0 = x0 (ACC_INIT) or the running sum (ACC_ADD);
+// INIT|ADD: b0 = x0, b1 = the acc rows (an earlier layer parked there); ACC_X: the hop's
+// input row x[r] (the previous layer) last. NB = 0: y only.
+template <int NB, int B>
 __device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, uint32_t f4,
                                                __amdgpu_buffer_rsrc_t ry, uint32_t ly,
-                                               __amdgpu_buffer_rsrc_t rb, uint32_t lb,
+                                               __amdgpu_buffer_rsrc_t rb0, uint32_t lb0,
+                                               __amdgpu_buffer_rsrc_t rb1, uint32_t lb1,
+                                               __amdgpu_buffer_rsrc_t rb2, uint32_t lb2,
                                                __amdgpu_buffer_rsrc_t ra, uint32_t la,
                                                bool div, float acc_div) {
   constexpr int kStride = 2 * kTiledWaves;
-  for (int i0 = rl; i0 - (rl & 1) < R; i0 += kStride * kEpiBatch) {
+  const __amdgpu_buffer_rsrc_t rb[3] = {rb0, rb1, rb2};
+  const uint32_t lb[3] = {lb0, lb1, lb2};
+  for (int i0 = rl; i0 - (rl & 1) < R; i0 += kStride * B) {
     // per-row offsets advance by a stride; the opaque copy keeps the compiler from hoisting
-    // kEpiBatch x 3 of them out of the persistent loop (they would spill)
-    uint32_t ol = (uint32_t)i0, ob = (uint32_t)i0 * lb + f4;
-    asm volatile("" : "+v"(ol), "+v"(ob));
-    float a[kEpiBatch], base[kEpiBatch];
+    // B x 3 of them out of the persistent loop (they would spill)
+    uint32_t ol = (uint32_t)i0, ob[3];
+    asm volatile("" : "+v"(ol));
 #pragma unroll
-    for (int q = 0; q < kEpiBatch; ++q) {
+    for (int j = 0; j < NB; ++j) {
+      ob[j] = (uint32_t)i0 * lb[j] + f4;
+      asm volatile("" : "+v"(ob[j]));
+    }
+    float a[B], base[NB > 0 ? NB : 1][B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
       a[q] = acc[min(ol, (uint32_t)R) * kSlice + (f4 >> 2)];
       ol += kStride;
-      if (ACC) {
-        base[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, ob, 0, 0));
-        ob += kStride * lb;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        base[j][q] =
+            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb[j], ob[j], 0, 0));
+        ob[j] += kStride * lb[j];
       }
     }
     uint32_t oy = (uint32_t)i0 * ly + f4, oa = (uint32_t)i0 * la + f4;
     asm volatile("" : "+v"(oy), "+v"(oa));
 #pragma unroll
-    for (int q = 0; q < kEpiBatch; ++q) {
+    for (int q = 0; q < B; ++q) {
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, a[q]), ry, oy, 0, 0);
       oy += kStride * ly;
-      if (ACC) {
-        float bsum = base[q] + a[q];
+      if (NB > 0) {
+        float bsum = base[0][q];
+#pragma unroll
+        for (int j = 1; j < NB; ++j) bsum = bsum + base[j][q];
+        bsum = bsum + a[q];
         if (div) bsum = bsum / acc_div;
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, bsum), ra, oa, 0, 0);
         oa += kStride * la;
@@ -319,17 +337,28 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     const int rl = 2 * w + half;
     const __amdgpu_buffer_rsrc_t ry = rows_rsrc((epi & GNNREC_EPI_NO_Y) ? nullptr : y, r0, ldy,
                                                 slice, nv);
-    if (epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) {
-      const bool init = (epi & GNNREC_EPI_ACC_INIT) != 0;
-      const float* bsrc = init ? self : accg;
-      const int64_t ldb = init ? ld_self : ld_acc;
-      tiled_epilogue<true>(acc, R, rl, f4, ry, (uint32_t)ldy * 4,
-                           rows_rsrc(bsrc, r0, ldb, slice, nv), (uint32_t)ldb * 4,
-                           rows_rsrc(accg, r0, ld_acc, slice, nv), (uint32_t)ld_acc * 4,
-                           (epi & GNNREC_EPI_ACC_DIV) != 0, acc_div);
-    } else {
-      tiled_epilogue<false>(acc, R, rl, f4, ry, (uint32_t)ldy * 4, ry, 0, ry, 0, false, 1.f);
-    }
+    // base inputs in layer order: x0 (INIT), the acc rows (ADD), the input rows (ACC_X)
+    const bool init = (epi & GNNREC_EPI_ACC_INIT) != 0, add = (epi & GNNREC_EPI_ACC_ADD) != 0,
+               xin = (epi & GNNREC_EPI_ACC_X) != 0;
+    const int nb = (int)init + (int)add + (int)xin;
+    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(init ? self : nullptr, r0, ld_self, slice, nv);
+    const __amdgpu_buffer_rsrc_t racc = rows_rsrc(nb ? accg : nullptr, r0, ld_acc, slice, nv);
+    const __amdgpu_buffer_rsrc_t rx = rows_rsrc(xin ? x : nullptr, r0, row_bytes / 4, slice, nv);
+    const uint32_t ls = (uint32_t)ld_self * 4, la = (uint32_t)ld_acc * 4, ly = (uint32_t)ldy * 4;
+    const __amdgpu_buffer_rsrc_t rb0 = init ? rs : racc, rb1 = (init && add) ? racc : rx;
+    const uint32_t lb0 = init ? ls : la, lb1 = (init && add) ? la : row_bytes;
+    const bool div = (epi & GNNREC_EPI_ACC_DIV) != 0;
+#define GNNREC_TILED_EPI(NB, B, DIV) \
+  tiled_epilogue<NB, B>(acc, R, rl, f4, ry, ly, rb0, lb0, rb1, lb1, rx, row_bytes, racc, la, DIV, acc_div)
+    if (nb == 0)
+      GNNREC_TILED_EPI(0, kEpiBatch, false);
+    else if (nb == 1)
+      GNNREC_TILED_EPI(1, kEpiBatch, div);
+    else if (nb == 2)
+      GNNREC_TILED_EPI(2, kEpiBatch3, div);
+    else
+      GNNREC_TILED_EPI(3, kEpiBatch3, div);
+#undef GNNREC_TILED_EPI
     __syncthreads();
   }
   // finished: never hold the group back again
@@ -629,6 +658,11 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
                  "spmm_tiled: ACC_INIT needs self");
   GNNREC_REQUIRE(!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) || (acc && ld_acc >= d),
                  "spmm_tiled: ACC needs acc");
+  GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_X) ||
+                     ((epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) && x_rows >= n_rows),
+                 "spmm_tiled: ACC_X needs ACC_INIT or ACC_ADD and a square operand");
+  GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_DIV) || (epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)),
+                 "spmm_tiled: ACC_DIV needs ACC_INIT or ACC_ADD");
   GNNREC_REQUIRE(meet_us >= 0 && meet_us <= 100000, "spmm_tiled: meet_us must be in [0, 1e5]");
   constexpr int64_t kMaxLd = ((int64_t)1 << 32) / (4 * 4096);   // epilogue row offsets: 32-bit
   GNNREC_REQUIRE(ldy <= kMaxLd && ld_self <= kMaxLd && ld_acc <= kMaxLd,

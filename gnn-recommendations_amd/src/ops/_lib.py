@@ -17,13 +17,14 @@ import torch  # noqa: F401  (load order: torch's HIP runtime first)
 
 _PKG_ROOT = Path(__file__).resolve().parents[2]
 LIB_PATH = Path(os.environ.get("GNNREC_LIB", _PKG_ROOT / "lib" / "libgnnrec.so"))
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 # gnnrec.h epilogue flags
 EPI_ACC_INIT = 1
 EPI_ACC_ADD = 2
 EPI_ACC_DIV = 4
 EPI_NO_Y = 8
+EPI_ACC_X = 16
 # column-ordered hop plan layout (include/gnnrec.h GNNREC_TILED_*)
 TILED_WAVES = 16
 TILED_CHUNK = 32

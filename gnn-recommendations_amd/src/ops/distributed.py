@@ -224,8 +224,23 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
     if work is None:
         work = make_work(dg, d, x0_pad.device)
     Y, Xa, Xb = work
-    acc = torch.empty((dg.n_local, d), dtype=torch.float32, device=x0_pad.device)
     self_rows = dg.local_slice(x0_pad)
+    from .functional import lightgcn_hop_schedule, tiled_plan_for
+    if (dg.world == 1 and native and masks is None and n_layers >= 2
+            and tiled_plan_for(dg.shard, x0_pad) is not None):
+        # one device, column-ordered kernel: the layer mean formed on the last hop from the
+        # parked layers (lightgcn_hop_schedule, deferred) — 6 instead of 8 epilogue row
+        # transfers at K = 3, same bits. acc is padded to the gather table's rows, since hop 2
+        # gathers from it (y1 is parked there).
+        acc_full = torch.empty((Xa.shape[0], d), dtype=torch.float32, device=x0_pad.device)
+        acc_full[dg.n_local:].zero_()
+        acc = acc_full[:dg.n_local]
+        bufs = {"x0": x0_pad, "acc": acc_full, "a": Xa, "b": Xb, None: None}
+        for xn, yn, epi in lightgcn_hop_schedule(n_layers, deferred=True):
+            hop(dg.shard, bufs[xn], None if yn is None else bufs[yn][:dg.n_local], epi=epi,
+                self_rows=self_rows, acc=acc, acc_div=float(n_layers + 1))
+        return acc
+    acc = torch.empty((dg.n_local, d), dtype=torch.float32, device=x0_pad.device)
     if n_layers == 0:
         acc.copy_(self_rows)
     x_in = x0_pad

@@ -14,7 +14,7 @@ from typing import Optional, Tuple
 import torch
 
 from . import _lib
-from ._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT, EPI_NO_Y, check, ptr
+from ._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT, EPI_ACC_X, EPI_NO_Y, check, ptr
 from .graph import CsrGraph
 
 
@@ -189,24 +189,64 @@ def mark_rows(row_ptr: torch.Tensor, col: torch.Tensor, marked: torch.Tensor,
     return m
 
 
-def _lightgcn_hops(op: CsrGraph, x0: torch.Tensor, K: int, masks) -> torch.Tensor:
+def lightgcn_hop_schedule(K: int, deferred: bool) -> list:
+    """The K hop launches of LightGCN propagation with the layer mean in their epilogues:
+    per hop (x, y, epi), x / y naming a buffer — "x0", "acc" (the output), "a", "b" (hop
+    buffers) or None (no y store).
+
+    Eager (any kernel): hop 1 acc = x0 + y1, then acc += yk, / (K+1) on the last hop — 8 row
+    transfers of the epilogue per K=3 forward (x0 read, y1/y2 written, acc written 3x and
+    read 2x). Deferred (column-ordered kernel only, EPI_ACC_X and INIT|ADD): hops 1 and 2 store
+    their output only — y1 parked in the acc rows — and hop 3 forms ((x0 + y1) + y2) + y3
+    reading x0, acc (y1) and its own input rows (y2): 6 transfers at K=3, 4 instead of 5 at K=2
+    (x0 + y1 read on hop 2, y1 being hop 2's input). The additions and their order are the
+    eager schedule's, so the bits are too. No hop gathers from the rows it writes."""
+    if K <= 0:
+        return []
+    if not deferred or K == 1:
+        sched = []
+        x = "x0"
+        for k in range(1, K + 1):
+            last = k == K
+            epi = (EPI_ACC_INIT if k == 1 else EPI_ACC_ADD) | ((EPI_ACC_DIV | EPI_NO_Y) if last else 0)
+            y = None if last else ("a" if k & 1 else "b")
+            sched.append((x, y, epi))
+            x = y
+        return sched
+    if K == 2:
+        return [("x0", "a", 0), ("a", None, EPI_ACC_INIT | EPI_ACC_X | EPI_ACC_DIV | EPI_NO_Y)]
+    sched = [("x0", "acc", 0), ("acc", "b", 0)]
+    x = "b"
+    for k in range(3, K + 1):
+        last = k == K
+        epi = (EPI_ACC_INIT | EPI_ACC_ADD | EPI_ACC_X) if k == 3 else EPI_ACC_ADD
+        if last:
+            epi |= EPI_ACC_DIV | EPI_NO_Y
+        y = None if last else ("a" if x == "b" else "b")
+        sched.append((x, y, epi))
+        x = y
+    return sched
+
+
+def _lightgcn_hops(op: CsrGraph, x0: torch.Tensor, K: int, masks,
+                   deferred: bool = False) -> torch.Tensor:
     """mean(x0, op x0, ..., op^K x0) as K spmm_into launches with the layer mean in their
-    epilogues — the launch and rounding order of gnnrec_lightgcn_split_f32. `masks(k, x_in)`
-    gives hop k's (x_mask, y_active), either None."""
+    epilogues (lightgcn_hop_schedule; eager: the launch and rounding order of
+    gnnrec_lightgcn_split_f32). `masks(k, x_in)` gives hop k's (x_mask, y_active), either
+    None. deferred: the column-ordered kernel's schedule (the caller checks that spmm_into
+    takes that kernel for (op, x0) and that no hop is masked)."""
     out = torch.empty_like(x0)
     if K == 0:
         out.copy_(x0)
         return out
-    bufs = [torch.empty_like(x0), torch.empty_like(x0)] if K > 1 else [None]
-    x_in = x0
-    for k in range(1, K + 1):
-        last = k == K
-        epi = (EPI_ACC_INIT if k == 1 else EPI_ACC_ADD) | ((EPI_ACC_DIV | EPI_NO_Y) if last else 0)
-        y = None if last else bufs[k & 1]
-        xm, ya = masks(k, x_in)
-        spmm_into(op, x_in, y, epi=epi, self_rows=x0, acc=out, acc_div=float(K + 1),
-                  x_mask=xm, y_active=ya)
-        x_in = y
+    bufs = {"x0": x0, "acc": out, None: None}
+    for k, (xn, yn, epi) in enumerate(lightgcn_hop_schedule(K, deferred), start=1):
+        for name in (xn, yn):
+            if name not in bufs:
+                bufs[name] = torch.empty_like(x0)
+        xm, ya = masks(k, bufs[xn])
+        spmm_into(op, bufs[xn], bufs[yn], epi=epi, self_rows=x0, acc=out,
+                  acc_div=float(K + 1), x_mask=xm, y_active=ya)
     return out
 
 
@@ -278,7 +318,8 @@ def lightgcn_forward(adj: CsrGraph, x0: torch.Tensor, n_layers: int,
         raise ValueError("LightGCN propagation needs a square operand matching x0")
     if not return_layers and tiled_plan_for(adj, x0) is not None:
         # per-hop launches of the column-ordered kernel, same epilogue order and bits
-        return _lightgcn_hops(adj, x0, int(n_layers), lambda k, x_in: (None, None)), None
+        return _lightgcn_hops(adj, x0, int(n_layers), lambda k, x_in: (None, None),
+                              deferred=True), None
     out = torch.empty_like(x0)
     layers = work0 = work1 = None
     if return_layers:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GNNREC_ABI_VERSION 5
+#define GNNREC_ABI_VERSION 6
 
 typedef struct ihipStream_t* gnnrec_stream_t;
 
@@ -46,11 +46,18 @@ enum gnnrec_status {
  *   ACC_INIT: acc[r] = self[r] + y[r]          (first hop: x0 + x1)
  *   ACC_ADD : acc[r] = acc[r] + y[r]           (later hops, sequential like torch.mean)
  *   ACC_DIV : then acc[r] = acc[r] / acc_div   (last hop: / (K+1))
- *   NO_Y    : do not store y (last hop when the layer output itself is not needed) */
+ *   NO_Y    : do not store y (last hop when the layer output itself is not needed)
+ * gnnrec_spmm_tiled_f32 only (ABI 6; the CSR entry points return GNNREC_EUNSUPPORTED):
+ *   ACC_INIT|ACC_ADD: acc[r] = (self[r] + acc[r]) + y[r]   (an earlier layer parked in acc)
+ *   ACC_X   : the hop's input row x[r] (the previous layer; square operand) is added after
+ *             the self/acc terms and before y[r]: acc[r] = ((self[r] [+ acc[r]]) + x[r]) + y[r]
+ *   With them the layer mean is formed once, on the last hop, from the parked layers
+ *   (hops 1..K-1 store y only): same additions in the same order, so the same bits. */
 #define GNNREC_EPI_ACC_INIT 1
 #define GNNREC_EPI_ACC_ADD 2
 #define GNNREC_EPI_ACC_DIV 4
 #define GNNREC_EPI_NO_Y 8
+#define GNNREC_EPI_ACC_X 16
 
 /* ---- library identity ------------------------------------------------------------ */
 const char* gnnrec_version(void);

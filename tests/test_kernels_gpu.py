@@ -510,3 +510,78 @@ def test_rows_gemm_fused_gat_epilogue(cuda):
     acc = base.clone()
     assert F.rows_gemm(z, W, epi=EPI_ACC_ADD | EPI_NO_Y, acc=acc) is None
     torch.testing.assert_close(acc, base + (z.double() @ W.double()).float(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("flags", ["init_add", "init_x", "add_x", "init_add_x"])
+def test_spmm_tiled_multi_input_epilogues(cuda, flags):
+    """ABI 6 epilogues of the column-ordered kernel: acc = ((self [+ acc]) [+ x[r]]) + y, in
+    that order, then / div; acc updated in place; strided tables."""
+    g, (rp, col, val) = random_graph(4000, 3000, 30000, 11, cuda)
+    n = g.shape[0]
+    big = torch.randn(n, 96, device=cuda) * 0.1
+    x = big[:, 16:80]                                    # ldx = 96
+    xs = x.contiguous().cpu().numpy()
+    yr = oracle.spmm(rp, col, val, xs)
+    x0 = torch.randn(n, 64, device=cuda) * 0.1
+    acc_in = torch.randn(n, 64, device=cuda) * 0.1
+    plan = g.tiled_plan(rows_per_block=333, panel=1024)
+    epi = {"init_add": _lib.EPI_ACC_INIT | _lib.EPI_ACC_ADD,
+           "init_x": _lib.EPI_ACC_INIT | _lib.EPI_ACC_X,
+           "add_x": _lib.EPI_ACC_ADD | _lib.EPI_ACC_X,
+           "init_add_x": _lib.EPI_ACC_INIT | _lib.EPI_ACC_ADD | _lib.EPI_ACC_X}[flags]
+    terms = []
+    if epi & _lib.EPI_ACC_INIT:
+        terms.append(x0.cpu().numpy())
+    if epi & _lib.EPI_ACC_ADD:
+        terms.append(acc_in.cpu().numpy())
+    if epi & _lib.EPI_ACC_X:
+        terms.append(xs)
+    want = terms[0]
+    for t in terms[1:]:
+        want = want + t
+    want = want + yr
+    for div in (1.0, 4.0):
+        acc = acc_in.clone()
+        y = torch.full((n, 64), float("nan"), device=cuda)
+        F.spmm_tiled_into(g, x, y, plan, epi=epi | (_lib.EPI_ACC_DIV if div != 1.0 else 0),
+                          self_rows=x0, acc=acc, acc_div=div)
+        np.testing.assert_array_equal(bits(y.cpu().numpy()), bits(yr))
+        w = want / np.float32(div) if div != 1.0 else want
+        np.testing.assert_array_equal(bits(acc.cpu().numpy()), bits(w))
+
+
+def test_csr_rejects_tiled_only_epilogues(cuda):
+    g, _ = random_graph(300, 200, 2000, 1, cuda)
+    x = torch.zeros(g.shape[0], 64, device=cuda)
+    acc = torch.zeros_like(x)
+    for epi in (_lib.EPI_ACC_INIT | _lib.EPI_ACC_X, _lib.EPI_ACC_INIT | _lib.EPI_ACC_ADD):
+        with pytest.raises(Exception, match="gnnrec_spmm_tiled_f32 only"):
+            F.spmm_into(g, x, torch.empty_like(x), epi=epi, self_rows=x, acc=acc)
+
+
+@pytest.mark.parametrize("K", [1, 2, 3, 4, 5])
+def test_lightgcn_deferred_schedule_bit_exact(cuda, monkeypatch, K):
+    """lightgcn_forward through the column-ordered kernel (deferred layer mean) and the
+    one-device lightgcn_propagate_dist equal the eager CSR launches (gnnrec_lightgcn_split_f32),
+    bit for bit, for every K."""
+    from src.ops.distributed import DistributedGraph, lightgcn_propagate_dist
+    monkeypatch.setattr(F, "TILED_MIN_ROWS", 0)
+    monkeypatch.setattr(F, "TILED_MIN_TABLE_BYTES", 0)
+    u_i = np.random.default_rng(K)
+    nu, ni = 3000, 2000
+    from src.ops import CsrGraph
+    full = CsrGraph.from_interactions(u_i.integers(0, nu, 40000), u_i.integers(0, ni, 40000), nu, ni)
+    g = full.to(cuda)
+    x0 = torch.randn(g.shape[0], 64, generator=torch.Generator().manual_seed(K)).to(cuda) * 0.1
+    ref, _ = F.lightgcn_forward(g, x0, K, return_layers=True)      # CSR, eager epilogues
+    assert F.tiled_plan_for(g, x0) is not None
+    out, _ = F.lightgcn_forward(g, x0, K)
+    assert torch.equal(bits_t(out), bits_t(ref))
+    dg = DistributedGraph(full, 0, 1, cuda)
+    xp = dg.pad_table(x0)
+    od = lightgcn_propagate_dist(dg, xp, K)
+    assert torch.equal(bits_t(od), bits_t(ref))
+
+
+def bits_t(t):
+    return t.contiguous().view(torch.int32)

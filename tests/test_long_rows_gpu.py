@@ -108,3 +108,19 @@ def test_model_class_bit_exact(case, cuda):
     with torch.no_grad():
         u2, i2 = m(g.to_torch_sparse_coo())
     assert torch.equal(u, u2) and torch.equal(i, i2)
+
+
+@pytest.mark.parametrize("rows_per_block", [1279, 97])
+def test_tiled_deferred_layer_mean_bit_exact(case, rows_per_block):
+    """The headline schedule (F.lightgcn_hop_schedule, deferred): y1 parked in the output rows,
+    the mean formed on hop 3 from x0, y1 and hop 3's own input rows (EPI_ACC_X) — the
+    reference's layer mean, bit for bit."""
+    f, g, x0, _, _ = case
+    plan = g.tiled_plan(rows_per_block=rows_per_block)
+    out = torch.full_like(x0, float("nan"))
+    bufs = {"x0": x0, "acc": out, "a": torch.empty_like(x0), "b": torch.empty_like(x0),
+            None: None}
+    for xn, yn, epi in F.lightgcn_hop_schedule(3, deferred=True):
+        F.spmm_tiled_into(g, bufs[xn], bufs[yn], plan, epi=epi, self_rows=x0, acc=out,
+                          acc_div=4.0)
+    check_layers(f, [], out)
