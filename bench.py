@@ -483,6 +483,9 @@ def main(argv=None) -> int:
                            "one launch per hop)" if tiled else
                            f"spmm_vec_kernel<{d}> (one launch per hop)"),
                 "launch_ms": launch_ms,
+                # per hop of the step (hop k = every K-th launch; N = 1 without chunks)
+                "launch_ms_per_hop": [float(np.mean(durs[k::K])) for k in range(K)]
+                if len(durs) == a.steps * K else None,
                 "bytes_per_launch_with_fused_epilogue": launch_bytes,
                 "layer_mean_schedule": "deferred (hop K forms the mean)"
                 if (world == 1 and tiled and K >= 2) else "eager (every hop's epilogue)",

@@ -54,7 +54,13 @@ constexpr int kGroup = 8;                         // steps whose reads precede t
 #define GNNREC_TILED_EPI_BATCH 20
 #endif
 constexpr int kEpiBatch = GNNREC_TILED_EPI_BATCH;   // epilogue rows per half-wave, loads in flight
-constexpr int kEpiBatch3 = 10;   // the same with two or three base inputs per row (VGPRs)
+#ifndef GNNREC_TILED_EPI_PRELOAD
+#define GNNREC_TILED_EPI_PRELOAD 1   // the first batch's base rows loaded before the pass-end barriers
+#endif
+#ifndef GNNREC_TILED_EPI_BATCH3
+#define GNNREC_TILED_EPI_BATCH3 10
+#endif
+constexpr int kEpiBatch3 = GNNREC_TILED_EPI_BATCH3;   // the same with 2-3 base inputs per row
 static_assert(kHalf == 16, "a half-chunk is one DPP row of 16 lanes");
 static_assert(kHalf == 2 * kGroup, "a half-chunk is applied as two groups");
 static_assert(GNNREC_TILED_MAX_ROWS < kRowMask, "row field is 11 bits (row R = scratch)");
@@ -199,38 +205,52 @@ __device__ __forceinline__ void tiled_apply(float* acc, uint32_t f4, const Tiled
 // (((b0 [+ b1]) [+ b2]) + y) [/ div] — b0 = x0 (ACC_INIT) or the running sum (ACC_ADD);
 // INIT|ADD: b0 = x0, b1 = the acc rows (an earlier layer parked there); ACC_X: the hop's
 // input row x[r] (the previous layer) last. NB = 0: y only.
-template <int NB, int B>
+template <int NB, int B, class Wait>
 __device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, uint32_t f4,
                                                __amdgpu_buffer_rsrc_t ry, uint32_t ly,
                                                __amdgpu_buffer_rsrc_t rb0, uint32_t lb0,
                                                __amdgpu_buffer_rsrc_t rb1, uint32_t lb1,
                                                __amdgpu_buffer_rsrc_t rb2, uint32_t lb2,
                                                __amdgpu_buffer_rsrc_t ra, uint32_t la,
-                                               bool div, float acc_div) {
+                                               bool div, float acc_div, Wait wait) {
   constexpr int kStride = 2 * kTiledWaves;
   const __amdgpu_buffer_rsrc_t rb[3] = {rb0, rb1, rb2};
   const uint32_t lb[3] = {lb0, lb1, lb2};
-  for (int i0 = rl; i0 - (rl & 1) < R; i0 += kStride * B) {
+  float base[NB > 0 ? NB : 1][B];
+  // the base rows of batch i0 (global, independent of the pass: the first batch is loaded
+  // before the pass-end barriers, so its latency hides behind the block's slowest wave)
+  auto load_base = [&](int i0) {
     // per-row offsets advance by a stride; the opaque copy keeps the compiler from hoisting
     // B x 3 of them out of the persistent loop (they would spill)
-    uint32_t ol = (uint32_t)i0, ob[3];
-    asm volatile("" : "+v"(ol));
+    uint32_t ob[3];
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       ob[j] = (uint32_t)i0 * lb[j] + f4;
       asm volatile("" : "+v"(ob[j]));
     }
-    float a[B], base[NB > 0 ? NB : 1][B];
 #pragma unroll
-    for (int q = 0; q < B; ++q) {
-      a[q] = acc[min(ol, (uint32_t)R) * kSlice + (f4 >> 2)];
-      ol += kStride;
+    for (int q = 0; q < B; ++q)
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
         base[j][q] =
             __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb[j], ob[j], 0, 0));
         ob[j] += kStride * lb[j];
       }
+  };
+  int i0 = rl;
+  if (GNNREC_TILED_EPI_PRELOAD) load_base(i0);
+  wait();
+  // the first batch runs even when rl is past the block's rows: its LDS reads stay inside
+  // (row R is the scratch row) and its stores fall outside the buffer ranges
+  for (;;) {
+    if (!GNNREC_TILED_EPI_PRELOAD) load_base(i0);
+    uint32_t ol = (uint32_t)i0;
+    asm volatile("" : "+v"(ol));
+    float a[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      a[q] = acc[min(ol, (uint32_t)R) * kSlice + (f4 >> 2)];
+      ol += kStride;
     }
     uint32_t oy = (uint32_t)i0 * ly + f4, oa = (uint32_t)i0 * la + f4;
     asm volatile("" : "+v"(oy), "+v"(oa));
@@ -248,6 +268,9 @@ __device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, 
         oa += kStride * la;
       }
     }
+    i0 += kStride * B;
+    if (i0 - (rl & 1) >= R) break;
+    if (GNNREC_TILED_EPI_PRELOAD) load_base(i0);
   }
 }
 
@@ -327,10 +350,12 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
 #undef GNNREC_TILED_STAGE
     }
     const int ns = nsteps[blk];
-    for (int i = cur; i < ns; ++i) {  // this wave's remaining steps + the last
-      __syncthreads();
-      GNNREC_TILED_STAMP(ev);
-    }
+    auto wait = [&]() {
+      for (int i = cur; i < ns; ++i) {  // this wave's remaining steps + the last
+        __syncthreads();
+        GNNREC_TILED_STAMP(ev);
+      }
+    };
     // epilogue: half-wave h of wave w owns rows i = 2w + h + 32q (see tiled_epilogue)
     const int64_t r0 = (int64_t)blk * R;
     const int nv = (int)min((int64_t)R, n_rows - r0);
@@ -349,7 +374,8 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     const uint32_t lb0 = init ? ls : la, lb1 = (init && add) ? la : row_bytes;
     const bool div = (epi & GNNREC_EPI_ACC_DIV) != 0;
 #define GNNREC_TILED_EPI(NB, B, DIV) \
-  tiled_epilogue<NB, B>(acc, R, rl, f4, ry, ly, rb0, lb0, rb1, lb1, rx, row_bytes, racc, la, DIV, acc_div)
+  tiled_epilogue<NB, B>(acc, R, rl, f4, ry, ly, rb0, lb0, rb1, lb1, rx, row_bytes, racc, la, DIV, \
+                        acc_div, wait)
     if (nb == 0)
       GNNREC_TILED_EPI(0, kEpiBatch, false);
     else if (nb == 1)
