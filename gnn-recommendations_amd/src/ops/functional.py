@@ -259,14 +259,20 @@ def lightgcn_backward(adj: CsrGraph, g: torch.Tensor, n_layers: int,
     2048 (tools/exp_masked.py): hop 1 1.9 ms masked+active vs 7.0 dense (row-parallel); hop 2
     (a quarter of the rows live) 5.9 ms masked, 6.0 + 0.4 (marking) masked+active, but 4.2 ms
     dense through the column-ordered kernel. Default: only hop 1 masked where that kernel
-    takes the operand, K-1 hops otherwise (a skipped row adds fmaf(v, 0, acc) = acc: the
-    same bits as the dense hop, which is the reference's own arithmetic)."""
+    takes the operand (and then the deferred layer mean), K-1 hops otherwise (a skipped row
+    adds fmaf(v, 0, acc) = acc: the same bits as the dense hop, which is the reference's own
+    arithmetic)."""
     at = adj.t()
     g = g.contiguous()
     _require_device(at, g)
     K = int(n_layers)
+    tiled = tiled_plan_for(at, g) is not None
     if masked_hops is None:
-        masked_hops = 1 if tiled_plan_for(at, g) is not None else K - 1
+        masked_hops = 1 if tiled else K - 1
+    # the deferred layer mean (lightgcn_hop_schedule) when the hop carrying its tiled-only
+    # epilogue (hop 2 at K = 2, hop 3 otherwise) is a dense column-ordered hop: a masked hop
+    # before it stores its y as the eager one does (+0 on skipped rows), so the same bits
+    deferred = tiled and K >= 2 and masked_hops < (2 if K == 2 else 3)
 
     def masks(k, x_in):
         if k > masked_hops:
@@ -276,7 +282,7 @@ def lightgcn_backward(adj: CsrGraph, g: torch.Tensor, n_layers: int,
         ya = mark_rows(adj.row_ptr, adj.col, xm, at.n_rows) if k <= active_hops else None
         return xm, ya
 
-    return _lightgcn_hops(at, g, K, masks)
+    return _lightgcn_hops(at, g, K, masks, deferred=deferred)
 
 
 def lightgcn_forward_rows(adj: CsrGraph, x0: torch.Tensor, n_layers: int, need: torch.Tensor,

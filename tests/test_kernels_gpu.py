@@ -585,3 +585,23 @@ def test_lightgcn_deferred_schedule_bit_exact(cuda, monkeypatch, K):
 
 def bits_t(t):
     return t.contiguous().view(torch.int32)
+
+
+@pytest.mark.parametrize("K", [2, 3, 4])
+def test_masked_backward_deferred_mean_bit_exact(cuda, monkeypatch, K):
+    """lightgcn_backward through the column-ordered kernel (forced): a masked first hop on the
+    row-parallel kernel, then the deferred layer mean on the tiled hops — equal to the eager
+    CSR propagation over A^T, bit for bit."""
+    monkeypatch.setattr(F, "TILED_MIN_ROWS", 0)
+    monkeypatch.setattr(F, "TILED_MIN_TABLE_BYTES", 0)
+    g, _ = random_graph(3000, 2000, 40000, 50 + K, cuda)
+    n = g.shape[0]
+    grad = torch.zeros(n, 64, device=cuda)
+    rows = torch.randperm(n, device=cuda)[:60]
+    grad[rows] = torch.randn(60, 64, device=cuda)
+    assert F.tiled_plan_for(g.t(), grad) is not None
+    ref, _ = F.lightgcn_forward(g.t(), grad, K, return_layers=True)   # CSR, eager epilogues
+    for mh, ah in ((None, 1), (1, 0), (2, 1)):
+        out = F.lightgcn_backward(g, grad, K, masked_hops=mh, active_hops=ah)
+        np.testing.assert_array_equal(bits(out.cpu().numpy()), bits(ref.cpu().numpy()),
+                                      err_msg=f"masked_hops={mh} active_hops={ah}")
