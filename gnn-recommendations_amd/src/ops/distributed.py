@@ -31,7 +31,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from ._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT, EPI_NO_Y
+from ._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT, EPI_ACC_X, EPI_NO_Y
 from .graph import CsrGraph
 
 HopFn = Callable[..., None]
@@ -226,19 +226,27 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
     Y, Xa, Xb = work
     self_rows = dg.local_slice(x0_pad)
     from .functional import lightgcn_hop_schedule, tiled_plan_for
-    if (dg.world == 1 and native and masks is None and n_layers >= 2
-            and tiled_plan_for(dg.shard, x0_pad) is not None):
+    # the hop carrying the deferred mean's tiled-only epilogue must be a dense hop
+    flag_hop = 2 if n_layers == 2 else 3
+    if (dg.world == 1 and native and n_layers >= 2
+            and tiled_plan_for(dg.shard, x0_pad) is not None
+            and (masks is None or masks(flag_hop, x0_pad) is None)):
         # one device, column-ordered kernel: the layer mean formed on the last hop from the
         # parked layers (lightgcn_hop_schedule, deferred) — 6 instead of 8 epilogue row
-        # transfers at K = 3, same bits. acc is padded to the gather table's rows, since hop 2
+        # transfers at K = 3, same bits (a masked hop before it stores its y as the eager one
+        # does: +0 on skipped rows). acc is padded to the gather table's rows, since hop 2
         # gathers from it (y1 is parked there).
         acc_full = torch.empty((Xa.shape[0], d), dtype=torch.float32, device=x0_pad.device)
         acc_full[dg.n_local:].zero_()
         acc = acc_full[:dg.n_local]
         bufs = {"x0": x0_pad, "acc": acc_full, "a": Xa, "b": Xb, None: None}
-        for xn, yn, epi in lightgcn_hop_schedule(n_layers, deferred=True):
+        for k, (xn, yn, epi) in enumerate(lightgcn_hop_schedule(n_layers, deferred=True),
+                                          start=1):
+            kw = mkw(k, bufs[xn])
+            if kw and (epi & EPI_ACC_X or (epi & EPI_ACC_INIT and epi & EPI_ACC_ADD)):
+                raise RuntimeError(f"deferred layer mean: hop {k} must not be masked")
             hop(dg.shard, bufs[xn], None if yn is None else bufs[yn][:dg.n_local], epi=epi,
-                self_rows=self_rows, acc=acc, acc_div=float(n_layers + 1))
+                self_rows=self_rows, acc=acc, acc_div=float(n_layers + 1), **kw)
         return acc
     acc = torch.empty((dg.n_local, d), dtype=torch.float32, device=x0_pad.device)
     if n_layers == 0:

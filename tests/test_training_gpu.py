@@ -137,3 +137,37 @@ def test_native_adam_matches_torch_adam(cuda):
     np.testing.assert_allclose(st1["exp_avg_sq"].cpu().numpy(), st2["exp_avg_sq"].cpu().numpy(),
                                rtol=1e-6, atol=1e-12)
     assert float(st1["step"]) == float(st2["step"]) == 5
+
+
+def test_sharded_step_deferred_mean_same_bits(cuda, monkeypatch):
+    """With the column-ordered kernel forced, the one-device sharded step's backward (a masked
+    hop 1, then the deferred layer mean) and its full propagations give the bits of the
+    row-parallel kernel's eager schedule, over three Adam steps."""
+    from conftest import load_golden
+    from src.models import LightGCN
+    from src.ops import functional as F
+    from src.ops.distributed import DistributedGraph
+    from src.training import lightgcn_train_step_dist
+    f = load_golden("bpr_train_K3_d64")
+    g, nu, ni = _golden_graph()
+    torch.manual_seed(56)
+    m = LightGCN(nu, ni, embedding_dim=64, n_layers=3, init_scale=0.1)
+    x0 = torch.cat([m.user_embedding.weight, m.item_embedding.weight]).detach()
+    res = []
+    for forced, subset in ((False, True), (True, True), (True, False)):
+        if forced:
+            monkeypatch.setattr(F, "TILED_MIN_ROWS", 0)
+            monkeypatch.setattr(F, "TILED_MIN_TABLE_BYTES", 0)
+        dg = DistributedGraph(g, 0, 1, cuda)
+        assert (F.tiled_plan_for(dg.shard, x0.to(cuda)) is not None) == forced
+        emb = torch.nn.Parameter(x0.to(cuda).clone())
+        opt = torch.optim.Adam([emb], lr=1e-2, weight_decay=1e-4)
+        losses = [float(lightgcn_train_step_dist(dg, emb, 3, nu,
+                                                 *[torch.from_numpy(f[k][b]).to(cuda)
+                                                   for k in ("users", "pos", "neg")], opt,
+                                                 row_subset=subset))
+                  for b in range(3)]
+        res.append((losses, emb.detach().clone()))
+    for losses, emb in res[1:]:
+        assert losses == res[0][0]
+        assert torch.equal(emb, res[0][1])
