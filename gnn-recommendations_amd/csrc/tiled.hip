@@ -57,6 +57,9 @@ constexpr int kEpiBatch = GNNREC_TILED_EPI_BATCH;   // epilogue rows per half-wa
 #ifndef GNNREC_TILED_EPI_PRELOAD
 #define GNNREC_TILED_EPI_PRELOAD 1   // the first batch's base rows loaded before the pass-end barriers
 #endif
+// epilogue stores non-temporal (aux bit 1, nt): the rows are read again only by the next
+// launch; 12.62 -> 12.56 ms per step (profiles/r02/exp_epi_store_policy.jsonl; sc1 write-through, 12.60)
+constexpr int kEpiStoreAux = 2;
 #ifndef GNNREC_TILED_EPI_BATCH3
 #define GNNREC_TILED_EPI_BATCH3 10
 #endif
@@ -256,7 +259,7 @@ __device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, 
     asm volatile("" : "+v"(oy), "+v"(oa));
 #pragma unroll
     for (int q = 0; q < B; ++q) {
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, a[q]), ry, oy, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, a[q]), ry, oy, 0, kEpiStoreAux);
       oy += kStride * ly;
       if (NB > 0) {
         float bsum = base[0][q];
@@ -264,7 +267,7 @@ __device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, 
         for (int j = 1; j < NB; ++j) bsum = bsum + base[j][q];
         bsum = bsum + a[q];
         if (div) bsum = bsum / acc_div;
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, bsum), ra, oa, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, bsum), ra, oa, 0, kEpiStoreAux);
         oa += kStride * la;
       }
     }
