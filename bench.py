@@ -174,16 +174,17 @@ def tiled_plan_info(g: CsrGraph, x: torch.Tensor):
 
 
 def cpu_baseline(g: CsrGraph, x0: torch.Tensor, K: int, n_users: int, gpu_hop1: np.ndarray,
-                 gpu_out: np.ndarray) -> dict:
+                 gpu_out: np.ndarray, reps: int = 2) -> dict:
     """The reference's CPU path as SURVEY §8 d3 specifies it, on this host's cores, for the
     WHOLE workload:
       * graph build (graph_builder.py:16-174: scipy COO -> tocsr -> D^-1/2 A D^-1/2 -> torch
         COO) over every deduplicated pair, compared bit for bit with the GPU's operand;
       * propagation (lightgcn.py:76-95): x = cat(U, I); K x torch.sparse.mm on the
         reference-layout uncoalesced int64 COO; torch.stack(layers).mean(0), no_grad.
-    One untimed warm-up hop over a 1 % row slice (thread pool / MKL start-up), then one timed
-    full propagation (a single rep: ~70 s of CPU work at 16 threads for G100M). Hop 1 and the
-    output are compared bit for bit with the GPU's (cpu_parity)."""
+    One untimed warm-up hop over a 1 % row slice (thread pool / MKL start-up), then `reps`
+    timed full propagations (SURVEY §8 d3 / BASELINE.md §3: >= 2 reps, the median reported,
+    every sample listed; ~70 s each at 16 threads for G100M). Every rep's hop 1 and output
+    are compared bit for bit with the GPU's (cpu_parity)."""
     import oracle.torch_ref as tr
     threads = host_threads()
     torch.set_num_threads(threads)
@@ -214,18 +215,24 @@ def cpu_baseline(g: CsrGraph, x0: torch.Tensor, K: int, n_users: int, gpu_hop1: 
         warm = tr.coo_operand(rp, col, val, N, slice(0, max(1, N // 100)))
         torch.sparse.mm(warm, xc)
         del warm
-        t0 = time.perf_counter()
-        layers = [xc]
-        x = xc
-        for _ in range(K):
-            x = torch.sparse.mm(A_ref, x)
-            layers.append(x)
-        out = torch.stack(layers, dim=0).mean(dim=0)
-        t = time.perf_counter() - t0
-    hop1_same = bool(np.array_equal(layers[1].numpy().view(np.uint32), gpu_hop1.view(np.uint32)))
-    out_same = bool(np.array_equal(out.numpy().view(np.uint32), gpu_out.view(np.uint32)))
-    max_abs = float(np.abs(out.numpy() - gpu_out).max())
-    del layers, out, x, A_ref
+        samples, hop1_same, out_same, max_abs = [], True, True, 0.0
+        for _ in range(max(1, int(reps))):
+            t0 = time.perf_counter()
+            layers = [xc]
+            x = xc
+            for _ in range(K):
+                x = torch.sparse.mm(A_ref, x)
+                layers.append(x)
+            out = torch.stack(layers, dim=0).mean(dim=0)
+            samples.append(time.perf_counter() - t0)
+            log(f"cpu: rep {len(samples)}: {samples[-1]:.1f}s")
+            hop1_same &= bool(np.array_equal(layers[1].numpy().view(np.uint32),
+                                             gpu_hop1.view(np.uint32)))
+            out_same &= bool(np.array_equal(out.numpy().view(np.uint32), gpu_out.view(np.uint32)))
+            max_abs = max(max_abs, float(np.abs(out.numpy() - gpu_out).max()))
+            del layers, out, x
+    t = float(np.median(samples))
+    del A_ref
     cpu_model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -235,12 +242,13 @@ def cpu_baseline(g: CsrGraph, x0: torch.Tensor, K: int, n_users: int, gpu_hop1: 
     except OSError:
         pass
     return {"value": K * g.nnz / t, "unit": "edges/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model, "seconds": t,
+            "cpu_model": cpu_model, "seconds": t, "seconds_samples": samples,
+            "statistic": f"median of {len(samples)} timed reps",
             "sample": f"the whole workload: LightGCN K={K} propagation (x0 [{N}, {xc.shape[1]}], "
                       f"{K} x torch.sparse.mm on the reference-layout uncoalesced int64 COO of "
                       f"all {g.nnz} nnz, graph_builder.py:163-172, then stack().mean(0), "
                       f"lightgcn.py:76-95), no_grad, 1 untimed warm-up hop over a 1% row "
-                      f"slice then 1 timed rep; torch {torch.__version__} "
+                      f"slice then {len(samples)} timed reps (median); torch {torch.__version__} "
                       f"({torch.get_num_threads()} threads)",
             "graph_build": {"pairs": nnz_u, "seconds": t_build,
                             "what": "scipy COO -> tocsr -> D^-1/2 A D^-1/2 -> torch COO over "
@@ -277,6 +285,8 @@ def main(argv=None) -> int:
     ap.add_argument("--pairs", type=int, default=100_000_000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-reps", type=int, default=2,
+                    help="timed reps of the reference CPU path (median reported)")
     ap.add_argument("--verify", action="store_true",
                     help="after timing, compare this rank's rows bit for bit with a single-device "
                          "propagation of the whole graph")
@@ -437,7 +447,7 @@ def main(argv=None) -> int:
         gpu_out = out.cpu().numpy()
         del hop1
         log("timing the reference CPU path (scipy build + K-hop torch.sparse.mm) ...")
-        cpu = cpu_baseline(cpu_graph, x0, K, a.users, gpu_hop1, gpu_out)
+        cpu = cpu_baseline(cpu_graph, x0, K, a.users, gpu_hop1, gpu_out, reps=a.cpu_reps)
         del gpu_hop1, gpu_out
 
     if rank == 0:
@@ -489,10 +499,14 @@ def main(argv=None) -> int:
                 "bytes_per_launch_with_fused_epilogue": launch_bytes,
                 "layer_mean_schedule": "deferred (hop K forms the mean)"
                 if (world == 1 and tiled and K >= 2) else "eager (every hop's epilogue)",
-                # the same launch priced by its MEASURED memory-side traffic (PMC): how close
-                # the random row gather runs to the fabric/HBM rate
-                "traffic_gbps": (traffic / (launch_ms * 1e-3) / 1e9) if traffic else None,
-                "traffic_frac": (traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS)
+                # the same launch priced by its MEASURED memory-side traffic (PMC FETCH_SIZE x 2
+                # + WRITE_SIZE). FETCH_SIZE counts the L2's requests to the fabric, Infinity-Cache
+                # hits included (MI355X_MICROARCH.md § HBM), so this is L2->fabric traffic, an
+                # upper bound of the HBM bytes — not HBM bandwidth
+                "traffic_what": "L2 -> fabric bytes per launch (FETCH_SIZE incl. Infinity-Cache "
+                                "hits, x2 gfx950 correction, + WRITE_SIZE)",
+                "fabric_gbps": (traffic / (launch_ms * 1e-3) / 1e9) if traffic else None,
+                "fabric_frac_of_hbm_peak": (traffic / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS)
                 if traffic else None,
             },
             "cpu_baseline": cpu,

@@ -6,28 +6,33 @@
 // neighbour row from beyond L2 (G100M: 16x the compulsory bytes). Here one persistent
 // 1024-thread workgroup per CU owns R destination rows per pass with fp32 accumulators in
 // LDS, and its 16 waves walk the rows' edges PANEL BY PANEL in ascending source column
-// (a step = one panel; a workgroup barrier between steps, so a row may move to another wave
-// from one step to the next without reordering its chain). The workgroups of a blockIdx % 8
-// group (one XCD under round-robin placement — speed only, never correctness) meet at every
-// pass start (bounded counter wait), so they sweep the same panels together and a gathered
-// source row is reused from the XCD's L2 by the group's other rows.
+// (a step = one panel; a workgroup barrier between steps, so a row may move to another slot
+// stream from one step to the next without reordering its chain). The workgroups of a
+// blockIdx % 8 group (one XCD under round-robin placement — speed only, never correctness)
+// meet at every pass start (bounded counter wait), so they sweep the same panels together and
+// a gathered source row is reused from the XCD's L2 by the group's other rows.
 //
 // Feature slices: a pass computes ONE 32-feature slice of its block's rows (a gather = one
-// 128-B line of a source row; the LDS row = 128 B), so R is twice what whole 64-feature rows
-// allow and an XCD group's pass covers twice the rows, touching each gathered line for more of
-// them (G100M: 14 passes x 1117 rows x 2 slices instead of 14 x 559 x 1). A d-wide hop is d/32
-// sweeps of the same plan; the work items are (slice, block) pairs, slice-major.
+// 128-B line of a source row; the LDS row = 128 B), so an XCD group's pass covers 35.7K rows
+// (G100M: 14 passes x 1117 rows x 2 slices). A d-wide hop is d/32 sweeps of the same plan; the
+// work items are (slice, block) pairs, slice-major.
 //
-// The two 32-lane halves of a wave take two slot streams (lane = half * 32 + feature). A chunk
-// holds 16 slots per half. Every lane loads ITS slot's word (column offset from the chunk's
-// panel base | local row), value and one word of the chunk header once per chunk (lane l:
-// slot (l / 32, l % 16)), and step t broadcasts slot t of each half to that half with DPP
-// row_newbcast:t (a 16-lane row reads its lane t), fused into the address add where the
-// compiler can; the header words (v_readlane) carry the step barriers, the chain mask (slot t
-// continues slot t-1's row in the same half: take the register value, not LDS) and the panel
-// base the chunk's buffer resource starts at. Pipeline per wave: chunk c+2's slot loads,
-// chunk c+1's gathers and chunk c's LDS read-fmaf-write in flight together. What bounds it:
-// the per-CU L1 miss path (one L2 request per gathered 128-B line).
+// Plan v3 (round 3): 16 bytes per lane. A wave runs EIGHT slot streams, one per 8-lane group
+// (lane = 8 g + q; lane q of group g owns features 4q .. 4q+3 of the slice), so one gather
+// instruction fetches eight 128-B lines with one buffer_load_dwordx4 per lane and one LDS
+// accumulator update is one ds_read_b128 / 4 fmaf / ds_write_b128 per lane. The per-CU L2->CU
+// rate of random 128-B lines is 2.2x higher in this form than with one dword per lane and two
+// lines per instruction (tools/gather_probe2.hip: 117 vs 53 GB/s per CU from L2;
+// profiles/r03/gather_probe2.jsonl) — the round-2 kernel's floor. A chunk is 8 steps x 8
+// streams = 64 slots, one per lane (lane 8 g + t holds slot t of stream g); step t hands slot
+// t of every stream to its group with two DPP row_newbcast moves under bank masks (lanes 0-7
+// of a 16-lane row read row lane t, lanes 8-15 read row lane 8 + t). The chunk header
+// {step barriers, chain mask lo, hi, panel base} comes back by v_readlane: bit 8 g + t of the
+// 64-bit chain mask = slot t of stream g continues slot t-1's row (take the register value);
+// SALU spreads the step's bits to lane masks. A chunk is applied as two groups of 4 steps
+// (reads of a group precede its writes; a row is at most one run of slots per group and
+// stream). Pipeline per wave: chunk c+2's slot loads, chunk c+1's 8 gathers and chunk c's LDS
+// chain in flight.
 #include <algorithm>
 #include <atomic>
 #include <mutex>
@@ -41,34 +46,62 @@
 namespace gnnrec {
 
 constexpr int kTiledWaves = GNNREC_TILED_WAVES;
-constexpr int kTiledChunk = GNNREC_TILED_CHUNK;   // slots per chunk (both halves)
-constexpr int kHalf = kTiledChunk / 2;            // slots per half = steps per chunk
+constexpr int kGroups = GNNREC_TILED_GROUPS;      // slot streams per wave (8 lanes each)
+constexpr int kSteps = GNNREC_TILED_STEPS;        // steps per chunk
+constexpr int kTiledChunk = GNNREC_TILED_CHUNK;   // slots per chunk (one per lane)
 constexpr int kTiledTail = GNNREC_TILED_TAIL;
 constexpr int kSlice = 32;                        // features per pass
+constexpr int kRowBytes = kSlice * 4;             // one LDS accumulator row, one gathered line
 constexpr int kRowBits = 11;
 constexpr int kRowMask = (1 << kRowBits) - 1;
 constexpr int kMaxPanel = 1 << 20;                // columns per panel (slot word: 21 bits)
 constexpr int kMaxRowBytes = GNNREC_TILED_MAX_LDX * 4;   // keeps the lane offset 32-bit
-constexpr int kGroup = 8;                         // steps whose reads precede their writes
-#ifndef GNNREC_TILED_EPI_BATCH
-#define GNNREC_TILED_EPI_BATCH 20
+constexpr int kApply = 4;                         // steps whose reads precede their writes
+#ifndef GNNREC_TILED_PLAN_AHEAD
+#define GNNREC_TILED_PLAN_AHEAD 3
 #endif
-constexpr int kEpiBatch = GNNREC_TILED_EPI_BATCH;   // epilogue rows per half-wave, loads in flight
+#ifndef GNNREC_TILED_GATHER_AHEAD
+#define GNNREC_TILED_GATHER_AHEAD 1
+#endif
+constexpr int kPlanAhead = GNNREC_TILED_PLAN_AHEAD;       // slot loads, chunks ahead of the apply
+constexpr int kGatherAhead = GNNREC_TILED_GATHER_AHEAD;   // gathers, chunks ahead of the apply
+constexpr int kMRing = kPlanAhead + 1;
+constexpr int kXRing = kGatherAhead + 1;
+constexpr int ring_gcd(int a, int b) { return b ? ring_gcd(b, a % b) : a; }
+constexpr int kRingUnroll = kMRing / ring_gcd(kMRing, kXRing) * kXRing;
+static_assert(kPlanAhead > kGatherAhead && kGatherAhead >= 1, "pipeline order");
+static_assert(kPlanAhead <= GNNREC_TILED_TAIL, "tail chunks cover the last prefetches");
+#ifndef GNNREC_TILED_EPI_BATCH
+#define GNNREC_TILED_EPI_BATCH 5
+#endif
+constexpr int kEpiBatch = GNNREC_TILED_EPI_BATCH;   // epilogue rows per group, loads in flight
+#ifndef GNNREC_TILED_EPI_BATCH3
+#define GNNREC_TILED_EPI_BATCH3 3
+#endif
+constexpr int kEpiBatch3 = GNNREC_TILED_EPI_BATCH3;   // the same with 2-3 base inputs per row
 #ifndef GNNREC_TILED_EPI_PRELOAD
 #define GNNREC_TILED_EPI_PRELOAD 1   // the first batch's base rows loaded before the pass-end barriers
 #endif
 // epilogue stores non-temporal (aux bit 1, nt): the rows are read again only by the next
-// launch; 12.62 -> 12.56 ms per step (profiles/r02/exp_epi_store_policy.jsonl; sc1 write-through, 12.60)
+// launch (round 2: 12.62 -> 12.56 ms per step, profiles/r02/exp_epi_store_policy.jsonl)
 constexpr int kEpiStoreAux = 2;
-#ifndef GNNREC_TILED_EPI_BATCH3
-#define GNNREC_TILED_EPI_BATCH3 10
-#endif
-constexpr int kEpiBatch3 = GNNREC_TILED_EPI_BATCH3;   // the same with 2-3 base inputs per row
-static_assert(kHalf == 16, "a half-chunk is one DPP row of 16 lanes");
-static_assert(kHalf == 2 * kGroup, "a half-chunk is applied as two groups");
+static_assert(kTiledChunk == kGroups * kSteps && kTiledChunk == 64, "one slot per lane");
+static_assert(kGroups == 8 && kSteps == 8, "a stream is 8 lanes: half a 16-lane DPP row");
+static_assert(kSteps == 2 * kApply, "a chunk is applied as two groups");
 static_assert(GNNREC_TILED_MAX_ROWS < kRowMask, "row field is 11 bits (row R = scratch)");
-static_assert((GNNREC_TILED_MAX_ROWS + 1) * kSlice * 4 <= 160 * 1024, "LDS");
+static_assert((GNNREC_TILED_MAX_ROWS + 1) * kRowBytes <= 160 * 1024, "LDS");
 static_assert((int64_t)kMaxPanel * kMaxRowBytes <= ((int64_t)1 << 32), "32-bit lane offsets");
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// Diagnostic builds only (tools/build_variant.sh, results wrong): bit 0 skips the LDS
+// accumulator reads and writes (registers instead), bit 1 replaces the gathers by a constant,
+// bit 2 skips the step barriers, bit 3 reads every chunk's slot words and values from the
+// plan's first 64 chunks (cache-resident plan stream; headers unchanged), bit 4 replaces the
+// DPP broadcasts by the lane's own value.
+#ifndef GNNREC_TILED_EXP
+#define GNNREC_TILED_EXP 0
+#endif
 
 // ---- device -----------------------------------------------------------------------------
 #ifdef GNNREC_TILED_TRACE
@@ -86,37 +119,36 @@ __device__ unsigned long long* g_tiled_trace;
 #define GNNREC_TILED_STAMP(ev) ((void)0)
 #endif
 
-struct TiledSlots {   // this lane's slot of the chunk: (half, lane % 16)
-  uint32_t o;         // byte offset of the source row from the chunk's panel base
+struct TiledSlots {   // this lane's slot of the chunk: stream lane / 8, step lane % 8
+  uint32_t w;         // slot word: (column - panel base) << kRowBits | local row
   float v;
-  uint32_t r;         // byte offset of the destination row's accumulator in LDS
   uint32_t h;         // word (lane % 4) of the chunk header
 };
 
+// Slot t of every stream to the stream's 8 lanes: within a 16-lane DPP row, lanes 0-7 (stream
+// 2k) take row lane t, lanes 8-15 (stream 2k+1) row lane 8 + t.
 template <int T>
-__device__ __forceinline__ uint32_t bcast(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + T, 0xF, 0xF, true);
+__device__ __forceinline__ uint32_t gbcast(uint32_t v) {
+  if (GNNREC_TILED_EXP & 16) return v ^ (T << 4);
+  // lanes 8-15 of the first move are left undefined: the second writes them
+  const int a = __builtin_amdgcn_mov_dpp((int)v, 0x150 + T, 0xF, 0x3, false);
+  return (uint32_t)__builtin_amdgcn_update_dpp(a, (int)v, 0x158 + T, 0xF, 0xC, false);
 }
 template <int T>
-__device__ __forceinline__ float bcastf(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
-                                                               0x150 + T, 0xF, 0xF, true));
+__device__ __forceinline__ float gbcastf(float v) {
+  return __builtin_bit_cast(float, gbcast<T>(__builtin_bit_cast(uint32_t, v)));
 }
 
-// Slot word: (column - chunk's panel base) << kRowBits | local row. The chunk header {step
-// barriers before the chunk, chain mask, panel base column, 0} is loaded with the slots as a
-// vector load (lane l: word l % 4) and read back with v_readlane: a scalar load would share
-// lgkmcnt with the LDS chain and stall it.
+// The chunk header {step barriers before the chunk, chain mask lo, chain mask hi, panel base
+// column} is loaded with the slots as a vector load (lane l: word l % 4) and read back with
+// v_readlane: a scalar load would share lgkmcnt with the LDS chain and stall it.
 __device__ __forceinline__ void tiled_slots(const uint32_t* __restrict__ ss,
                                             const float* __restrict__ sv,
-                                            const uint32_t* __restrict__ hdr, int64_t c,
-                                            int my_slot, int lane, uint32_t row_bytes,
+                                            const uint32_t* __restrict__ hdr, int64_t c, int lane,
                                             TiledSlots& m) {
-  const int64_t i = c * kTiledChunk + my_slot;
-  const uint32_t wd = ss[i];
-  m.o = __umul24(wd >> kRowBits, row_bytes);
+  const int64_t i = ((GNNREC_TILED_EXP & 8) ? (c & 63) : c) * kTiledChunk + lane;
+  m.w = ss[i];
   m.v = sv[i];
-  m.r = (wd & kRowMask) * (kSlice * 4);
   m.h = hdr[4 * c + (lane & 3)];
 }
 
@@ -140,17 +172,30 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const char* xs, uin
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* p, int64_t r0,
                                                             int64_t ld, int slice, int rows) {
   const float* b = p ? p + r0 * ld + (int64_t)slice * kSlice : p;
-  const uint32_t n = p ? (uint32_t)(rows - 1) * (uint32_t)ld * 4u + kSlice * 4u : 0u;
+  const uint32_t n = p ? (uint32_t)(rows - 1) * (uint32_t)ld * 4u + kRowBytes : 0u;
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(b), 0, (int)n, 0x00020000);
+}
+
+__device__ __forceinline__ f4 load4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ void store4(f4 v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+  __builtin_amdgcn_raw_buffer_store_b128(
+      __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r, off, 0,
+      kEpiStoreAux);
 }
 
 template <int... T>
 __device__ __forceinline__ void tiled_gather(std::integer_sequence<int, T...>,
-                                             __amdgpu_buffer_rsrc_t xr, uint32_t f4,
-                                             const TiledSlots& m, float (&x)[kHalf]) {
-  ((x[T] = __builtin_bit_cast(
-        float, __builtin_amdgcn_raw_buffer_load_b32(xr, bcast<T>(m.o) + f4, 0, 0))),
-   ...);
+                                             __amdgpu_buffer_rsrc_t xr, uint32_t q16,
+                                             uint32_t row_bytes, const TiledSlots& m,
+                                             f4 (&x)[kSteps]) {
+  const uint32_t o = __umul24(m.w >> kRowBits, row_bytes);   // this lane's slot's source row
+  if constexpr (GNNREC_TILED_EXP & 2) {
+    ((x[T] = f4{__builtin_bit_cast(float, gbcast<T>(o)), 1.f, 1.f, 1.f}), ...);
+  } else {
+    ((x[T] = load4(xr, gbcast<T>(o) + q16)), ...);
+  }
 }
 
 // lane-wise select on a wave-uniform 64-bit lane mask held in SGPRs (no compare per lane)
@@ -159,67 +204,100 @@ __device__ __forceinline__ float select_lanes(float if0, float if1, uint64_t mas
   asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if0), "v"(if1), "s"(mask));
   return r;
 }
+__device__ __forceinline__ f4 select4(f4 if0, f4 if1, uint64_t mask) {
+  f4 r;
+  r.x = select_lanes(if0.x, if1.x, mask);
+  r.y = select_lanes(if0.y, if1.y, mask);
+  r.z = select_lanes(if0.z, if1.z, mask);
+  r.w = select_lanes(if0.w, if1.w, mask);
+  return r;
+}
 
+// lanes of the streams whose slot T continues slot T-1's row: bit 8 g + T of cm -> byte g
 template <int T>
-__device__ __forceinline__ uint64_t chain_lanes(uint32_t cm) {
-  // slot T of half 0 (lanes 0-31): bit T; of half 1 (lanes 32-63): bit 16 + T
-  const uint32_t lo = 0u - ((cm >> T) & 1u), hi = 0u - ((cm >> (16 + T)) & 1u);
-  return ((uint64_t)hi << 32) | lo;
+__device__ __forceinline__ uint64_t chain_lanes(uint64_t cm) {
+  uint64_t m = (cm >> T) & 0x0101010101010101ull;
+  m |= m << 1;
+  m |= m << 2;
+  m |= m << 4;
+  return m;
 }
 
-// Steps G .. G+7 of a chunk: 8 accumulator reads, 8 chained fmaf, 8 writes. A chunk is
-// applied as two such groups, so a row may appear in both groups of a piece: the second
-// group's reads follow the first group's writes in the wave's LDS order (and a slot at step 8
-// chaining on step 7 selects the value step 7 just wrote).
-template <int G, int... T>
-__device__ __forceinline__ void tiled_apply8(std::integer_sequence<int, T...>, char* base,
-                                             uint32_t f4, const TiledSlots& m,
-                                             const float (&x)[kHalf], uint32_t cm,
-                                             float& prev) {
+__device__ __forceinline__ f4 fma4(float v, f4 x, f4 a) {
+  f4 r;
+  r.x = __builtin_fmaf(v, x.x, a.x);
+  r.y = __builtin_fmaf(v, x.y, a.y);
+  r.z = __builtin_fmaf(v, x.z, a.z);
+  r.w = __builtin_fmaf(v, x.w, a.w);
+  return r;
+}
+
+// Steps G .. G+3 of a chunk: 4 accumulator reads, 4 chained fmaf, 4 writes (per lane: 16 B
+// of a row each). A chunk is applied as two such groups, so a row may appear in both groups
+// of a stream: the second group's reads follow the first group's writes in the wave's LDS
+// order (and a slot at step 4 chaining on step 3 selects the value step 3 just wrote).
+template <bool CHAIN, int G, int... T>
+__device__ __forceinline__ void tiled_apply4(std::integer_sequence<int, T...>, char* base,
+                                             uint32_t q16, uint32_t r, const TiledSlots& m,
+                                             const f4 (&x)[kSteps], uint64_t cm, f4& prev) {
   uint32_t a[sizeof...(T)];
-  ((a[T] = bcast<G + T>(m.r) + f4), ...);
-  float av[sizeof...(T)];
-  ((av[T] = *reinterpret_cast<float*>(base + a[T])), ...);
-  // slot t continuing slot t-1's row (same half) chains on its register value
-  ((av[T] = __builtin_fmaf(bcastf<G + T>(m.v), x[G + T],
-                           G + T > 0 ? select_lanes(av[T], T > 0 ? av[T > 0 ? T - 1 : 0] : prev,
-                                                    chain_lanes<G + T>(cm))
-                                     : av[T])),
-   ...);
-  ((*reinterpret_cast<float*>(base + a[T]) = av[T]), ...);
-  prev = av[sizeof...(T) - 1];
+  ((a[T] = gbcast<G + T>(r) + q16), ...);
+  f4 av[sizeof...(T)];
+  if constexpr (GNNREC_TILED_EXP & 1)
+    ((av[T] = f4{__builtin_bit_cast(float, a[T]), 0.f, 0.f, 0.f}), ...);
+  else
+    ((av[T] = *reinterpret_cast<const f4*>(base + a[T])), ...);
+  if constexpr (CHAIN) {
+    // slot t continuing slot t-1's row (same stream) chains on its register value
+    ((av[T] = fma4(gbcastf<G + T>(m.v), x[G + T],
+                   G + T > 0 ? select4(av[T], T > 0 ? av[T > 0 ? T - 1 : 0] : prev,
+                                       chain_lanes<G + T>(cm))
+                             : av[T])),
+     ...);
+  } else {
+    ((av[T] = fma4(gbcastf<G + T>(m.v), x[G + T], av[T])), ...);
+  }
+  if constexpr (GNNREC_TILED_EXP & 1)
+    prev = prev + ((av[T]) + ...);
+  else
+    ((*reinterpret_cast<f4*>(base + a[T]) = av[T]), ...);
+  prev = (GNNREC_TILED_EXP & 1) ? prev : av[sizeof...(T) - 1];
 }
 
-__device__ __forceinline__ void tiled_apply(float* acc, uint32_t f4, const TiledSlots& m,
-                                            const float (&x)[kHalf], uint32_t cm) {
-  constexpr auto k8 = std::make_integer_sequence<int, kGroup>{};
+template <bool CHAIN>
+__device__ __forceinline__ void tiled_apply(float* acc, uint32_t q16, const TiledSlots& m,
+                                            const f4 (&x)[kSteps], uint64_t cm, f4& sink) {
+  constexpr auto k4 = std::make_integer_sequence<int, kApply>{};
   char* base = reinterpret_cast<char*>(acc);
-  float prev = 0.f;
-  tiled_apply8<0>(k8, base, f4, m, x, cm, prev);
-  tiled_apply8<kGroup>(k8, base, f4, m, x, cm, prev);
+  f4 prev = (GNNREC_TILED_EXP & 1) ? sink : f4{0.f, 0.f, 0.f, 0.f};
+  const uint32_t r = (m.w & kRowMask) * kRowBytes;   // this lane's slot's accumulator row
+  tiled_apply4<CHAIN, 0>(k4, base, q16, r, m, x, cm, prev);
+  tiled_apply4<CHAIN, kApply>(k4, base, q16, r, m, x, cm, prev);
+  if (GNNREC_TILED_EXP & 1) sink = prev;
 }
 
-// Pass-end epilogue of one half-wave: its rows i = rl + 32q of the block (rl = 2 * wave +
-// half), B at a time with every load of a batch issued before the first use. All offsets are
-// 32-bit rows of buffers based at the block's first row whose ranges end at the last valid
-// row: loads past it return 0 and stores are dropped, so there is no branch (a branch around
-// a load makes the compiler wait for it in place). A null ry: no y output.
+// Pass-end epilogue of one 8-lane group: its rows i = rl + 128 j of the block (rl = 8 * wave
+// + group), B at a time with every load of a batch issued before the first use; lane q moves
+// 16 B of each row. All offsets are 32-bit rows of buffers based at the block's first row
+// whose ranges end at the last valid row: loads past it return 0 and stores are dropped, so
+// there is no branch (a branch around a load makes the compiler wait for it in place). A null
+// ry: no y output.
 // NB base inputs (the layer-mean terms before this hop, in layer order): acc_out =
 // (((b0 [+ b1]) [+ b2]) + y) [/ div] — b0 = x0 (ACC_INIT) or the running sum (ACC_ADD);
 // INIT|ADD: b0 = x0, b1 = the acc rows (an earlier layer parked there); ACC_X: the hop's
-// input row x[r] (the previous layer) last. NB = 0: y only.
+// input row (the previous layer) last. NB = 0: y only.
 template <int NB, int B, class Wait>
-__device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, uint32_t f4,
+__device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, uint32_t q16,
                                                __amdgpu_buffer_rsrc_t ry, uint32_t ly,
                                                __amdgpu_buffer_rsrc_t rb0, uint32_t lb0,
                                                __amdgpu_buffer_rsrc_t rb1, uint32_t lb1,
                                                __amdgpu_buffer_rsrc_t rb2, uint32_t lb2,
                                                __amdgpu_buffer_rsrc_t ra, uint32_t la,
                                                bool div, float acc_div, Wait wait) {
-  constexpr int kStride = 2 * kTiledWaves;
+  constexpr int kStride = kGroups * kTiledWaves;
   const __amdgpu_buffer_rsrc_t rb[3] = {rb0, rb1, rb2};
   const uint32_t lb[3] = {lb0, lb1, lb2};
-  float base[NB > 0 ? NB : 1][B];
+  f4 base[NB > 0 ? NB : 1][B];
   // the base rows of batch i0 (global, independent of the pass: the first batch is loaded
   // before the pass-end barriers, so its latency hides behind the block's slowest wave)
   auto load_base = [&](int i0) {
@@ -228,15 +306,14 @@ __device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, 
     uint32_t ob[3];
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      ob[j] = (uint32_t)i0 * lb[j] + f4;
+      ob[j] = (uint32_t)i0 * lb[j] + q16;
       asm volatile("" : "+v"(ob[j]));
     }
 #pragma unroll
     for (int q = 0; q < B; ++q)
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        base[j][q] =
-            __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb[j], ob[j], 0, 0));
+        base[j][q] = load4(rb[j], ob[j]);
         ob[j] += kStride * lb[j];
       }
   };
@@ -245,36 +322,44 @@ __device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, 
   wait();
   // the first batch runs even when rl is past the block's rows: its LDS reads stay inside
   // (row R is the scratch row) and its stores fall outside the buffer ranges
+  const char* lds = reinterpret_cast<const char*>(acc);
   for (;;) {
     if (!GNNREC_TILED_EPI_PRELOAD) load_base(i0);
     uint32_t ol = (uint32_t)i0;
     asm volatile("" : "+v"(ol));
-    float a[B];
+    f4 a[B];
 #pragma unroll
     for (int q = 0; q < B; ++q) {
-      a[q] = acc[min(ol, (uint32_t)R) * kSlice + (f4 >> 2)];
+      a[q] = *reinterpret_cast<const f4*>(lds + min(ol, (uint32_t)R) * kRowBytes + q16);
       ol += kStride;
     }
-    uint32_t oy = (uint32_t)i0 * ly + f4, oa = (uint32_t)i0 * la + f4;
+    uint32_t oy = (uint32_t)i0 * ly + q16, oa = (uint32_t)i0 * la + q16;
     asm volatile("" : "+v"(oy), "+v"(oa));
 #pragma unroll
     for (int q = 0; q < B; ++q) {
-      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, a[q]), ry, oy, 0, kEpiStoreAux);
+      store4(a[q], ry, oy);
       oy += kStride * ly;
       if (NB > 0) {
-        float bsum = base[0][q];
+        f4 bsum = base[0][q];
 #pragma unroll
         for (int j = 1; j < NB; ++j) bsum = bsum + base[j][q];
         bsum = bsum + a[q];
         if (div) bsum = bsum / acc_div;
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, bsum), ra, oa, 0, kEpiStoreAux);
+        store4(bsum, ra, oa);
         oa += kStride * la;
       }
     }
     i0 += kStride * B;
-    if (i0 - (rl & 1) >= R) break;
+    if (i0 - (rl & (kGroups - 1)) >= R) break;   // wave-uniform: the wave's first row
     if (GNNREC_TILED_EPI_PRELOAD) load_base(i0);
   }
+}
+
+// the main loop unrolled over one turn of the pipeline rings (compile-time ring indices)
+template <class F, int... I>
+__device__ __forceinline__ void run_ring(std::integer_sequence<int, I...>, F&& stage) {
+  for (;;)
+    if ((stage(std::integral_constant<int, I>{}) || ...)) break;
 }
 
 __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
@@ -285,13 +370,11 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     float* __restrict__ y, int64_t ldy, int64_t n_rows, int epi, const float* __restrict__ self,
     int64_t ld_self, float* __restrict__ accg, int64_t ld_acc, float acc_div,
     unsigned* __restrict__ sync, unsigned meet_ticks) {
-  extern __shared__ float acc[];  // [(R+1)][32]: row R is the padding slots' scratch row
-  constexpr auto kSeq = std::make_integer_sequence<int, kHalf>{};
+  extern __shared__ f4 acc4[];   // [(R+1)][32] floats: row R is the padding slots' scratch row
+  float* acc = reinterpret_cast<float*>(acc4);
+  constexpr auto kSeq = std::make_integer_sequence<int, kSteps>{};
   const int lane = threadIdx.x & 63;
-  const int half = lane >> 5;
-  const int f = lane & 31;
-  const uint32_t f4 = (uint32_t)f * 4;
-  const int my_slot = half * kHalf + (lane & 15);
+  const uint32_t q16 = (uint32_t)(lane & 7) * 16;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   unsigned* ctr = sync + (blockIdx.x % 8) * 32;   // the group's counter, own 128-B line
   const long long G = gridDim.x / 8 + ((blockIdx.x % 8) < (gridDim.x % 8) ? 1 : 0);
@@ -311,47 +394,56 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     }
     const int slice = item / nb_pad, blk = item - slice * nb_pad;
     if (blk >= n_blocks) continue;   // padding item (uniform over the workgroup)
-    for (int i = threadIdx.x; i < (R + 1) * kSlice; i += kTiledWaves * 64) acc[i] = 0.f;
+    {
+      const f4 z = {0.f, 0.f, 0.f, 0.f};
+      for (int i = threadIdx.x; i < (R + 1) * (kSlice / 4); i += kTiledWaves * 64) acc4[i] = z;
+    }
     __syncthreads();
     GNNREC_TILED_STAMP(ev);
-    const uint32_t soff = (uint32_t)slice * kSlice * 4;
+    const uint32_t soff = (uint32_t)slice * kRowBytes;
     const char* xs = reinterpret_cast<const char*>(x) + soff;
     const uint64_t xs_bytes = x_bytes - soff;
     const int64_t s = (int64_t)blk * kTiledWaves + w;
     const int64_t b = wptr[s], e = wptr[s + 1];
     int cur = 0;
+    f4 sink = {0.f, 0.f, 0.f, 0.f};   // diagnostic builds only (GNNREC_TILED_EXP & 1)
     if (b < e) {
-      // slot loads (and headers) two chunks ahead, gathers one chunk ahead of the LDS chain (a
-      // third chunk of gathers in flight measured the same: profiles/r02/tiled_depth3.jsonl)
-      TiledSlots M0, M1, M2;
-      float X0[kHalf], X1[kHalf];
+      // a ring of kPlanAhead + 1 slot sets and kGatherAhead + 1 gathered chunks: stage c loads
+      // chunk c + kPlanAhead's slots, gathers chunk c + kGatherAhead and applies chunk c
+      TiledSlots M[kMRing];
+      f4 X[kXRing][kSteps];
       int64_t c = b;
-      tiled_slots(ss, sv, hdr, c, my_slot, lane, row_bytes, M0);
-      tiled_slots(ss, sv, hdr, c + 1, my_slot, lane, row_bytes, M1);
-      tiled_gather(kSeq, chunk_rsrc(xs, xs_bytes, hdr_word<2>(M0), row_bytes), f4, M0, X0);
-#define GNNREC_TILED_STAGE(MLOAD, MG, XG, MA, XA)                                     \
-  {                                                                                   \
-    tiled_slots(ss, sv, hdr, c + 2, my_slot, lane, row_bytes, MLOAD);                 \
-    tiled_gather(kSeq, chunk_rsrc(xs, xs_bytes, hdr_word<2>(MG), row_bytes), f4, MG, XG); \
-    const int bar = (int)hdr_word<0>(MA);                                             \
-    for (int i = 0; i < bar; ++i) {                                                   \
-      __syncthreads();                                                                \
-      GNNREC_TILED_STAMP(ev);                                                         \
-    }                                                                                 \
-    cur += bar;                                                                       \
-    tiled_apply(acc, f4, MA, XA, hdr_word<1>(MA));                                    \
-    if (++c >= e) break;                                                              \
-  }
-      for (;;) {
-        GNNREC_TILED_STAGE(M2, M1, X1, M0, X0)
-        GNNREC_TILED_STAGE(M0, M2, X0, M1, X1)
-        GNNREC_TILED_STAGE(M1, M0, X1, M2, X0)
-        GNNREC_TILED_STAGE(M2, M1, X0, M0, X1)
-        GNNREC_TILED_STAGE(M0, M2, X1, M1, X0)
-        GNNREC_TILED_STAGE(M1, M0, X0, M2, X1)
-      }
-#undef GNNREC_TILED_STAGE
+#pragma unroll
+      for (int j = 0; j < kPlanAhead; ++j) tiled_slots(ss, sv, hdr, c + j, lane, M[j]);
+#pragma unroll
+      for (int j = 0; j < kGatherAhead; ++j)
+        tiled_gather(kSeq, chunk_rsrc(xs, xs_bytes, hdr_word<3>(M[j]), row_bytes), q16,
+                     row_bytes, M[j], X[j]);
+      auto stage = [&](auto ic) -> bool {
+        constexpr int I = decltype(ic)::value;
+        tiled_slots(ss, sv, hdr, c + kPlanAhead, lane, M[(I + kPlanAhead) % kMRing]);
+        {
+          const TiledSlots& mg = M[(I + kGatherAhead) % kMRing];
+          tiled_gather(kSeq, chunk_rsrc(xs, xs_bytes, hdr_word<3>(mg), row_bytes), q16,
+                       row_bytes, mg, X[(I + kGatherAhead) % kXRing]);
+        }
+        const TiledSlots& ma = M[I % kMRing];
+        const int bar = (int)hdr_word<0>(ma);
+        for (int i = 0; i < bar; ++i) {
+          if (!(GNNREC_TILED_EXP & 4)) __syncthreads();
+          GNNREC_TILED_STAMP(ev);
+        }
+        cur += bar;
+        const uint64_t cm = (uint64_t)hdr_word<1>(ma) | ((uint64_t)hdr_word<2>(ma) << 32);
+        if (cm)
+          tiled_apply<true>(acc, q16, ma, X[I % kXRing], cm, sink);
+        else
+          tiled_apply<false>(acc, q16, ma, X[I % kXRing], 0, sink);
+        return ++c >= e;
+      };
+      run_ring(std::make_integer_sequence<int, kRingUnroll>{}, stage);
     }
+    if (GNNREC_TILED_EXP & 1) *reinterpret_cast<f4*>(reinterpret_cast<char*>(acc) + R * kRowBytes + q16) = sink;
     const int ns = nsteps[blk];
     auto wait = [&]() {
       for (int i = cur; i < ns; ++i) {  // this wave's remaining steps + the last
@@ -359,10 +451,10 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
         GNNREC_TILED_STAMP(ev);
       }
     };
-    // epilogue: half-wave h of wave w owns rows i = 2w + h + 32q (see tiled_epilogue)
+    // epilogue: group g of wave w owns rows i = 8w + g + 128j (see tiled_epilogue)
     const int64_t r0 = (int64_t)blk * R;
     const int nv = (int)min((int64_t)R, n_rows - r0);
-    const int rl = 2 * w + half;
+    const int rl = kGroups * w + (lane >> 3);
     const __amdgpu_buffer_rsrc_t ry = rows_rsrc((epi & GNNREC_EPI_NO_Y) ? nullptr : y, r0, ldy,
                                                 slice, nv);
     // base inputs in layer order: x0 (INIT), the acc rows (ADD), the input rows (ACC_X)
@@ -377,7 +469,7 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     const uint32_t lb0 = init ? ls : la, lb1 = (init && add) ? la : row_bytes;
     const bool div = (epi & GNNREC_EPI_ACC_DIV) != 0;
 #define GNNREC_TILED_EPI(NB, B, DIV) \
-  tiled_epilogue<NB, B>(acc, R, rl, f4, ry, ly, rb0, lb0, rb1, lb1, rx, row_bytes, racc, la, DIV, \
+  tiled_epilogue<NB, B>(acc, R, rl, q16, ry, ly, rb0, lb0, rb1, lb1, rx, row_bytes, racc, la, DIV, \
                         acc_div, wait)
     if (nb == 0)
       GNNREC_TILED_EPI(0, kEpiBatch, false);
@@ -404,7 +496,7 @@ extern "C" int gnnrec_debug_tiled_trace(void* buf) {
 // ---- host plan builder --------------------------------------------------------------------
 namespace {
 
-constexpr int kVirt = 2 * kTiledWaves;   // slot streams per block: (wave, half)
+constexpr int kVirt = kGroups * kTiledWaves;   // slot streams per block: (wave, group)
 
 struct Run {
   int32_t p, row;   // panel, local row
@@ -429,16 +521,15 @@ struct Slot {
   int32_t t;        // edge of the run
 };
 
-// One stream's slots of a step cut into groups of kGroup (two groups = its half of a chunk):
-// slots in ascending column sub-panel, rows in order inside one (a row's edges keep their
-// column order); a row appears in a group only as ONE run of consecutive slots (the kernel
-// reads a group's accumulators before it writes any) — a slot that would repeat a row
-// non-adjacently is deferred, with the rest of that row, to a later group (per-row order
-// kept). Padded to a multiple of kHalf.
-void half_chunks(const std::vector<const Run*>& runs, const int32_t* col, int sub_panel,
-                 std::vector<Slot>& seq) {
+// One stream's slots of a step cut into groups of kApply (the kernel reads a group's
+// accumulators before it writes any): slots in ascending column sub-panel, rows in order
+// inside one (a row's edges keep their column order); a row appears in a group only as ONE
+// run of consecutive slots — a slot that would repeat a row non-adjacently is deferred, with
+// the rest of that row, to a later group (per-row order kept). Padded to a multiple of kSteps.
+void stream_slots(const std::vector<const Run*>& runs, const int32_t* col, int sub_panel,
+                  std::vector<Slot>& seq) {
   std::vector<Slot> pending, deferred;
-  std::vector<int> in_chunk, blocked;
+  std::vector<int> in_group, blocked;
   seq.clear();
   for (const Run* e : runs)
     for (int t = 0; t < e->n; ++t) pending.push_back({e, t});
@@ -449,33 +540,34 @@ void half_chunks(const std::vector<const Run*>& runs, const int32_t* col, int su
     });
   while (!pending.empty()) {
     deferred.clear();
-    in_chunk.clear();
+    in_group.clear();
     blocked.clear();
     int n = 0, last = -1;
     const size_t start = seq.size();
     for (size_t q = 0; q < pending.size(); ++q) {
       const Slot& sl = pending[q];
-      if (n == kGroup) {   // group full: the rest keeps its order for the next ones
+      if (n == kApply) {   // group full: the rest keeps its order for the next ones
         deferred.insert(deferred.end(), pending.begin() + q, pending.end());
         break;
       }
       const int r = sl.run->row;
       const bool is_blocked = std::find(blocked.begin(), blocked.end(), r) != blocked.end();
-      const bool seen = std::find(in_chunk.begin(), in_chunk.end(), r) != in_chunk.end();
+      const bool seen = std::find(in_group.begin(), in_group.end(), r) != in_group.end();
       if (is_blocked || (seen && r != last)) {
         if (seen && r != last && !is_blocked) blocked.push_back(r);
         deferred.push_back(sl);
         continue;
       }
       seq.push_back(sl);
-      if (!seen) in_chunk.push_back(r);
+      if (!seen) in_group.push_back(r);
       last = r;
       ++n;
     }
-    while (seq.size() - start < (size_t)kGroup) seq.push_back({nullptr, 0});
+    if (!deferred.empty())   // only the stream's last group may end short
+      while (seq.size() - start < (size_t)kApply) seq.push_back({nullptr, 0});
     pending.swap(deferred);
   }
-  while (seq.size() % kHalf) seq.push_back({nullptr, 0});
+  while (seq.size() % kSteps) seq.push_back({nullptr, 0});
 }
 
 void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_t n_rows,
@@ -498,13 +590,13 @@ void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_
   int64_t load[kVirt];
   std::vector<const Run*> wl[kVirt];
   std::vector<const Run*> g;
-  std::vector<Slot> hs[2];
+  std::vector<Slot> hs[kGroups];
   int32_t step = 0;
   size_t i = 0;
   while (i < runs.size()) {
     size_t j = i;
     while (j < runs.size() && runs[j].p == runs[i].p) ++j;
-    // LPT over the (wave, half) streams: longest run first onto the least loaded
+    // LPT over the (wave, group) streams: longest run first onto the least loaded
     g.clear();
     for (size_t q = i; q < j; ++q) g.push_back(&runs[q]);
     std::stable_sort(g.begin(), g.end(), [](const Run* a, const Run* c) { return a->n > c->n; });
@@ -521,36 +613,42 @@ void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_
     }
     const uint32_t base = (uint32_t)runs[i].p * (uint32_t)panel;   // the step's first column
     for (int w = 0; w < kTiledWaves; ++w) {
-      if (wl[2 * w].empty() && wl[2 * w + 1].empty()) continue;
-      for (int h = 0; h < 2; ++h) half_chunks(wl[2 * w + h], col, sub_panel, hs[h]);
-      const size_t n = std::max(hs[0].size(), hs[1].size());
-      for (int h = 0; h < 2; ++h) hs[h].resize(n, Slot{nullptr, 0});
+      bool any = false;
+      for (int q = 0; q < kGroups; ++q) any |= !wl[kGroups * w + q].empty();
+      if (!any) continue;
+      size_t n = 0;
+      for (int q = 0; q < kGroups; ++q) {
+        stream_slots(wl[kGroups * w + q], col, sub_panel, hs[q]);
+        n = std::max(n, hs[q].size());
+      }
+      for (int q = 0; q < kGroups; ++q) hs[q].resize(n, Slot{nullptr, 0});
       uint32_t bar = (uint32_t)(step - cur[w]);
-      for (size_t c = 0; c < n; c += kHalf) {
+      for (size_t c = 0; c < n; c += kSteps) {
         // padding slots gather a line the chunk fetches anyway (its first real slot's)
         uint32_t x0 = 0;
         for (int q = 0; q < kTiledChunk; ++q) {
-          const Slot& sl = hs[q / kHalf][c + q % kHalf];
+          const Slot& sl = hs[q / kSteps][c + q % kSteps];
           if (sl.run) {
             x0 = (uint32_t)col[sl.run->k + sl.t] - base;
             break;
           }
         }
-        uint32_t cmask = 0;
-        for (int h = 0; h < 2; ++h)
-          for (int t = 0; t < kHalf; ++t) {
-            const Slot& sl = hs[h][c + t];
+        uint64_t cmask = 0;
+        for (int q = 0; q < kGroups; ++q)       // lane 8 q + t: slot t of stream q
+          for (int t = 0; t < kSteps; ++t) {
+            const Slot& sl = hs[q][c + t];
             if (!sl.run) {
               out.slot[w].push_back(x0 << kRowBits | (uint32_t)R);
               out.val[w].push_back(0.f);
               continue;
             }
             const int64_t k = sl.run->k + sl.t;
-            if (t > 0 && hs[h][c + t - 1].run == sl.run) cmask |= 1u << (16 * h + t);
+            if (t > 0 && hs[q][c + t - 1].run == sl.run) cmask |= 1ull << (kSteps * q + t);
             out.slot[w].push_back(((uint32_t)col[k] - base) << kRowBits | (uint32_t)sl.run->row);
             out.val[w].push_back(val[k]);
           }
-        out.hdr[w].insert(out.hdr[w].end(), {bar, cmask, base, 0u});
+        out.hdr[w].insert(out.hdr[w].end(),
+                          {bar, (uint32_t)cmask, (uint32_t)(cmask >> 32), base});
         bar = 0;
       }
       cur[w] = step;
@@ -632,7 +730,7 @@ extern "C" int gnnrec_tiled_plan_emit(void* plan, uint32_t* slot, float* val, ui
       std::copy(bp.hdr[w].begin(), bp.hdr[w].end(), hdr + 4 * c);
     }
   }
-  // tail chunks for the last prefetches: harmless slots (row 0 of x, row field all ones)
+  // tail chunks for the last prefetches: harmless slots (row 0 of x, the scratch-row field)
   const int64_t end = wave_ptr[nb * kTiledWaves];
   for (int64_t s = end * kTiledChunk; s < (end + kTiledTail) * kTiledChunk; ++s) {
     slot[s] = (uint32_t)kRowMask;
@@ -680,13 +778,15 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
                  "spmm_tiled: bad rows_per_block");
   GNNREC_REQUIRE(n_rows >= 0 && n_blocks == (n_rows + rows_per_block - 1) / rows_per_block,
                  "spmm_tiled: n_blocks does not match n_rows / rows_per_block");
-  GNNREC_REQUIRE(ldx >= d && x_rows >= 0 && ldx * 4 <= kMaxRowBytes,
-                 "spmm_tiled: need d <= ldx <= %d", kMaxRowBytes / 4);
-  GNNREC_REQUIRE((epi & GNNREC_EPI_NO_Y) || (y && ldy >= d), "spmm_tiled: null y or ldy < d");
-  GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_INIT) || (self && ld_self >= d),
-                 "spmm_tiled: ACC_INIT needs self");
-  GNNREC_REQUIRE(!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) || (acc && ld_acc >= d),
-                 "spmm_tiled: ACC needs acc");
+  GNNREC_REQUIRE(ldx >= d && ldx % 4 == 0 && x_rows >= 0 && ldx * 4 <= kMaxRowBytes,
+                 "spmm_tiled: need d <= ldx <= %d and ldx %% 4 == 0", kMaxRowBytes / 4);
+  GNNREC_REQUIRE((epi & GNNREC_EPI_NO_Y) || (y && ldy >= d && ldy % 4 == 0),
+                 "spmm_tiled: null y or ldy < d or ldy %% 4 != 0");
+  GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_INIT) || (self && ld_self >= d && ld_self % 4 == 0),
+                 "spmm_tiled: ACC_INIT needs self (ld %% 4 == 0)");
+  GNNREC_REQUIRE(!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) ||
+                     (acc && ld_acc >= d && ld_acc % 4 == 0),
+                 "spmm_tiled: ACC needs acc (ld %% 4 == 0)");
   GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_X) ||
                      ((epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) && x_rows >= n_rows),
                  "spmm_tiled: ACC_X needs ACC_INIT or ACC_ADD and a square operand");
@@ -700,12 +800,16 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
   if (n_rows == 0) return GNNREC_OK;
   GNNREC_REQUIRE(slot && val && hdr && wave_ptr && n_steps && x && sync,
                  "spmm_tiled: null pointer");
+  GNNREC_REQUIRE(aligned16(x) && ((epi & GNNREC_EPI_NO_Y) || aligned16(y)) &&
+                     (!(epi & GNNREC_EPI_ACC_INIT) || aligned16(self)) &&
+                     (!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) || aligned16(acc)),
+                 "spmm_tiled: x / y / self / acc must be 16-B aligned");
   hipStream_t s = as_hip(stream);
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 256;
-  const size_t lds = (size_t)(rows_per_block + 1) * kSlice * sizeof(float);
+  const size_t lds = (size_t)(rows_per_block + 1) * kRowBytes;
   if (lds > 64 * 1024 && tiled_lds_attribute(dev) < 0) {
     set_error("spmm_tiled: the device refused %zu bytes of dynamic LDS", lds);
     return GNNREC_EHIP;

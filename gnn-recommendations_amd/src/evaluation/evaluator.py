@@ -50,8 +50,31 @@ def compute_metrics_from_topk(topk_items, user_ids: List[int], ground_truth: Dic
     return out
 
 
-def embedding_statistics(emb: torch.Tensor, exact_limit: int = 65536,
-                         chunk: int = 4096) -> Dict[str, float]:
+def _row_chunks(parts, rows: int):
+    """(global first row, fp32 chunk) over the row-concatenation of `parts`, `rows` at a time
+    (a chunk never spans two parts; nothing is copied beyond one chunk)."""
+    r0 = 0
+    for p in parts:
+        for s in range(0, p.shape[0], rows):
+            yield r0 + s, p[s:s + rows].detach().float()
+        r0 += p.shape[0]
+
+
+def _take_rows(parts, idx: torch.Tensor) -> torch.Tensor:
+    """Rows `idx` (global, in that order) of the row-concatenation of `parts`."""
+    out = torch.empty((idx.numel(), parts[0].shape[1]), dtype=torch.float32,
+                      device=parts[0].device)
+    r0 = 0
+    for p in parts:
+        sel = ((idx >= r0) & (idx < r0 + p.shape[0])).nonzero().flatten()
+        if sel.numel():
+            out[sel] = p.detach()[idx[sel] - r0].float()
+        r0 += p.shape[0]
+    return out
+
+
+def embedding_statistics(emb, exact_limit: int = 65536, chunk: int = 4096,
+                         stat_rows: int = 1 << 20) -> Dict[str, float]:
     """The over-smoothing statistics evaluate() adds (evaluator.py:116-121 ->
     training/metrics.py:229-315), on the propagated table where it lives:
     mcs = mean off-diagonal cosine similarity, mad = mean off-diagonal pairwise Euclidean
@@ -60,32 +83,52 @@ def embedding_statistics(emb: torch.Tensor, exact_limit: int = 65536,
     here mcs is the exact identity (||sum e_n||^2 - sum ||e_n||^2) / (N (N-1)) over
     L2-normalised rows and mad runs over row chunks, so nothing N x N is held. Above
     `exact_limit` nodes mad is taken over a fixed-seed sample of that many rows (flagged
-    'mad_sampled'). Values agree with the reference to fp32 reassociation."""
-    e = emb.detach().float()
-    n = e.shape[0]
+    'mad_sampled'). Values agree with the reference to fp32 reassociation.
+
+    `emb` is one [N, d] table or a sequence of tables read as their row-concatenation (the
+    user and item halves: no torch.cat copy). mcs and variance run over `stat_rows`-row
+    chunks with float64 sums, so the transient memory is a chunk, not the table (G100M:
+    ~0.5 GB instead of ~150 GB of float64 copies)."""
+    parts = [emb] if torch.is_tensor(emb) else [p for p in emb if p.shape[0] > 0]
+    n = sum(p.shape[0] for p in parts)
     out: Dict[str, float] = {}
     if n < 2:
         return {"mcs": float("nan"), "mad": float("nan"), "variance": float("nan")}
-    en = torch.nn.functional.normalize(e, p=2, dim=1).double()
-    s = en.sum(0)
-    out["mcs"] = float(((s @ s) - (en * en).sum()) / (n * (n - 1)))
-    sub = e
+    dev = parts[0].device
+    d = parts[0].shape[1]
+    s = torch.zeros(d, dtype=torch.float64, device=dev)
+    ss = torch.zeros((), dtype=torch.float64, device=dev)
+    colsum = torch.zeros(d, dtype=torch.float64, device=dev)
+    for _, c in _row_chunks(parts, stat_rows):
+        en = torch.nn.functional.normalize(c, p=2, dim=1).double()
+        s += en.sum(0)
+        ss += (en * en).sum()
+        colsum += c.double().sum(0)
+    out["mcs"] = float(((s @ s) - ss) / (n * (n - 1)))
+    mean = colsum / n
+    dev2 = torch.zeros(d, dtype=torch.float64, device=dev)
+    for _, c in _row_chunks(parts, stat_rows):
+        dev2 += ((c.double() - mean) ** 2).sum(0)
+    variance = float((dev2 / (n - 1)).mean())
     if n > exact_limit:
         g = torch.Generator(device="cpu").manual_seed(0)
-        sub = e[torch.randperm(n, generator=g)[:exact_limit].to(e.device)]
+        sub = _take_rows(parts, torch.randperm(n, generator=g)[:exact_limit].to(dev))
         out["mad_sampled"] = float(exact_limit)
+    else:
+        sub = _take_rows(parts, torch.arange(n, device=dev)) if len(parts) > 1 else \
+            parts[0].detach().float()
     m = sub.shape[0]
     nsq = (sub ** 2).sum(1)
-    tot = torch.zeros((), dtype=torch.float64, device=e.device)
+    tot = torch.zeros((), dtype=torch.float64, device=dev)
     for r0 in range(0, m, chunk):
         blk = sub[r0:r0 + chunk]
         d2 = nsq[r0:r0 + chunk, None] + nsq[None, :] - 2 * (blk @ sub.T)
-        d = torch.sqrt(torch.clamp(d2, min=0))
-        idx = torch.arange(blk.shape[0], device=e.device)
-        d[idx, r0 + idx] = 0.0                       # the diagonal is excluded from the mean
-        tot += d.double().sum()
+        dist = torch.sqrt(torch.clamp(d2, min=0))
+        idx = torch.arange(blk.shape[0], device=dev)
+        dist[idx, r0 + idx] = 0.0                    # the diagonal is excluded from the mean
+        tot += dist.double().sum()
     out["mad"] = float(tot / (m * (m - 1)))
-    out["variance"] = float(e.var(dim=0).mean())
+    out["variance"] = variance
     return out
 
 
@@ -142,5 +185,5 @@ class Evaluator:
             seen_ptr, seen_col = dataset.seen_items(include_valid=mask_valid)
             topk = self.topk(user_emb, item_emb, users, max(self.k_values), seen_ptr, seen_col)
             metrics = compute_metrics_from_topk(topk, users, gt, dataset.n_items, self.k_values)
-            metrics.update(embedding_statistics(torch.cat([user_emb, item_emb], dim=0)))
+            metrics.update(embedding_statistics((user_emb, item_emb)))
             return metrics

@@ -64,8 +64,13 @@ class GATLayer(nn.Module):
 
     @staticmethod
     def _project(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-        """x @ w^T; on a ROCm device the streaming MFMA row GEMM (gnnrec_rows_gemm_f32)."""
-        if x.is_cuda:
+        """x @ w^T; on a ROCm device the streaming MFMA row GEMM (gnnrec_rows_gemm_f32) for the
+        shapes it has an instance for, otherwise — explicitly — a plain library GEMM
+        (hipBLASLt through torch.matmul on the same device; rows_gemm itself never falls
+        back)."""
+        if x.is_cuda and ops.functional.rows_gemm_supported(x.shape[1], w.shape[0]):
+            if not ops.functional._rows_view_ok(x):
+                x = x.contiguous()
             return ops.functional.rows_gemm(x, w.t())
         return x @ w.t()
 
@@ -82,7 +87,10 @@ class GATLayer(nn.Module):
         in_dim-wide gather instead of the H*out_dim-wide h (4x fewer bytes for the last GAT
         layer). Same value reassociated (fp32 tolerance, like the rest of GAT)."""
         return (not self.concat_heads and self.in_dim % 4 == 0
-                and self.n_heads * self.in_dim in (16, 32, 64, 128, 256))
+                and self.n_heads * self.in_dim in (16, 32, 64, 128, 256)
+                # the head mean W_h after the aggregation runs on the native row GEMM only
+                and ops.functional.rows_gemm_supported(self.n_heads * self.in_dim,
+                                                       self.out_dim))
 
     def head_mean_weight(self) -> torch.Tensor:
         """[H*in, out] = vstack(W_h^T) / H: z (per-head aggregates of x) @ this = the head mean."""

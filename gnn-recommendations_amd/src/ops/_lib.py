@@ -17,7 +17,7 @@ import torch  # noqa: F401  (load order: torch's HIP runtime first)
 
 _PKG_ROOT = Path(__file__).resolve().parents[2]
 LIB_PATH = Path(os.environ.get("GNNREC_LIB", _PKG_ROOT / "lib" / "libgnnrec.so"))
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # gnnrec.h epilogue flags
 EPI_ACC_INIT = 1
@@ -27,8 +27,10 @@ EPI_NO_Y = 8
 EPI_ACC_X = 16
 # column-ordered hop plan layout (include/gnnrec.h GNNREC_TILED_*)
 TILED_WAVES = 16
-TILED_CHUNK = 32
-TILED_TAIL = 2
+TILED_GROUPS = 8
+TILED_STEPS = 8
+TILED_CHUNK = 64
+TILED_TAIL = 8
 TILED_MAX_ROWS = 1279
 TILED_SYNC_WORDS = 256
 TILED_HDR_WORDS = 4

@@ -84,12 +84,18 @@ def _tiled_rows_per_block(n_rows: int, device, reserve_cus: int = 0) -> int:
     return min(TILED_MAX_ROWS, -(-n_rows // (passes * cus)))
 
 
+def _tiled_views_ok(*tables) -> bool:
+    """The column-ordered kernel moves 16 B per lane: 16-B aligned rows (ld % 4 == 0)."""
+    return all(t is None or (t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0) for t in tables)
+
+
 def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None,
-                   reserve_cus: int = 0):
-    """The column-ordered plan spmm_into would use for (adj, x), or None (CSR kernel)."""
+                   reserve_cus: int = 0, outputs=()):
+    """The column-ordered plan spmm_into would use for (adj, x) (and the `outputs` tables
+    it writes or reads row-wise), or None (CSR kernel)."""
     if (not TILED_HOP or x_mask is not None or y_active is not None or x.shape[1] % 32
             or adj.n_rows < max(TILED_MIN_ROWS, 1) or adj.nnz == 0
-            or x.stride(0) > TILED_MAX_LDX
+            or x.stride(0) > TILED_MAX_LDX or not _tiled_views_ok(x, *outputs)
             or x.shape[0] * x.shape[1] * 4 < TILED_MIN_TABLE_BYTES
             or adj.max_degree() > TILED_MAX_DEGREE):
         return None
@@ -135,7 +141,9 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
                                  or y_active.numel() < adj.n_rows):
         raise ValueError("y_active must be a uint8 tensor on x's device with a byte per "
                          "destination row")
-    plan = tiled_plan_for(adj, x, x_mask, y_active, reserve_cus)
+    plan = tiled_plan_for(adj, x, x_mask, y_active, reserve_cus,
+                          outputs=(y, self_rows if epi & EPI_ACC_INIT else None,
+                                   acc if epi & (EPI_ACC_INIT | EPI_ACC_ADD) else None))
     if plan is not None:
         spmm_tiled_into(adj, x, y, plan, epi=epi, self_rows=self_rows, acc=acc, acc_div=acc_div,
                         meet_us=meet_us)
@@ -488,12 +496,15 @@ def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh:
                   heads: int, o_dim: int, slope: float = 0.2, mean_heads: bool = False,
                   apply_elu: bool = False, *, out: Optional[torch.Tensor] = None, epi: int = 0,
                   self_rows: Optional[torch.Tensor] = None, acc: Optional[torch.Tensor] = None,
-                  acc_div: float = 1.0, heavy_threshold: int = GAT_HEAVY_THRESHOLD,
+                  acc_div: float = 1.0, heavy_threshold: Optional[int] = None,
                   shared_rows: bool = False) -> Optional[torch.Tensor]:
     """Sparse edge-softmax aggregation of one GAT layer, all heads (gnnrec_gat_aggregate_f32),
     with rows longer than `heavy_threshold` split into segments (gnnrec_gat_heavy_f32).
     shared_rows: `h` is ONE [N, o_dim] table every head aggregates (head_stride 0), e.g. the
-    layer input x when W_h is applied after the aggregation."""
+    layer input x when W_h is applied after the aggregation. heavy_threshold None:
+    GAT_HEAVY_THRESHOLD at call time; 0: no split."""
+    if heavy_threshold is None:
+        heavy_threshold = GAT_HEAVY_THRESHOLD
     h = _rowmajor(h)
     # score tables are read in place with their row strides (e.g. columns of the projection
     # output); only a column-strided view is compacted
@@ -529,35 +540,51 @@ def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh:
     return out
 
 
+def rows_gemm_supported(k: int, p: int) -> bool:
+    """(k, p) shapes gnnrec_rows_gemm_f32 has an instance for (csrc/dense_epi.hip)."""
+    return k in (64, 128, 256) and p % 4 == 0 and 0 < p <= (80 if k == 64 else 64)
+
+
+def _rows_view_ok(t: torch.Tensor) -> bool:
+    return t.dim() == 2 and t.stride(-1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
+
+
 def rows_gemm(x: torch.Tensor, B: torch.Tensor, out: Optional[torch.Tensor] = None, *,
               apply_elu: bool = False, epi: int = 0, self_rows: Optional[torch.Tensor] = None,
               acc: Optional[torch.Tensor] = None, acc_div: float = 1.0) -> Optional[torch.Tensor]:
     """x [n, k] @ B [k, p] on the matrix cores (gnnrec_rows_gemm_f32): the tall-skinny GAT
     projections, streamed at HBM rate instead of hipBLASLt's 1-3 TB/s, with GAT's epilogue
     optionally fused (ELU, then the layer-mean accumulator acc = (self_rows | acc) + y
-    [/ acc_div], as gat_aggregate). fp32 (tolerance-equal to torch.matmul). Shapes the kernel
-    does not take run the same arithmetic through torch on the same device."""
+    [/ acc_div], as gat_aggregate). fp32 (tolerance-equal to torch.matmul). Native only: a
+    shape the kernel has no instance for (rows_gemm_supported), a tensor off x's device or a
+    misaligned view raises — the caller decides what runs instead (GATLayer._project)."""
+    if x.dim() != 2 or B.dim() != 2:
+        raise ValueError("rows_gemm: x and B must be 2-D")
     n, k = x.shape
     p = B.shape[1]
     no_y = bool(epi & EPI_NO_Y)
+    if B.shape[0] != k:
+        raise ValueError(f"rows_gemm: B has {B.shape[0]} rows, x has {k} columns")
+    if not x.is_cuda:
+        raise ValueError("rows_gemm needs x on a ROCm device")
     rows = [t for t in (out, self_rows, acc) if t is not None]
-    ok = (x.is_cuda and x.dtype == torch.float32 and B.dtype == torch.float32
-          and k in (64, 128, 256) and p % 4 == 0 and (p <= 80 if k == 64 else p <= 64)
-          and all(t.stride(-1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
-                  for t in [x] + rows))
-    if not ok:
-        y = torch.matmul(x, B)
-        if apply_elu:
-            y = torch.nn.functional.elu(y)
-        if epi & (EPI_ACC_INIT | EPI_ACC_ADD):
-            b = (self_rows if epi & EPI_ACC_INIT else acc) + y
-            acc.copy_(b / acc_div if epi & EPI_ACC_DIV else b)
-        if no_y:
-            return None
-        if out is not None:
-            out.copy_(y)
-            return out
-        return y
+    for t in [B] + rows:
+        if t.device != x.device:
+            raise ValueError(f"rows_gemm: tensor on {t.device}, x on {x.device}")
+    for t in [x, B] + rows:
+        if t.dtype != torch.float32:
+            raise TypeError(f"rows_gemm: expected float32, got {t.dtype}")
+    for t, w in ((out, p), (self_rows, p), (acc, p)):
+        if t is not None and (t.shape[0] != n or t.shape[1] < w):
+            raise ValueError("rows_gemm: out / self_rows / acc must be [n, >= p]")
+    if epi & EPI_ACC_INIT and self_rows is None or epi & (EPI_ACC_INIT | EPI_ACC_ADD) and acc is None:
+        raise ValueError("rows_gemm: the ACC epilogue needs acc (and self_rows for ACC_INIT)")
+    if not rows_gemm_supported(k, p):
+        raise NotImplementedError(f"rows_gemm: no kernel instance for k={k}, p={p} "
+                                  "(k 64: p <= 80; k 128/256: p <= 64; p % 4 == 0)")
+    if not all(_rows_view_ok(t) for t in [x] + rows):
+        raise ValueError("rows_gemm: x / out / self_rows / acc must be row-major views with "
+                         "ld % 4 == 0 and 16-B aligned rows")
     Bc = B.contiguous()
     if out is None and not no_y:
         out = torch.empty((n, p), dtype=torch.float32, device=x.device)

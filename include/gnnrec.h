@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GNNREC_ABI_VERSION 6
+#define GNNREC_ABI_VERSION 7
 
 typedef struct ihipStream_t* gnnrec_stream_t;
 
@@ -139,29 +139,36 @@ int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col, const
  * columns; steps are separated by a workgroup barrier; the workgroups of a blockIdx%8 group
  * start each pass together), so the rows of an XCD gather each source row while it is in that
  * XCD's L2. The features are done in 32-wide slices (one 128-B cache line of a source row per
- * gather), one slice per pass of a block, so a 160 KB LDS holds 1279 rows' accumulators; the
- * two 32-lane halves of a wave take two slot streams. Every row is still +0 then one fmaf per
- * neighbour in ascending column order: bit-exact.
+ * gather), one slice per pass of a block, so a 160 KB LDS holds 1279 rows' accumulators. A
+ * wave runs GNNREC_TILED_GROUPS slot streams, one per 8-lane group (16 B of the line per
+ * lane). Every row is still +0 then one fmaf per neighbour in ascending column order:
+ * bit-exact.
  *
  * The operand is re-laid out once on the host from the CSR (gnnrec_tiled_plan_build, then
  * gnnrec_tiled_plan_emit into caller buffers, then gnnrec_tiled_plan_free); the plan depends
  * on neither d nor the x table's stride. Per (block, wave) the plan is a run of chunks; a
- * chunk is GNNREC_TILED_CHUNK slots, the first half for lanes 0-31, the second for lanes 32-63
- * (a slot stream each); a slot is one uint32 word ((col - panel base) << 11 | local row; row
- * rows_per_block = a padding slot) and one fp32 value; per chunk hdr[4] = {step barriers
- * before the chunk, chain mask: bit t (first half) / 16 + t (second half) = slot t continues
- * slot t-1's row, panel base column (every slot of a chunk lies in one panel of at most 2^20
- * columns), 0}. Inside a half, a row appears in each group of 8 slots as at most one run of
+ * chunk is GNNREC_TILED_STEPS steps x GNNREC_TILED_GROUPS streams = GNNREC_TILED_CHUNK slots,
+ * entry 8 g + t = slot t of stream g (ABI 7; ABI 6 had two 16-slot halves); a slot is one
+ * uint32 word ((col - panel base) << 11 | local row; row rows_per_block = a padding slot) and
+ * one fp32 value; per chunk hdr[4] = {step barriers before the chunk, chain mask bits 0-31,
+ * bits 32-63 (bit 8 g + t = slot t of stream g continues slot t-1's row), panel base column
+ * (every slot of a chunk lies in one panel of at most 2^20 columns)}. Inside a stream a row
+ * appears in each group of 4 slots (steps 0-3, 4-7 of a chunk) as at most one run of
  * consecutive slots. Slot arrays hold (n_chunks + GNNREC_TILED_TAIL) * GNNREC_TILED_CHUNK
  * entries, hdr 4 * (n_chunks + GNNREC_TILED_TAIL) (tail chunks read by the last prefetches);
  * wave_ptr [n_blocks * GNNREC_TILED_WAVES + 1] are chunk offsets; n_steps [n_blocks].
  * rows_per_block <= GNNREC_TILED_MAX_ROWS. gnnrec_spmm_tiled_f32 needs d % 32 == 0,
- * d <= ldx <= GNNREC_TILED_MAX_LDX (any table size), `sync`: a device scratch of
- * GNNREC_TILED_SYNC_WORDS uint32 (zeroed per call), and meet_us: the bound of the pass-start
- * meeting in microseconds (0: no meeting — e.g. when other kernels share the device). */
+ * d <= ldx <= GNNREC_TILED_MAX_LDX (any table size), every table 16-B aligned with its
+ * leading dimension a multiple of 4, `sync`: a device scratch of GNNREC_TILED_SYNC_WORDS
+ * uint32 (zeroed per call), and meet_us: the bound of the pass-start meeting in microseconds
+ * (0: no meeting — e.g. when other kernels share the device). */
+#ifndef GNNREC_TILED_WAVES   /* experiment builds may override it (plan and kernel together) */
 #define GNNREC_TILED_WAVES 16
-#define GNNREC_TILED_CHUNK 32
-#define GNNREC_TILED_TAIL 2
+#endif
+#define GNNREC_TILED_GROUPS 8
+#define GNNREC_TILED_STEPS 8
+#define GNNREC_TILED_CHUNK 64
+#define GNNREC_TILED_TAIL 8
 #define GNNREC_TILED_MAX_ROWS 1279
 #define GNNREC_TILED_SYNC_WORDS 256
 #define GNNREC_TILED_HDR_WORDS 4

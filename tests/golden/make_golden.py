@@ -190,6 +190,151 @@ def make_edge_paths(gb, OBG, ESBC, PT):
     print(f"edge_paths: E={src.size}")
 
 
+def ml1m_golden_graph():
+    """The ML-1M-shaped pairs stored in lightgcn_ml1m_K3_d64.npz (config 2's graph)."""
+    with np.load(OUT / "lightgcn_ml1m_K3_d64.npz", allow_pickle=False) as z:
+        return (z["users"].astype(np.int64), z["items"].astype(np.int64), int(z["n_users"]),
+                int(z["n_items"]))
+
+
+def ml1m_rows(norm):
+    """The output rows a real-shape fixture keeps: every heavy row (> 256 neighbours, up to
+    5 857) plus every 13th row (the whole [N, (K+1) d] tables would be 10 MB per model)."""
+    deg = np.bincount(norm.row, minlength=norm.shape[0])
+    return np.union1d(np.nonzero(deg > 256)[0], np.arange(0, norm.shape[0], 13)).astype(np.int64)
+
+
+def make_ml1m_models(gb, NGCF, GSL, OBG):
+    """Config 3's models on config 2's real-shape graph (rows of up to 5 857 neighbours)
+    instead of the 800-node g_small: the reference's NGCF K=3 d=64 (ngcf.py:52-86, 170-190),
+    NGCF + GAS composed from the reference's own NGCFLayer and GroupShuffleLayer
+    (x_{l+1} = GS_l(NGCFLayer_l(x_l)), group_shuffle_layer.py:73-96 — the reference has no
+    such model class), and OrthogonalBundleGNN on the adjacency path (model.py:120-213)."""
+    import torch
+    u, i, nu, ni = ml1m_golden_graph()
+    norm, _, t_adj = ref_graph(gb, u, i, nu, ni)
+    rows = ml1m_rows(norm)
+
+    def ngcf(seed):
+        torch.manual_seed(seed)
+        m = NGCF(nu, ni, embedding_dim=64, layer_sizes=[64, 64, 64], dropout=0.1,
+                 init_scale=0.1)
+        with torch.no_grad():
+            for L in m.layers:
+                L.W1.bias.normal_(0, 0.05)
+                L.W2.bias.normal_(0, 0.05)
+        return m.eval()
+
+    def ngcf_arrays(m):
+        # the embedding tables are re-drawn from the seed by the drop-in class (same RNG
+        # order, tests/test_models.py); their hash pins that
+        arrs = dict(emb_sha256=np.array([sha256(m.user_embedding.weight.detach().numpy()),
+                                         sha256(m.item_embedding.weight.detach().numpy())]))
+        for li, L in enumerate(m.layers):
+            arrs[f"W1_{li}"] = L.W1.weight.detach().numpy()
+            arrs[f"b1_{li}"] = L.W1.bias.detach().numpy()
+            arrs[f"W2_{li}"] = L.W2.weight.detach().numpy()
+            arrs[f"b2_{li}"] = L.W2.bias.detach().numpy()
+        return arrs
+
+    m = ngcf(311)
+    with torch.no_grad():
+        ue, ie = m(t_adj)
+    out = torch.cat([ue, ie]).numpy()
+    np.savez_compressed(OUT / "ngcf_ml1m_d64.npz", rows=rows, out_rows=out[rows], seed=311,
+                        n_users=nu, n_items=ni, **ngcf_arrays(m))
+
+    m = ngcf(312)
+    torch.manual_seed(313)
+    gsl = [GSL(64, 8, init_scale=0.01) for _ in range(3)]
+    with torch.no_grad():
+        for gs in gsl:
+            for p in gs.skew_params:
+                p.mul_(30.0)
+        x = torch.cat([m.user_embedding.weight, m.item_embedding.weight])
+        outs = [x]
+        for L, gs in zip(m.layers, gsl):
+            x = gs(L(x, t_adj))
+            outs.append(x)
+        out = torch.cat(outs, dim=1).numpy()
+    arrs = ngcf_arrays(m)
+    for li, gs in enumerate(gsl):
+        arrs[f"gs_skew_{li}"] = np.stack([p.detach().numpy() for p in gs.skew_params])
+        arrs[f"gs_perm_{li}"] = gs.perm.numpy()
+    np.savez_compressed(OUT / "ngcf_gas_ml1m_d64.npz", rows=rows, out_rows=out[rows], seed=312,
+                        n_users=nu, n_items=ni, **arrs)
+
+    torch.manual_seed(331)
+    m = OBG(nu, ni, embedding_dim=64, n_layers=3, block_size=8, residual_alpha=0.1, dropout=0.0,
+            init_scale=0.1, use_parallel_transport=True)
+    with torch.no_grad():
+        m.layer_weights.copy_(torch.tensor([0.3, -0.2, 0.5, 0.1]))
+        for L in list(m.local_transform_layers) + list(m.connection_layers):
+            for p in L.skew_params:
+                p.mul_(20.0)
+    m.eval()
+    with torch.no_grad():
+        ue, ie = m(adj_matrix=t_adj)
+        layers = m.get_layer_embeddings(adj_matrix=t_adj)
+    out = torch.cat([ue, ie]).numpy()
+    arrs = dict(emb_sha256=np.array([sha256(m.user_embedding.weight.detach().numpy()),
+                                     sha256(m.item_embedding.weight.detach().numpy())]),
+                seed=331, n_users=nu, n_items=ni,
+                layer_weights=m.layer_weights.detach().numpy(), rows=rows, out_rows=out[rows],
+                layers_rows=np.stack([x.numpy()[rows] for x in layers]))
+    for li in range(3):
+        gsl_, bcl = m.local_transform_layers[li], m.connection_layers[li]
+        arrs[f"gs_skew_{li}"] = np.stack([p.detach().numpy() for p in gsl_.skew_params])
+        arrs[f"gs_perm_{li}"] = gsl_.perm.numpy()
+        arrs[f"bc_skew_{li}"] = np.stack([p.detach().numpy() for p in bcl.skew_params])
+        arrs[f"bc_perm_{li}"] = bcl.shuffle_perm.numpy()
+    np.savez_compressed(OUT / "ob_ml1m_d64.npz", **arrs)
+    print(f"ml1m_models: N={nu + ni}, {rows.size} rows kept")
+
+
+def gat_heavy_pairs():
+    """A min-degree-1 power-law bipartite graph with rows above GAT_HEAVY_THRESHOLD (2048):
+    3 000 users x 4 000 items, Zipf(1.6) item popularity (the two most popular items reach
+    ~2 900 and ~2 600 users), one hub user with 2 500 items, every node at least one edge."""
+    rng = np.random.default_rng(91)
+    nu, ni = 3000, 4000
+    u = rng.integers(0, nu, 40000)
+    i = np.minimum(rng.zipf(1.6, 40000) - 1, ni - 1)
+    u = np.concatenate([u, np.zeros(2500, np.int64), np.arange(nu), rng.integers(0, nu, ni)])
+    i = np.concatenate([i, rng.choice(ni, 2500, replace=False), rng.integers(0, ni, nu),
+                        np.arange(ni)])
+    key = u * ni + i
+    _, first = np.unique(key, return_index=True)
+    keep = np.sort(first)
+    return u[keep], i[keep], nu, ni
+
+
+def make_gat_heavy(gb, GAT):
+    """Config 5's degree-bucketed path pinned to the reference itself: the reference's dense
+    GAT (gat.py:76-151, 258-297; [N, N] masked softmax per head, N = 7 000) K=3 d=64 with 4
+    heads on gat_heavy_pairs(), whose longest rows (2 500+ neighbours) exceed the native
+    kernel's GAT_HEAVY_THRESHOLD and run through the segment + merge kernels."""
+    import torch
+    u, i, nu, ni = gat_heavy_pairs()
+    _, _, t = ref_graph(gb, u, i, nu, ni)
+    torch.manual_seed(92)
+    m = GAT(nu, ni, embedding_dim=64, n_layers=3, n_heads=4, dropout=0.1, alpha=0.2,
+            init_scale=0.1)
+    m.eval()
+    with torch.no_grad():
+        ue, ie = m(t)
+    deg = np.bincount(np.concatenate([u, nu + i]), minlength=nu + ni)
+    arrs = dict(users=u.astype(np.int16), items=i.astype(np.int16), n_users=nu, n_items=ni,
+                seed=92, max_degree=int(deg.max()), user_out=ue.numpy(), item_out=ie.numpy())
+    for li, L in enumerate(m.layers):
+        arrs[f"W_{li}"] = np.stack([w.weight.detach().numpy() for w in L.W])
+        arrs[f"a_self_{li}"] = np.stack([a.detach().numpy()[:, 0] for a in L.a_self])
+        arrs[f"a_neigh_{li}"] = np.stack([a.detach().numpy()[:, 0] for a in L.a_neigh])
+    np.savez_compressed(OUT / "gat_heavy_d64_h4.npz", **arrs)
+    print(f"gat_heavy: N={nu + ni} nnz={2 * u.size} max degree {deg.max()}, "
+          f"{int((deg > 2048).sum())} rows > 2048")
+
+
 def make_emb_stats():
     """The over-smoothing statistics Evaluator.evaluate adds (evaluator.py:116-121 ->
     training/metrics.py:229-315) on a table with a zero row and two identical rows."""
@@ -207,7 +352,8 @@ def make_emb_stats():
 def main():
     import torch
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="", help="comma list: long_rows, edge_paths, emb_stats")
+    ap.add_argument("--only", default="", help="comma list: long_rows, edge_paths, emb_stats, "
+                                               "ml1m_models, gat_heavy")
     only = set(filter(None, ap.parse_args().only.split(",")))
     gb, LightGCN, NGCF, GAT, GSL, BCL, OBG = _import_reference()
     torch.set_num_threads(1)
@@ -220,6 +366,10 @@ def main():
             make_edge_paths(gb, OBG, EdgeSpecificBundleConnection, parallel_transport_along_edges)
         if "emb_stats" in only:
             make_emb_stats()
+        if "ml1m_models" in only:
+            make_ml1m_models(gb, NGCF, GSL, OBG)
+        if "gat_heavy" in only:
+            make_gat_heavy(gb, GAT)
         return
     meta = dict(torch=torch.__version__, numpy=np.__version__)
     import scipy
@@ -404,6 +554,8 @@ def main():
     make_long_rows(gb, LightGCN)
     make_edge_paths(gb, OBG, EdgeSpecificBundleConnection, parallel_transport_along_edges)
     make_emb_stats()
+    make_ml1m_models(gb, NGCF, GSL, OBG)
+    make_gat_heavy(gb, GAT)
 
     with open(OUT / "VERSIONS.txt", "w") as f:
         for k, v in meta.items():

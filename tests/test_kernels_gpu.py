@@ -493,6 +493,23 @@ def test_rows_gemm_matches_fp32_matmul(cuda, k, p):
     assert F.rows_gemm(x[:0], B.to(cuda)).shape == (0, p)
 
 
+def test_rows_gemm_unsupported_shapes_raise(cuda):
+    """No hidden fallback: a shape without a kernel instance, a mismatched B, a tensor on
+    another device or a misaligned view raises instead of running torch.matmul."""
+    x = torch.randn(100, 64, device=cuda)
+    with pytest.raises(NotImplementedError):
+        F.rows_gemm(x, torch.randn(64, 84, device=cuda))          # p > 80 at k = 64
+    with pytest.raises(NotImplementedError):
+        F.rows_gemm(torch.randn(100, 32, device=cuda), torch.randn(32, 8, device=cuda))
+    with pytest.raises(ValueError):
+        F.rows_gemm(x, torch.randn(128, 8, device=cuda))          # B rows != k
+    with pytest.raises(ValueError):
+        F.rows_gemm(x, torch.randn(64, 8))                        # B on the host
+    with pytest.raises(ValueError):
+        F.rows_gemm(torch.randn(100, 65, device=cuda)[:, 1:], torch.randn(64, 8, device=cuda))
+    assert not F.rows_gemm_supported(64, 84) and F.rows_gemm_supported(256, 64)
+
+
 def test_rows_gemm_fused_gat_epilogue(cuda):
     """rows_gemm's ELU + layer-mean epilogue == the same steps in torch (GAT's last layer)."""
     from src.ops._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT, EPI_NO_Y

@@ -268,3 +268,20 @@ def test_edge_specific_cpu_matches_reference():
         out = esbc.transport(x, ei, et)
     np.testing.assert_allclose(ref_path.numpy(), f["y"], rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(out.numpy(), f["y"], rtol=1e-5, atol=1e-5)
+
+
+def test_rows_gemm_guards_on_host():
+    """rows_gemm has no torch fallback: host tensors and mismatched shapes raise before any
+    native call; GAT picks the native row GEMM only for shapes it has an instance for."""
+    from src.ops import functional as F
+    from src.models.baselines.gat import GATLayer
+    with pytest.raises(ValueError):
+        F.rows_gemm(torch.randn(8, 64), torch.randn(64, 8))          # x on the host
+    with pytest.raises(ValueError):
+        F.rows_gemm(torch.randn(8, 64), torch.randn(32, 8))          # B rows != k
+    assert F.rows_gemm_supported(64, 72) and F.rows_gemm_supported(128, 64)
+    assert not F.rows_gemm_supported(64, 84) and not F.rows_gemm_supported(32, 8)
+    assert not F.rows_gemm_supported(128, 136) and not F.rows_gemm_supported(64, 6)
+    # last (head-mean) layer of a 128-wide GAT: H * in = 512 has no instance -> not shared
+    assert not GATLayer(128, 128, 4, concat_heads=False).shares_input()
+    assert GATLayer(64, 64, 4, concat_heads=False).shares_input()

@@ -101,50 +101,54 @@ def test_partition_covers_rows_and_remaps_columns(world):
 def _walk_tiled_plan(plan, n_rows, R):
     """Replay gnnrec_spmm_tiled_f32's schedule on the host: per row, the (col, val) sequence
     its accumulator receives, in kernel order; checks the plan's structural rules on the way
-    (include/gnnrec.h: chunks of two 16-slot halves, per-chunk {barriers, chain mask, panel
-    base, 0}; slot word = (col - base) << 11 | row; a row at most one run per group of 8
-    slots of a half; every slot of a chunk inside its panel)."""
+    (include/gnnrec.h, ABI 7: chunks of 8 steps x 8 slot streams, entry 8 g + t = slot t of
+    stream g; per-chunk {barriers, chain mask lo, hi, panel base}; slot word = (col - base) <<
+    11 | row; a row at most one run per group of 4 slots of a stream; every slot of a chunk
+    inside its panel)."""
     sw = plan["slot"].numpy().view(np.uint32)
     val = plan["val"].numpy()
     hdr = plan["hdr"].numpy().view(np.uint32)
     panel = plan["panel"]
     wp = plan["wave_ptr"].numpy()
     ns = plan["n_steps"].numpy()
-    W, CH, H, GR = _lib.TILED_WAVES, _lib.TILED_CHUNK, _lib.TILED_CHUNK // 2, 8
+    W, CH, NG, S, GR = (_lib.TILED_WAVES, _lib.TILED_CHUNK, _lib.TILED_GROUPS, _lib.TILED_STEPS,
+                        4)
+    assert CH == NG * S
     seq = [[] for _ in range(n_rows)]
     for b in range(plan["n_blocks"]):
-        owner = {}            # (step, row) -> (wave, half): a row lives on one stream per step
-        events = []           # (step, slot index, row, col, val)
+        owner = {}            # (step, row) -> (wave, stream): a row lives on one stream per step
+        events = []           # (step, wave, chunk, step in chunk, row, col, val)
         for w in range(W):
             cur = 0
             for c in range(wp[b * W + w], wp[b * W + w + 1]):
                 cur += int(hdr[4 * c])
-                cm = int(hdr[4 * c + 1])
-                pbase = int(hdr[4 * c + 2])
-                assert pbase % panel == 0 and hdr[4 * c + 3] == 0
-                for h in range(2):
-                    base = c * CH + h * H
-                    rows = [int(sw[base + t]) & 2047 for t in range(H)]
-                    for g0 in range(0, H, GR):
+                cm = int(hdr[4 * c + 1]) | (int(hdr[4 * c + 2]) << 32)
+                pbase = int(hdr[4 * c + 3])
+                assert pbase % panel == 0
+                for g in range(NG):
+                    base = c * CH + g * S
+                    rows = [int(sw[base + t]) & 2047 for t in range(S)]
+                    for g0 in range(0, S, GR):
                         grp = rows[g0:g0 + GR]
                         runs = [r for t, r in enumerate(grp)
                                 if r != R and (t == 0 or grp[t - 1] != r)]
                         assert len(runs) == len(set(runs)), "a row must be one run per group"
-                    for t in range(H):
+                    for t in range(S):
                         row = rows[t]
-                        chain = (cm >> (16 * h + t)) & 1
+                        chain = (cm >> (S * g + t)) & 1
                         if row == R:
                             assert val[base + t] == 0 and chain == 0
                             continue
                         assert row < R
                         assert chain == (1 if (t > 0 and rows[t - 1] == row) else 0)
-                        assert owner.setdefault((cur, row), (w, h)) == (w, h)
+                        assert owner.setdefault((cur, row), (w, g)) == (w, g)
                         rel = int(sw[base + t]) >> 11
                         assert rel < panel
-                        events.append((cur, base + t, row, pbase + rel, val[base + t]))
+                        events.append((cur, w, c, t, row, pbase + rel, val[base + t]))
             assert cur <= max(ns[b] - 1, 0)
-        events.sort(key=lambda e: (e[0], e[1]))
-        for _, _, row, col, v in events:
+        # inside a step a row is on one stream, which applies its slots in chunk / step order
+        events.sort(key=lambda e: (e[0], e[1], e[2], e[3]))
+        for _, _, _, _, row, col, v in events:
             seq[b * R + row].append((col, v))
     return seq
 
@@ -155,8 +159,8 @@ def _walk_tiled_plan(plan, n_rows, R):
 def test_tiled_plan_preserves_every_row_chain(R, panel, sub):
     """The column-ordered plan visits each row's neighbours exactly in CSR order (ascending
     columns: the fmaf order that makes the hop bit-exact), once each, one slot stream per row
-    and step, a row at most one run of slots per half-chunk (sub-panel order interleaves
-    rows), with chain bits exactly on run continuations inside a half-chunk."""
+    and step, a row at most one run of slots per 4-slot group of a stream (sub-panel order
+    interleaves rows), with chain bits exactly on run continuations inside a chunk."""
     rng = np.random.default_rng(R + panel + sub)
     u = np.concatenate([rng.integers(0, 700, 6000), np.zeros(300, np.int64)])  # a long row
     i = np.concatenate([rng.integers(0, 900, 6000), np.arange(300)])
@@ -239,3 +243,36 @@ def test_mfma_accumulators_never_partially_overlap():
                 assert not (same_file and (d0, d1) != (c0, c1) and d0 <= c1 and c0 <= d1), \
                     f"{src}: partially overlapping MFMA accumulators: {m[0]}"
     assert checked > 500
+
+
+def test_tiled_plan_build_with_offsets_past_2_31():
+    """row_ptr holds absolute int64 offsets (gnnrec.h): a row_ptr shifted by 2^31 + 4096 with
+    col / val base pointers shifted down by the same amount must give the identical plan (the
+    plan builder never truncates a nonzero offset to 32 bits)."""
+    import ctypes as C
+    rng = np.random.default_rng(5)
+    G = CsrGraph.from_interactions(rng.integers(0, 400, 8000), rng.integers(0, 600, 8000), 400, 600)
+    L = _lib.lib()
+    off = (1 << 31) + 4096
+    rp = np.ascontiguousarray(G.row_ptr.numpy())
+    col = np.ascontiguousarray(G.col.numpy())
+    val = np.ascontiguousarray(G.val.numpy())
+    plans = []
+    for shift in (0, off):
+        rps = rp + shift
+        h, nc, nb = C.c_void_p(), C.c_int64(), C.c_int64()
+        _lib.check(L.gnnrec_tiled_plan_build(rps.ctypes.data, col.ctypes.data - 4 * shift,
+                                             val.ctypes.data - 4 * shift, rp.size - 1, 37, 256,
+                                             32, 2, C.byref(h), C.byref(nc), C.byref(nb)), "build")
+        chunks = nc.value + _lib.TILED_TAIL
+        arrs = (np.empty(chunks * _lib.TILED_CHUNK, np.uint32),
+                np.empty(chunks * _lib.TILED_CHUNK, np.float32),
+                np.empty(chunks * 4, np.uint32), np.empty(nb.value * _lib.TILED_WAVES + 1, np.int64),
+                np.empty(nb.value, np.int32))
+        try:
+            _lib.check(L.gnnrec_tiled_plan_emit(h, *(a.ctypes.data for a in arrs)), "emit")
+        finally:
+            L.gnnrec_tiled_plan_free(h)
+        plans.append(arrs)
+    for a, b in zip(*plans):
+        assert np.array_equal(a.view(np.uint8), b.view(np.uint8))

@@ -82,6 +82,15 @@ def test_embedding_statistics_match_reference():
     assert "mad_sampled" not in st
     st2 = embedding_statistics(torch.from_numpy(f["emb"]), exact_limit=300)
     assert st2["mad_sampled"] == 300.0 and abs(st2["mcs"] - st["mcs"]) < 1e-12
+    # the user / item halves as two parts, statistics over small row chunks: no concatenated
+    # copy, same values (float64 sums reassociated)
+    e = torch.from_numpy(f["emb"])
+    h = e.shape[0] // 3
+    st3 = embedding_statistics((e[:h], e[h:]), chunk=128, stat_rows=37)
+    for key in ("mcs", "mad", "variance"):
+        assert abs(st3[key] - st[key]) <= 1e-9 * max(1.0, abs(st[key])), key
+    st4 = embedding_statistics((e[:h], e[h:]), exact_limit=300, stat_rows=37)
+    assert st4["mad"] == st2["mad"]
 
 
 def test_bench_cpu_baseline_leg_checks_parity():

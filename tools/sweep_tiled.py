@@ -48,7 +48,7 @@ for spec in args:
         w = plan["slot"].long() & 0xFFFFFFFF
         plan["slot"] = ((torch.remainder(w >> 11, rows) << 11) | (w & 2047)).int()
         hdr = plan["hdr"].clone().view(-1, 4)
-        hdr[:, 2] = 0
+        hdr[:, 3] = 0
         plan["hdr"] = hdr.view(-1)
     times = []
     for _ in range(12):
