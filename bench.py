@@ -102,6 +102,36 @@ class HopTimer:
         return [s.elapsed_time(e) for s, e in self.pairs]
 
 
+class ExchangeTimer:
+    """HIP events on the compute stream around each per-hop exchange (N > 1): before the
+    exchange call and after it returns (torch's RCCL work makes the current stream wait on
+    the exchange's completion), i.e. the time the hop chain is held by the exchange — the
+    whole transfer when it is not overlapped, its un-overlapped tail when chunks are."""
+
+    def __init__(self, dg):
+        self.pairs = []
+        self.active = False
+        for name in ("exchange", "finish"):
+            fn = getattr(dg, name)
+            setattr(dg, name, self._wrap(fn))
+
+    def _wrap(self, fn):
+        def timed(*a, **kw):
+            if not self.active:
+                return fn(*a, **kw)
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            s.record()
+            r = fn(*a, **kw)
+            e.record()
+            self.pairs.append((s, e))
+            return r
+        return timed
+
+    def durations_ms(self):
+        return [s.elapsed_time(e) for s, e in self.pairs]
+
+
 def hop_bytes_alg(nnz: int, rows: int, src: int, d: int) -> int:
     """SURVEY §8(d) compulsory bytes of one hop: CSR once (int64 row_ptr, int32 col, fp32 val),
     every distinct source row once, every destination row written once. G100M d=64, one
@@ -347,6 +377,7 @@ def main(argv=None) -> int:
     del full
 
     timer = HopTimer()
+    xtimer = ExchangeTimer(dg) if world > 1 else None
     chunks, reserve = 1, 0
 
     def step():
@@ -391,6 +422,8 @@ def main(argv=None) -> int:
     if world > 1:
         dist.barrier()
     timer.active = True
+    if xtimer is not None:
+        xtimer.active = True
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for _ in range(a.steps):
@@ -400,6 +433,8 @@ def main(argv=None) -> int:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     timer.active = False
+    if xtimer is not None:
+        xtimer.active = False
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -408,9 +443,10 @@ def main(argv=None) -> int:
 
     durs = timer.durations_ms()
     alg_bytes = float(hop_bytes_alg(dg.shard.nnz, dg.n_local, src, d))
-    # one device + column-ordered kernel: the deferred layer mean (lightgcn_propagate_dist)
-    per_hop = hop_bytes(dg.shard.nnz, dg.n_local, src, d, K, world,
-                        deferred=(world == 1 and tiled and K >= 2))
+    # column-ordered kernel: the deferred layer mean (lightgcn_propagate_dist), on shards too
+    # unless the flag hop would be chunked (K > 3 with overlap chunks)
+    deferred = tiled and K >= 2 and (K <= 3 or chunks == 1 or world == 1)
+    per_hop = hop_bytes(dg.shard.nnz, dg.n_local, src, d, K, world, deferred=deferred)
     launch_bytes = float(np.mean(per_hop))
     # kernel time per hop (= per launch at N=1; the sum of its chunk launches when the hop is
     # split into overlap chunks)
@@ -498,7 +534,7 @@ def main(argv=None) -> int:
                 if len(durs) == a.steps * K else None,
                 "bytes_per_launch_with_fused_epilogue": launch_bytes,
                 "layer_mean_schedule": "deferred (hop K forms the mean)"
-                if (world == 1 and tiled and K >= 2) else "eager (every hop's epilogue)",
+                if deferred else "eager (every hop's epilogue)",
                 # the same launch priced by its MEASURED memory-side traffic (PMC FETCH_SIZE x 2
                 # + WRITE_SIZE). FETCH_SIZE counts the L2's requests to the fabric, Infinity-Cache
                 # hits included (MI355X_MICROARCH.md § HBM), so this is L2->fabric traffic, an
@@ -514,7 +550,11 @@ def main(argv=None) -> int:
             "edges_per_s_per_interaction": value / 2.0,
             "hbm_gbps_algorithmic_step": K * launch_bytes * world / (ms_per_step * 1e-3) / 1e9,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
-            "exchange": dict(exchange_info, recv_bytes_per_hop_per_rank=dg.recv_rows() * d * 4)
+            "exchange": dict(exchange_info, recv_bytes_per_hop_per_rank=dg.recv_rows() * d * 4,
+                             # rank 0's compute-stream view per exchanged hop (K - 1 per step)
+                             exchange_ms_per_hop=(float(np.sum(xtimer.durations_ms()))
+                                                  / (a.steps * max(1, K - 1))) if xtimer else None,
+                             compute_ms_per_hop=launch_ms)
             if world > 1 else None,
         }
         if check:

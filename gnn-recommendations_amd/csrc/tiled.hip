@@ -50,18 +50,28 @@ constexpr int kGroups = GNNREC_TILED_GROUPS;      // slot streams per wave (8 la
 constexpr int kSteps = GNNREC_TILED_STEPS;        // steps per chunk
 constexpr int kTiledChunk = GNNREC_TILED_CHUNK;   // slots per chunk (one per lane)
 constexpr int kTiledTail = GNNREC_TILED_TAIL;
+constexpr int kChunkWords = 2 * GNNREC_TILED_CHUNK + GNNREC_TILED_HDR_WORDS;   // 132
 constexpr int kSlice = 32;                        // features per pass
 constexpr int kRowBytes = kSlice * 4;             // one LDS accumulator row, one gathered line
 constexpr int kRowBits = 11;
 constexpr int kRowMask = (1 << kRowBits) - 1;
 constexpr int kMaxPanel = 1 << 20;                // columns per panel (slot word: 21 bits)
 constexpr int kMaxRowBytes = GNNREC_TILED_MAX_LDX * 4;   // keeps the lane offset 32-bit
-constexpr int kApply = 4;                         // steps whose reads precede their writes
+#ifndef GNNREC_TILED_NOCHAIN
+#define GNNREC_TILED_NOCHAIN 0
+#endif
+// NOCHAIN: a row appears at most once per chunk of a stream, so all 8 reads of a chunk precede
+// its writes and no slot chains on a register value
+constexpr bool kNoChain = GNNREC_TILED_NOCHAIN != 0;
+#ifndef GNNREC_TILED_APPLY
+#define GNNREC_TILED_APPLY 4
+#endif
+constexpr int kApply = GNNREC_TILED_APPLY;        // steps whose reads precede their writes
 #ifndef GNNREC_TILED_PLAN_AHEAD
-#define GNNREC_TILED_PLAN_AHEAD 3
+#define GNNREC_TILED_PLAN_AHEAD 5
 #endif
 #ifndef GNNREC_TILED_GATHER_AHEAD
-#define GNNREC_TILED_GATHER_AHEAD 1
+#define GNNREC_TILED_GATHER_AHEAD 2
 #endif
 constexpr int kPlanAhead = GNNREC_TILED_PLAN_AHEAD;       // slot loads, chunks ahead of the apply
 constexpr int kGatherAhead = GNNREC_TILED_GATHER_AHEAD;   // gathers, chunks ahead of the apply
@@ -87,7 +97,7 @@ constexpr int kEpiBatch3 = GNNREC_TILED_EPI_BATCH3;   // the same with 2-3 base 
 constexpr int kEpiStoreAux = 2;
 static_assert(kTiledChunk == kGroups * kSteps && kTiledChunk == 64, "one slot per lane");
 static_assert(kGroups == 8 && kSteps == 8, "a stream is 8 lanes: half a 16-lane DPP row");
-static_assert(kSteps == 2 * kApply, "a chunk is applied as two groups");
+static_assert(kSteps == 2 * kApply || kSteps == kApply, "a chunk is one or two apply groups");
 static_assert(GNNREC_TILED_MAX_ROWS < kRowMask, "row field is 11 bits (row R = scratch)");
 static_assert((GNNREC_TILED_MAX_ROWS + 1) * kRowBytes <= 160 * 1024, "LDS");
 static_assert((int64_t)kMaxPanel * kMaxRowBytes <= ((int64_t)1 << 32), "32-bit lane offsets");
@@ -98,7 +108,7 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 // accumulator reads and writes (registers instead), bit 1 replaces the gathers by a constant,
 // bit 2 skips the step barriers, bit 3 reads every chunk's slot words and values from the
 // plan's first 64 chunks (cache-resident plan stream; headers unchanged), bit 4 replaces the
-// DPP broadcasts by the lane's own value.
+// DPP broadcasts by the lane's own value, bit 5 skips the main loop (passes and epilogues).
 #ifndef GNNREC_TILED_EXP
 #define GNNREC_TILED_EXP 0
 #endif
@@ -141,15 +151,34 @@ __device__ __forceinline__ float gbcastf(float v) {
 
 // The chunk header {step barriers before the chunk, chain mask lo, chain mask hi, panel base
 // column} is loaded with the slots as a vector load (lane l: word l % 4) and read back with
-// v_readlane: a scalar load would share lgkmcnt with the LDS chain and stall it.
-__device__ __forceinline__ void tiled_slots(const uint32_t* __restrict__ ss,
-                                            const float* __restrict__ sv,
-                                            const uint32_t* __restrict__ hdr, int64_t c, int lane,
-                                            TiledSlots& m) {
-  const int64_t i = ((GNNREC_TILED_EXP & 8) ? (c & 63) : c) * kTiledChunk + lane;
-  m.w = ss[i];
-  m.v = sv[i];
-  m.h = hdr[4 * c + (lane & 3)];
+// v_readlane: a scalar load would share lgkmcnt with the LDS chain and stall it. The plan is
+// ONE stream of chunks {64 x (slot word, value), 4 header words} read through a buffer
+// resource based at the wave's first chunk: the lane part of the offset is a constant VGPR
+// and the chunk part an SGPR (no per-load address math), one rsrc (SGPR pressure).
+struct PlanStream {
+  __amdgpu_buffer_rsrc_t r;   // the wave's chunks: kChunkWords words each
+  uint32_t lane_off;          // lane * 8: this lane's {word, value}
+  uint32_t hdr_off;           // the header word lane % 4
+};
+
+__device__ __forceinline__ PlanStream plan_stream(const uint32_t* plan, int64_t b, int lane) {
+  PlanStream p;
+  p.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(plan + b * kChunkWords), 0,
+                                          0x7FFFFFFF, 0x00020000);
+  p.lane_off = (uint32_t)lane * 8;
+  p.hdr_off = (uint32_t)(2 * kTiledChunk + (lane & 3)) * 4;
+  return p;
+}
+
+// chunk b + i of the wave (i < 2^21: a wave's chunks of one pass)
+__device__ __forceinline__ void tiled_slots(const PlanStream& p, int i, TiledSlots& m) {
+  if (GNNREC_TILED_EXP & 8) i &= 63;
+  const int so = i * (kChunkWords * 4);
+  // two adjacent dwords, merged into one buffer_load_dwordx2 by the compiler (the _b64
+  // builtin of this toolchain returned only the low dword)
+  m.w = __builtin_amdgcn_raw_buffer_load_b32(p.r, p.lane_off, so, 0);
+  m.v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(p.r, p.lane_off + 4, so, 0));
+  m.h = __builtin_amdgcn_raw_buffer_load_b32(p.r, p.hdr_off, so, 0);
 }
 
 template <int W>
@@ -158,13 +187,15 @@ __device__ __forceinline__ uint32_t hdr_word(const TiledSlots& m) {
 }
 
 // The gathers of a chunk read through a buffer whose base is its panel's first source row, so
-// lane offsets stay 32-bit for any table size.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const char* xs, uint64_t xs_bytes,
-                                                             uint32_t base, uint32_t row_bytes) {
-  const uint64_t off = (uint64_t)base * row_bytes;
-  const uint64_t left = off < xs_bytes ? xs_bytes - off : 0;
-  const uint32_t n = left > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)left;
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(xs) + off, 0, (int)n, 0x00020000);
+// lane offsets stay 32-bit for any table size; its range ends at the table's last row (in
+// 32-bit row units: all scalar arithmetic, no 64-bit compares).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const char* xs, uint32_t x_rows,
+                                                             uint32_t base, uint32_t row_bytes,
+                                                             uint32_t lim_rows) {
+  const uint32_t left = base < x_rows ? x_rows - base : 0u;
+  const uint32_t n = left >= lim_rows ? 0xFFFFFFFFu : left * row_bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(xs) + (uint64_t)base * row_bytes, 0,
+                                           (int)n, 0x00020000);
 }
 
 // Rows [r0, r0 + rows) of a row-major fp32 table (row stride ld), from column slice * 32: the
@@ -272,7 +303,7 @@ __device__ __forceinline__ void tiled_apply(float* acc, uint32_t q16, const Tile
   f4 prev = (GNNREC_TILED_EXP & 1) ? sink : f4{0.f, 0.f, 0.f, 0.f};
   const uint32_t r = (m.w & kRowMask) * kRowBytes;   // this lane's slot's accumulator row
   tiled_apply4<CHAIN, 0>(k4, base, q16, r, m, x, cm, prev);
-  tiled_apply4<CHAIN, kApply>(k4, base, q16, r, m, x, cm, prev);
+  if constexpr (kApply < kSteps) tiled_apply4<CHAIN, kApply>(k4, base, q16, r, m, x, cm, prev);
   if (GNNREC_TILED_EXP & 1) sink = prev;
 }
 
@@ -363,13 +394,13 @@ __device__ __forceinline__ void run_ring(std::integer_sequence<int, I...>, F&& s
 }
 
 __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
-    const uint32_t* __restrict__ ss, const float* __restrict__ sv,
-    const uint32_t* __restrict__ hdr, const int64_t* __restrict__ wptr,
+    const uint32_t* __restrict__ plan, const int64_t* __restrict__ wptr,
     const int32_t* __restrict__ nsteps, int n_blocks, int nb_pad, int n_items, int R,
-    const float* __restrict__ x, uint64_t x_bytes, uint32_t row_bytes,
-    float* __restrict__ y, int64_t ldy, int64_t n_rows, int epi, const float* __restrict__ self,
-    int64_t ld_self, float* __restrict__ accg, int64_t ld_acc, float acc_div,
-    unsigned* __restrict__ sync, unsigned meet_ticks) {
+    const float* __restrict__ x, uint32_t x_rows32, uint32_t row_bytes,
+    float* __restrict__ y, uint32_t ldy4, int n_rows, int epi, const float* __restrict__ self,
+    uint32_t ls4, float* __restrict__ accg, uint32_t la4, float acc_div,
+    const float* __restrict__ prev, uint32_t lp4, unsigned* __restrict__ sync,
+    unsigned meet_ticks) {
   extern __shared__ f4 acc4[];   // [(R+1)][32] floats: row R is the padding slots' scratch row
   float* acc = reinterpret_cast<float*>(acc4);
   constexpr auto kSeq = std::make_integer_sequence<int, kSteps>{};
@@ -377,8 +408,8 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
   const uint32_t q16 = (uint32_t)(lane & 7) * 16;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   unsigned* ctr = sync + (blockIdx.x % 8) * 32;   // the group's counter, own 128-B line
-  const long long G = gridDim.x / 8 + ((blockIdx.x % 8) < (gridDim.x % 8) ? 1 : 0);
-  long long pass = 0;
+  const int G = gridDim.x / 8 + ((blockIdx.x % 8) < (gridDim.x % 8) ? 1 : 0);
+  int pass = 0;
 #ifdef GNNREC_TILED_TRACE
   int ev = 0;
 #endif
@@ -387,8 +418,8 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
       // pass start: report the finished pass, wait (bounded) for the group's others
       __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const unsigned long long t0 = wall_clock64();
-      while ((long long)__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                 G * pass &&
+      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                 (unsigned)(G * pass) &&
              wall_clock64() - t0 < meet_ticks)
         __builtin_amdgcn_s_sleep(2);
     }
@@ -402,9 +433,9 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     GNNREC_TILED_STAMP(ev);
     const uint32_t soff = (uint32_t)slice * kRowBytes;
     const char* xs = reinterpret_cast<const char*>(x) + soff;
-    const uint64_t xs_bytes = x_bytes - soff;
+    const uint32_t lim_rows = 0xFFFFFFFFu / row_bytes;   // rows whose bytes exceed 32 bits
     const int64_t s = (int64_t)blk * kTiledWaves + w;
-    const int64_t b = wptr[s], e = wptr[s + 1];
+    const int64_t b = wptr[s], e = (GNNREC_TILED_EXP & 32) ? b : wptr[s + 1];
     int cur = 0;
     f4 sink = {0.f, 0.f, 0.f, 0.f};   // diagnostic builds only (GNNREC_TILED_EXP & 1)
     if (b < e) {
@@ -412,19 +443,21 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
       // chunk c + kPlanAhead's slots, gathers chunk c + kGatherAhead and applies chunk c
       TiledSlots M[kMRing];
       f4 X[kXRing][kSteps];
-      int64_t c = b;
+      const PlanStream ps = plan_stream(plan, b, lane);
+      const int nc = (int)(e - b);   // this wave's chunks of the pass
+      int c = 0;
 #pragma unroll
-      for (int j = 0; j < kPlanAhead; ++j) tiled_slots(ss, sv, hdr, c + j, lane, M[j]);
+      for (int j = 0; j < kPlanAhead; ++j) tiled_slots(ps, c + j, M[j]);
 #pragma unroll
       for (int j = 0; j < kGatherAhead; ++j)
-        tiled_gather(kSeq, chunk_rsrc(xs, xs_bytes, hdr_word<3>(M[j]), row_bytes), q16,
+        tiled_gather(kSeq, chunk_rsrc(xs, x_rows32, hdr_word<3>(M[j]), row_bytes, lim_rows), q16,
                      row_bytes, M[j], X[j]);
       auto stage = [&](auto ic) -> bool {
         constexpr int I = decltype(ic)::value;
-        tiled_slots(ss, sv, hdr, c + kPlanAhead, lane, M[(I + kPlanAhead) % kMRing]);
+        tiled_slots(ps, c + kPlanAhead, M[(I + kPlanAhead) % kMRing]);
         {
           const TiledSlots& mg = M[(I + kGatherAhead) % kMRing];
-          tiled_gather(kSeq, chunk_rsrc(xs, xs_bytes, hdr_word<3>(mg), row_bytes), q16,
+          tiled_gather(kSeq, chunk_rsrc(xs, x_rows32, hdr_word<3>(mg), row_bytes, lim_rows), q16,
                        row_bytes, mg, X[(I + kGatherAhead) % kXRing]);
         }
         const TiledSlots& ma = M[I % kMRing];
@@ -434,12 +467,13 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
           GNNREC_TILED_STAMP(ev);
         }
         cur += bar;
-        const uint64_t cm = (uint64_t)hdr_word<1>(ma) | ((uint64_t)hdr_word<2>(ma) << 32);
-        if (cm)
+        const uint64_t cm =
+            kNoChain ? 0 : (uint64_t)hdr_word<1>(ma) | ((uint64_t)hdr_word<2>(ma) << 32);
+        if (!kNoChain && cm)
           tiled_apply<true>(acc, q16, ma, X[I % kXRing], cm, sink);
         else
           tiled_apply<false>(acc, q16, ma, X[I % kXRing], 0, sink);
-        return ++c >= e;
+        return ++c >= nc;
       };
       run_ring(std::make_integer_sequence<int, kRingUnroll>{}, stage);
     }
@@ -452,24 +486,25 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
       }
     };
     // epilogue: group g of wave w owns rows i = 8w + g + 128j (see tiled_epilogue)
-    const int64_t r0 = (int64_t)blk * R;
-    const int nv = (int)min((int64_t)R, n_rows - r0);
+    const int r0 = blk * R;
+    const int nv = min(R, n_rows - r0);
     const int rl = kGroups * w + (lane >> 3);
-    const __amdgpu_buffer_rsrc_t ry = rows_rsrc((epi & GNNREC_EPI_NO_Y) ? nullptr : y, r0, ldy,
-                                                slice, nv);
-    // base inputs in layer order: x0 (INIT), the acc rows (ADD), the input rows (ACC_X)
+    const __amdgpu_buffer_rsrc_t ry = rows_rsrc((epi & GNNREC_EPI_NO_Y) ? nullptr : y, r0,
+                                                ldy4 / 4, slice, nv);
+    // base inputs in layer order: x0 (INIT), the acc rows (ADD), the previous layer (ACC_X:
+    // `prev`, by default the hop's own input rows)
     const bool init = (epi & GNNREC_EPI_ACC_INIT) != 0, add = (epi & GNNREC_EPI_ACC_ADD) != 0,
                xin = (epi & GNNREC_EPI_ACC_X) != 0;
     const int nb = (int)init + (int)add + (int)xin;
-    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(init ? self : nullptr, r0, ld_self, slice, nv);
-    const __amdgpu_buffer_rsrc_t racc = rows_rsrc(nb ? accg : nullptr, r0, ld_acc, slice, nv);
-    const __amdgpu_buffer_rsrc_t rx = rows_rsrc(xin ? x : nullptr, r0, row_bytes / 4, slice, nv);
-    const uint32_t ls = (uint32_t)ld_self * 4, la = (uint32_t)ld_acc * 4, ly = (uint32_t)ldy * 4;
+    const __amdgpu_buffer_rsrc_t rs = rows_rsrc(init ? self : nullptr, r0, ls4 / 4, slice, nv);
+    const __amdgpu_buffer_rsrc_t racc = rows_rsrc(nb ? accg : nullptr, r0, la4 / 4, slice, nv);
+    const __amdgpu_buffer_rsrc_t rx = rows_rsrc(xin ? prev : nullptr, r0, lp4 / 4, slice, nv);
+    const uint32_t ls = ls4, la = la4, ly = ldy4;
     const __amdgpu_buffer_rsrc_t rb0 = init ? rs : racc, rb1 = (init && add) ? racc : rx;
-    const uint32_t lb0 = init ? ls : la, lb1 = (init && add) ? la : row_bytes;
+    const uint32_t lb0 = init ? ls : la, lb1 = (init && add) ? la : lp4;
     const bool div = (epi & GNNREC_EPI_ACC_DIV) != 0;
 #define GNNREC_TILED_EPI(NB, B, DIV) \
-  tiled_epilogue<NB, B>(acc, R, rl, q16, ry, ly, rb0, lb0, rb1, lb1, rx, row_bytes, racc, la, DIV, \
+  tiled_epilogue<NB, B>(acc, R, rl, q16, ry, ly, rb0, lb0, rb1, lb1, rx, lp4, racc, la, DIV, \
                         acc_div, wait)
     if (nb == 0)
       GNNREC_TILED_EPI(0, kEpiBatch, false);
@@ -505,9 +540,7 @@ struct Run {
 };
 
 struct BlockPlan {
-  std::vector<uint32_t> slot[kTiledWaves];
-  std::vector<float> val[kTiledWaves];
-  std::vector<uint32_t> hdr[kTiledWaves];   // 4 words per chunk
+  std::vector<uint32_t> stream[kTiledWaves];   // kChunkWords per chunk
   int32_t nsteps = 0;
 };
 
@@ -553,8 +586,11 @@ void stream_slots(const std::vector<const Run*>& runs, const int32_t* col, int s
       const int r = sl.run->row;
       const bool is_blocked = std::find(blocked.begin(), blocked.end(), r) != blocked.end();
       const bool seen = std::find(in_group.begin(), in_group.end(), r) != in_group.end();
-      if (is_blocked || (seen && r != last)) {
-        if (seen && r != last && !is_blocked) blocked.push_back(r);
+      // a repeat of the group's row: deferred unless it continues the run (chain), and
+      // always without chains
+      const bool repeat = seen && (kNoChain || r != last);
+      if (is_blocked || repeat) {
+        if (repeat && !is_blocked) blocked.push_back(r);
         deferred.push_back(sl);
         continue;
       }
@@ -634,21 +670,20 @@ void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_
           }
         }
         uint64_t cmask = 0;
+        std::vector<uint32_t>& o = out.stream[w];
         for (int q = 0; q < kGroups; ++q)       // lane 8 q + t: slot t of stream q
           for (int t = 0; t < kSteps; ++t) {
             const Slot& sl = hs[q][c + t];
             if (!sl.run) {
-              out.slot[w].push_back(x0 << kRowBits | (uint32_t)R);
-              out.val[w].push_back(0.f);
+              o.insert(o.end(), {x0 << kRowBits | (uint32_t)R, 0u});
               continue;
             }
             const int64_t k = sl.run->k + sl.t;
             if (t > 0 && hs[q][c + t - 1].run == sl.run) cmask |= 1ull << (kSteps * q + t);
-            out.slot[w].push_back(((uint32_t)col[k] - base) << kRowBits | (uint32_t)sl.run->row);
-            out.val[w].push_back(val[k]);
+            o.insert(o.end(), {((uint32_t)col[k] - base) << kRowBits | (uint32_t)sl.run->row,
+                               __builtin_bit_cast(uint32_t, val[k])});
           }
-        out.hdr[w].insert(out.hdr[w].end(),
-                          {bar, (uint32_t)cmask, (uint32_t)(cmask >> 32), base});
+        o.insert(o.end(), {bar, (uint32_t)cmask, (uint32_t)(cmask >> 32), base});
         bar = 0;
       }
       cur[w] = step;
@@ -703,40 +738,40 @@ extern "C" int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* co
   }
   int64_t tot = 0;
   for (const auto& bp : pl->blocks)
-    for (int w = 0; w < kTiledWaves; ++w) tot += (int64_t)bp.hdr[w].size() / 4;
+    for (int w = 0; w < kTiledWaves; ++w) tot += (int64_t)bp.stream[w].size() / kChunkWords;
   *n_chunks = tot;
   *n_blocks = pl->n_blocks;
   *plan = pl;
   return GNNREC_OK;
 }
 
-extern "C" int gnnrec_tiled_plan_emit(void* plan, uint32_t* slot, float* val, uint32_t* hdr,
-                                      int64_t* wave_ptr, int32_t* n_steps) {
-  GNNREC_REQUIRE(plan && slot && val && hdr && wave_ptr && n_steps, "tiled_emit: null pointer");
+extern "C" int gnnrec_tiled_plan_emit(void* plan, uint32_t* stream, int64_t* wave_ptr,
+                                      int32_t* n_steps) {
+  GNNREC_REQUIRE(plan && stream && wave_ptr && n_steps, "tiled_emit: null pointer");
   auto* pl = static_cast<TiledPlan*>(plan);
   const int64_t nb = pl->n_blocks;
   wave_ptr[0] = 0;
   for (int64_t b = 0; b < nb; ++b)
     for (int w = 0; w < kTiledWaves; ++w)
       wave_ptr[b * kTiledWaves + w + 1] =
-          wave_ptr[b * kTiledWaves + w] + (int64_t)pl->blocks[b].hdr[w].size() / 4;
+          wave_ptr[b * kTiledWaves + w] + (int64_t)pl->blocks[b].stream[w].size() / kChunkWords;
   for (int64_t b = 0; b < nb; ++b) {
     const BlockPlan& bp = pl->blocks[b];
     n_steps[b] = bp.nsteps;
-    for (int w = 0; w < kTiledWaves; ++w) {
-      const int64_t c = wave_ptr[b * kTiledWaves + w];
-      std::copy(bp.slot[w].begin(), bp.slot[w].end(), slot + c * kTiledChunk);
-      std::copy(bp.val[w].begin(), bp.val[w].end(), val + c * kTiledChunk);
-      std::copy(bp.hdr[w].begin(), bp.hdr[w].end(), hdr + 4 * c);
-    }
+    for (int w = 0; w < kTiledWaves; ++w)
+      std::copy(bp.stream[w].begin(), bp.stream[w].end(),
+                stream + wave_ptr[b * kTiledWaves + w] * kChunkWords);
   }
   // tail chunks for the last prefetches: harmless slots (row 0 of x, the scratch-row field)
   const int64_t end = wave_ptr[nb * kTiledWaves];
-  for (int64_t s = end * kTiledChunk; s < (end + kTiledTail) * kTiledChunk; ++s) {
-    slot[s] = (uint32_t)kRowMask;
-    val[s] = 0.f;
+  for (int64_t c = end; c < end + kTiledTail; ++c) {
+    uint32_t* o = stream + c * kChunkWords;
+    for (int l = 0; l < kTiledChunk; ++l) {
+      o[2 * l] = (uint32_t)kRowMask;
+      o[2 * l + 1] = 0u;
+    }
+    for (int q = 0; q < GNNREC_TILED_HDR_WORDS; ++q) o[2 * kTiledChunk + q] = 0u;
   }
-  for (int64_t s = 4 * end; s < 4 * (end + kTiledTail); ++s) hdr[s] = 0;
   return GNNREC_OK;
 }
 
@@ -764,14 +799,25 @@ int tiled_lds_attribute(int dev) {
 }
 }  // namespace
 
-extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
-                                     const uint32_t* hdr, const int64_t* wave_ptr,
+extern "C" int gnnrec_spmm_tiled_supported(int32_t device, int32_t rows_per_block) {
+  if (rows_per_block < 1 || rows_per_block > GNNREC_TILED_MAX_ROWS) return 0;
+  int cur = 0;
+  if (hipGetDevice(&cur) != hipSuccess) return 0;
+  if (device != cur && hipSetDevice(device) != hipSuccess) return 0;
+  const size_t lds = (size_t)(rows_per_block + 1) * kRowBytes;
+  const int ok = lds <= 64 * 1024 || tiled_lds_attribute(device) > 0;
+  if (device != cur) (void)hipSetDevice(cur);
+  return ok;
+}
+
+extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* plan, const int64_t* wave_ptr,
                                      const int32_t* n_steps, int64_t n_blocks,
                                      int32_t rows_per_block, const float* x, int64_t x_rows,
                                      int64_t ldx, float* y, int64_t ldy, int64_t n_rows, int32_t d,
                                      int32_t epi, const float* self, int64_t ld_self, float* acc,
-                                     int64_t ld_acc, float acc_div, uint32_t* sync,
-                                     int32_t meet_us, gnnrec_stream_t stream) {
+                                     int64_t ld_acc, float acc_div, const float* prev,
+                                     int64_t ld_prev, uint32_t* sync, int32_t meet_us,
+                                     gnnrec_stream_t stream) {
   GNNREC_REQUIRE(d > 0 && d % kSlice == 0, "spmm_tiled: d must be a multiple of 32 (got %d)",
                  (int)d);
   GNNREC_REQUIRE(rows_per_block >= 1 && rows_per_block <= GNNREC_TILED_MAX_ROWS,
@@ -787,19 +833,26 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
   GNNREC_REQUIRE(!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) ||
                      (acc && ld_acc >= d && ld_acc % 4 == 0),
                  "spmm_tiled: ACC needs acc (ld %% 4 == 0)");
-  GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_X) ||
-                     ((epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) && x_rows >= n_rows),
-                 "spmm_tiled: ACC_X needs ACC_INIT or ACC_ADD and a square operand");
+  if (prev == nullptr) {   // ACC_X default: the hop's own input rows
+    prev = x;
+    ld_prev = ldx;
+    GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_X) || x_rows >= n_rows,
+                   "spmm_tiled: ACC_X without prev needs a square operand");
+  }
+  GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_X) || (epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)),
+                 "spmm_tiled: ACC_X needs ACC_INIT or ACC_ADD");
+  GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_X) || (ld_prev >= d && ld_prev % 4 == 0 &&
+                                               aligned16(prev)),
+                 "spmm_tiled: ACC_X rows must be 16-B aligned with ld %% 4 == 0, ld >= d");
   GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_DIV) || (epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)),
                  "spmm_tiled: ACC_DIV needs ACC_INIT or ACC_ADD");
   GNNREC_REQUIRE(meet_us >= 0 && meet_us <= 100000, "spmm_tiled: meet_us must be in [0, 1e5]");
   constexpr int64_t kMaxLd = ((int64_t)1 << 32) / (4 * 4096);   // epilogue row offsets: 32-bit
-  GNNREC_REQUIRE(ldy <= kMaxLd && ld_self <= kMaxLd && ld_acc <= kMaxLd,
+  GNNREC_REQUIRE(ldy <= kMaxLd && ld_self <= kMaxLd && ld_acc <= kMaxLd && ld_prev <= kMaxLd,
                  "spmm_tiled: output / self / acc row strides must be <= %lld",
                  (long long)kMaxLd);
   if (n_rows == 0) return GNNREC_OK;
-  GNNREC_REQUIRE(slot && val && hdr && wave_ptr && n_steps && x && sync,
-                 "spmm_tiled: null pointer");
+  GNNREC_REQUIRE(plan && wave_ptr && n_steps && x && sync, "spmm_tiled: null pointer");
   GNNREC_REQUIRE(aligned16(x) && ((epi & GNNREC_EPI_NO_Y) || aligned16(y)) &&
                      (!(epi & GNNREC_EPI_ACC_INIT) || aligned16(self)) &&
                      (!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) || aligned16(acc)),
@@ -817,14 +870,16 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
   const int64_t grid = std::min<int64_t>(cus, n_blocks);
   const int64_t nb_pad = ceil_div(n_blocks, grid) * grid;   // every slice starts a pass
   const int64_t n_items = (int64_t)(d / kSlice) * nb_pad;
-  GNNREC_REQUIRE(n_items < INT32_MAX, "spmm_tiled: too many blocks");
+  GNNREC_REQUIRE(n_items < INT32_MAX && n_rows < INT32_MAX && x_rows < INT32_MAX,
+                 "spmm_tiled: too many blocks / rows");
   if (hipMemsetAsync(sync, 0, GNNREC_TILED_SYNC_WORDS * sizeof(uint32_t), s) != hipSuccess)
     return check_launch("spmm_tiled (sync reset)");
   hipLaunchKernelGGL(tiled_hop_kernel, dim3((unsigned)grid), dim3(kTiledWaves * 64), lds, s,
-                     slot, val, hdr, wave_ptr, n_steps,
+                     plan, wave_ptr, n_steps,
                      (int)n_blocks, (int)nb_pad, (int)n_items, (int)rows_per_block, x,
-                     (uint64_t)(x_rows * ldx * 4), (uint32_t)(ldx * 4), y, ldy,
-                     n_rows, epi, self, ld_self, acc, ld_acc, acc_div, sync,
+                     (uint32_t)x_rows, (uint32_t)(ldx * 4), y, (uint32_t)(ldy * 4),
+                     (int)n_rows, epi, self, (uint32_t)(ld_self * 4), acc, (uint32_t)(ld_acc * 4),
+                     acc_div, prev, (uint32_t)(ld_prev * 4), sync,
                      (unsigned)meet_us * 100u /* wall_clock64 runs at 100 MHz */);
   return check_launch("spmm_tiled");
 }

@@ -38,10 +38,11 @@ HopFn = Callable[..., None]
 
 
 def _native_hop(adj, x, y, *, epi, self_rows, acc, acc_div, x_mask=None, y_active=None,
-                meet_us=None, reserve_cus=0):
+                meet_us=None, reserve_cus=0, prev=None):
     from .functional import spmm_into
     spmm_into(adj, x, y, epi=epi, self_rows=self_rows, acc=acc, acc_div=acc_div,
-              x_mask=x_mask, y_active=y_active, meet_us=meet_us, reserve_cus=reserve_cus)
+              x_mask=x_mask, y_active=y_active, meet_us=meet_us, reserve_cus=reserve_cus,
+              prev=prev)
 
 
 class DistributedGraph:
@@ -190,7 +191,8 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
                             gather_output: bool = False, hop_fn: Optional[HopFn] = None,
                             work: Optional[tuple] = None, overlap_chunks: int = 1,
                             masks: Optional[Callable] = None,
-                            reserve_cus: int = 0) -> torch.Tensor:
+                            reserve_cus: int = 0,
+                            deferred: Optional[bool] = None) -> torch.Tensor:
     """LightGCN propagation over a row-sharded operand.
 
     x0_pad: [world*rows_pad, d] padded initial table (identical on every rank).
@@ -208,6 +210,9 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
     reserve_cus (overlapped chunks): a chunk's column-ordered kernel is sized for that many
     fewer CUs than the device has (one pass of cus - reserve_cus workgroups), so the
     exchange's RCCL kernels find free CUs while it runs (the kernel takes a CU's whole LDS).
+    deferred: the deferred layer mean (_propagate_deferred); None = whenever the native hop
+    runs the shard on the column-ordered kernel (the only one with its epilogue); True forces
+    it for an injected hop_fn that implements that epilogue (CPU tests).
     """
     hop = hop_fn or _native_hop
     # the native hop's pass-start meeting must not wait on workgroups that share the device
@@ -225,34 +230,19 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
         work = make_work(dg, d, x0_pad.device)
     Y, Xa, Xb = work
     self_rows = dg.local_slice(x0_pad)
-    from .functional import lightgcn_hop_schedule, tiled_plan_for
-    # the hop carrying the deferred mean's tiled-only epilogue must be a dense hop
-    flag_hop = 2 if n_layers == 2 else 3
-    if (dg.world == 1 and native and n_layers >= 2
-            and tiled_plan_for(dg.shard, x0_pad) is not None
-            and (masks is None or masks(flag_hop, x0_pad) is None)):
-        # one device, column-ordered kernel: the layer mean formed on the last hop from the
-        # parked layers (lightgcn_hop_schedule, deferred) — 6 instead of 8 epilogue row
-        # transfers at K = 3, same bits (a masked hop before it stores its y as the eager one
-        # does: +0 on skipped rows). acc is padded to the gather table's rows, since hop 2
-        # gathers from it (y1 is parked there).
-        acc_full = torch.empty((Xa.shape[0], d), dtype=torch.float32, device=x0_pad.device)
-        acc_full[dg.n_local:].zero_()
-        acc = acc_full[:dg.n_local]
-        bufs = {"x0": x0_pad, "acc": acc_full, "a": Xa, "b": Xb, None: None}
-        for k, (xn, yn, epi) in enumerate(lightgcn_hop_schedule(n_layers, deferred=True),
-                                          start=1):
-            kw = mkw(k, bufs[xn])
-            if kw and (epi & EPI_ACC_X or (epi & EPI_ACC_INIT and epi & EPI_ACC_ADD)):
-                raise RuntimeError(f"deferred layer mean: hop {k} must not be masked")
-            hop(dg.shard, bufs[xn], None if yn is None else bufs[yn][:dg.n_local], epi=epi,
-                self_rows=self_rows, acc=acc, acc_div=float(n_layers + 1), **kw)
-        return acc
+    from .functional import tiled_plan_for
+    chunked = overlap_chunks > 1 and dg.world > 1 and dg.exchange_mode == "p2p"
+    # the deferred layer mean (functional.lightgcn_hop_schedule): its flag hop (the last at
+    # K <= 3) runs on the column-ordered kernel over the whole shard, never in chunks
+    if deferred is None:
+        deferred = native and tiled_plan_for(dg.shard, x0_pad) is not None
+    if deferred and n_layers >= 2 and (n_layers <= 3 or not chunked):
+        return _propagate_deferred(dg, x0_pad, n_layers, hop, mkw, work, self_rows, chunked,
+                                   overlap_chunks, chunk_kw, masks, gather_output)
     acc = torch.empty((dg.n_local, d), dtype=torch.float32, device=x0_pad.device)
     if n_layers == 0:
         acc.copy_(self_rows)
     x_in = x0_pad
-    chunked = overlap_chunks > 1 and dg.world > 1 and dg.exchange_mode == "p2p"
     for k in range(1, n_layers + 1):
         last = k == n_layers
         epi = EPI_ACC_INIT if k == 1 else EPI_ACC_ADD
@@ -291,6 +281,74 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
     if dg.world == 1:
         return acc
     Y[:dg.n_local].copy_(acc)
+    full = torch.empty_like(x0_pad)
+    dg.all_gather(full, Y)
+    return dg.unpad_table(full)
+
+
+def _propagate_deferred(dg, x0_pad, K, hop, mkw, work, self_rows, chunked, overlap_chunks,
+                        chunk_kw, masks, gather_output):
+    """lightgcn_propagate_dist with the deferred layer mean (functional.lightgcn_hop_schedule,
+    deferred=True) on any number of ranks: hop 1 parks y1 in the output rows, the mean is
+    formed once on hop 3 from x0, the parked y1 and the previous layer's own rows
+    (EPI_ACC_X with an explicit `prev`: on a shard they live in this rank's exchange piece,
+    not in the gathered table) — 6 instead of 8 epilogue row transfers per K=3 step, the same
+    additions in the same order as the eager schedule, so the same bits.
+    Buffers per schedule name: the rank's PIECE (rows_pad rows: what its hop writes and sends)
+    and the GATHERED table (world * rows_pad rows: what the next hop reads). One device: they
+    are the same buffer and nothing is exchanged. A mask that `masks` returns for a hop whose
+    epilogue only the column-ordered kernel has (ACC_X, ACC_INIT|ACC_ADD) is dropped: a dense
+    hop gives the same bits (a skipped zero row adds fmaf(v, 0, acc) = acc)."""
+    from .functional import lightgcn_hop_schedule
+    Y, Xa, Xb = work
+    n, d, dev = dg.n_local, x0_pad.shape[1], x0_pad.device
+    if dg.world == 1:
+        # y1 is gathered by hop 2 straight from the output rows: pad them to the table's rows
+        acc_piece = torch.empty((Xa.shape[0], d), dtype=torch.float32, device=dev)
+        acc_piece[n:].zero_()
+        piece = {"acc": acc_piece, "a": Xa, "b": Xb}
+        gath = dict(piece)
+    else:
+        acc_piece = torch.zeros((dg.rows_pad, d), dtype=torch.float32, device=dev)
+        piece = {"acc": acc_piece, "a": Y, "b": Y}
+        gath = {}
+    acc = acc_piece[:n]
+    sched = lightgcn_hop_schedule(K, deferred=True)
+    readers = {k: xn for k, (xn, _, _) in enumerate(sched, start=1)}
+    for k, (xn, yn, epi) in enumerate(sched, start=1):
+        x_in = x0_pad if xn == "x0" else gath[xn]
+        kw = mkw(k, x_in)
+        if kw and (epi & EPI_ACC_X or (epi & EPI_ACC_INIT and epi & EPI_ACC_ADD)):
+            kw = {}                                  # tiled-only epilogue: dense, same bits
+        prev = piece[xn][:n] if (epi & EPI_ACC_X) else None
+        y = piece[yn] if yn is not None else None
+        needed = yn is not None and any(readers.get(j) == yn for j in range(k + 1, K + 1))
+        common = dict(epi=epi, acc_div=float(K + 1))
+        if dg.world == 1 or not needed:
+            hop(dg.shard, x_in, None if y is None else y[:n], self_rows=self_rows, acc=acc,
+                prev=prev, **common, **kw)
+            continue
+        target = Xa if x_in is not Xa else Xb        # never the table this hop reads
+        if not chunked:
+            hop(dg.shard, x_in, y[:n], self_rows=self_rows, acc=acc, prev=prev, **common, **kw)
+            dg.exchange(target, y)
+        else:
+            pending = []
+            m = masks(k, x_in) if (masks is not None and kw) else None
+            for c0, c1 in dg.chunk_bounds(overlap_chunks):
+                r1 = min(c1, n)
+                if r1 > c0:
+                    ckw = {} if m is None else {"x_mask": m[0],
+                                                "y_active": None if m[1] is None else m[1][c0:r1]}
+                    hop(dg.shard.row_slice(c0, r1), x_in, y[c0:r1], self_rows=self_rows[c0:r1],
+                        acc=acc[c0:r1], prev=None if prev is None else prev[c0:r1], **common,
+                        **ckw, **chunk_kw)
+                pending += dg.post_chunk(target, y, c0, c1)
+            dg.finish(pending)
+        gath[yn] = target
+    if not gather_output or dg.world == 1:
+        return acc
+    Y[:n].copy_(acc)
     full = torch.empty_like(x0_pad)
     dg.all_gather(full, Y)
     return dg.unpad_table(full)

@@ -89,18 +89,33 @@ def _tiled_views_ok(*tables) -> bool:
     return all(t is None or (t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0) for t in tables)
 
 
+_TILED_OK: dict = {}
+
+
+def _tiled_supported(device, rows_per_block: int) -> bool:
+    """Whether `device` grants the column-ordered kernel its LDS (gnnrec_spmm_tiled_supported,
+    cached per device and block size)."""
+    key = (torch.device(device).index or 0, int(rows_per_block))
+    if key not in _TILED_OK:
+        _TILED_OK[key] = bool(_lib.lib().gnnrec_spmm_tiled_supported(*key))
+    return _TILED_OK[key]
+
+
 def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None,
                    reserve_cus: int = 0, outputs=()):
     """The column-ordered plan spmm_into would use for (adj, x) (and the `outputs` tables
-    it writes or reads row-wise), or None (CSR kernel)."""
+    it writes or reads row-wise), or None (CSR kernel). A device that cannot grant the
+    kernel's LDS (rows per block + 1 accumulator rows of 128 B) keeps the CSR kernel."""
     if (not TILED_HOP or x_mask is not None or y_active is not None or x.shape[1] % 32
             or adj.n_rows < max(TILED_MIN_ROWS, 1) or adj.nnz == 0
             or x.stride(0) > TILED_MAX_LDX or not _tiled_views_ok(x, *outputs)
             or x.shape[0] * x.shape[1] * 4 < TILED_MIN_TABLE_BYTES
             or adj.max_degree() > TILED_MAX_DEGREE):
         return None
-    return adj.tiled_plan(rows_per_block=_tiled_rows_per_block(adj.n_rows, x.device,
-                                                               reserve_cus))
+    R = _tiled_rows_per_block(adj.n_rows, x.device, reserve_cus)
+    if not _tiled_supported(x.device, R):
+        return None
+    return adj.tiled_plan(rows_per_block=R)
 
 
 def _heavy_args(adj: CsrGraph, x: torch.Tensor, heavy_threshold: int):
@@ -121,14 +136,15 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
               acc_div: float = 1.0, heavy_threshold: Optional[int] = None,
               x_mask: Optional[torch.Tensor] = None,
               y_active: Optional[torch.Tensor] = None, meet_us: Optional[int] = None,
-              reserve_cus: int = 0) -> None:
+              reserve_cus: int = 0, prev: Optional[torch.Tensor] = None) -> None:
     """y = A x with an optional fused layer-mean epilogue (gnnrec_spmm_csr_masked_f32: rows
     longer than `heavy_threshold` run on the workgroup-per-row kernel; rows of x whose
     `x_mask` byte is 0 are all-zero and are not gathered — same bits; destination rows whose
     `y_active` byte is 0 are not computed — y is +0 there, or the true value). `meet_us`: the
     column-ordered kernel's pass-start meeting bound (None: TILED_MEET_US); `reserve_cus`: its
-    single-pass grid leaves that many CUs free (_tiled_rows_per_block)."""
-    _require_device(adj, x, y, self_rows, acc)
+    single-pass grid leaves that many CUs free (_tiled_rows_per_block); `prev`: the ACC_X
+    rows (column-ordered kernel only; default x's own rows)."""
+    _require_device(adj, x, y, self_rows, acc, prev)
     if x_mask is not None and (x_mask.dtype != torch.uint8 or x_mask.device != x.device
                                or x_mask.numel() < adj.shape[1]):
         raise ValueError("x_mask must be a uint8 tensor on x's device with a byte per row")
@@ -143,10 +159,11 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
                          "destination row")
     plan = tiled_plan_for(adj, x, x_mask, y_active, reserve_cus,
                           outputs=(y, self_rows if epi & EPI_ACC_INIT else None,
-                                   acc if epi & (EPI_ACC_INIT | EPI_ACC_ADD) else None))
+                                   acc if epi & (EPI_ACC_INIT | EPI_ACC_ADD) else None,
+                                   prev if epi & EPI_ACC_X else None))
     if plan is not None:
         spmm_tiled_into(adj, x, y, plan, epi=epi, self_rows=self_rows, acc=acc, acc_div=acc_div,
-                        meet_us=meet_us)
+                        meet_us=meet_us, prev=prev)
         return
     check(L.gnnrec_spmm_csr_masked_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(x_mask),
                                        ptr(y_active), ptr(y), y.stride(0) if y is not None else d, d, epi,
@@ -160,18 +177,19 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
 def spmm_tiled_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], plan: dict, *,
                     epi: int = 0, self_rows: Optional[torch.Tensor] = None,
                     acc: Optional[torch.Tensor] = None, acc_div: float = 1.0,
-                    meet_us: Optional[int] = None) -> None:
+                    meet_us: Optional[int] = None, prev: Optional[torch.Tensor] = None) -> None:
     """spmm_into through the column-ordered kernel with an explicit plan (adj.tiled_plan());
     same results, bit for bit. The plan's sync words make
-    concurrent launches of one plan on different streams unsafe."""
-    _require_device(adj, x, y, self_rows, acc)
+    concurrent launches of one plan on different streams unsafe. `prev`: the ACC_X rows
+    ([n_rows, >= d]; None: x's own rows)."""
+    _require_device(adj, x, y, self_rows, acc, prev)
     d = x.shape[1]
     check(_lib.lib().gnnrec_spmm_tiled_f32(
-        ptr(plan["slot"]), ptr(plan["val"]), ptr(plan["hdr"]),
-        ptr(plan["wave_ptr"]), ptr(plan["n_steps"]), plan["n_blocks"], plan["rows_per_block"],
+        ptr(plan["stream"]), ptr(plan["wave_ptr"]), ptr(plan["n_steps"]), plan["n_blocks"], plan["rows_per_block"],
         ptr(x), x.shape[0], x.stride(0), ptr(y), y.stride(0) if y is not None else d, adj.n_rows,
         d, epi, ptr(self_rows), self_rows.stride(0) if self_rows is not None else d, ptr(acc),
-        acc.stride(0) if acc is not None else d, float(acc_div), ptr(plan["sync"]),
+        acc.stride(0) if acc is not None else d, float(acc_div), ptr(prev),
+        prev.stride(0) if prev is not None else d, ptr(plan["sync"]),
         int(TILED_MEET_US if meet_us is None else meet_us),
         _lib.stream_of(adj.device)), "gnnrec_spmm_tiled_f32")
 

@@ -32,6 +32,7 @@ from .graph import CsrGraph
 _LIVE: "weakref.WeakValueDictionary" = weakref.WeakValueDictionary()
 _OWNED: dict = {}          # raw-tensor operands: key -> (CsrGraph, source tensors)
 _OWNED_MAX = 4
+_OWNED_MAX_BYTES = 8 << 30  # operand bytes (CSR; cached plans come on top) kept alive here
 
 
 def _key(row_ptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, n_cols: int):
@@ -56,10 +57,20 @@ def graph_of(row_ptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, n_cols
     hit = _OWNED.get(k)
     if hit is not None:
         return hit[0]
-    if len(_OWNED) >= _OWNED_MAX:
-        _OWNED.pop(next(iter(_OWNED)))
+    # Not registered eagerly (e.g. an operand first seen under torch.compile, or one dropped
+    # before backward): a fresh CsrGraph re-derives its plans and transpose on first use —
+    # seconds of host work and GBs of device memory on a G100M-sized operand. Say so.
+    import warnings
+    nbytes = sum(t.numel() * t.element_size() for t in (row_ptr, col, val))
+    warnings.warn(f"gnnrec: operand ({row_ptr.numel() - 1} rows, {col.numel()} nnz) was not "
+                  "registered through functional.spmm / lightgcn_propagate; building a new "
+                  "CsrGraph (its tiled plan and transpose are rebuilt on first use)",
+                  RuntimeWarning, stacklevel=2)
+    while _OWNED and (len(_OWNED) >= _OWNED_MAX or
+                      sum(v[2] for v in _OWNED.values()) + nbytes > _OWNED_MAX_BYTES):
+        _OWNED.pop(next(iter(_OWNED)))          # oldest first
     g = CsrGraph(row_ptr, col, val, (row_ptr.numel() - 1, int(n_cols)))
-    _OWNED[k] = (g, (row_ptr, col, val))
+    _OWNED[k] = (g, (row_ptr, col, val), nbytes)
     return g
 
 

@@ -18,19 +18,26 @@ import oracle
 from conftest import golden_csr, load_golden
 
 from src.ops import CsrGraph
-from src.ops._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT, EPI_NO_Y
+from src.ops._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT, EPI_ACC_X, EPI_NO_Y
 from src.ops.distributed import DistributedGraph, lightgcn_propagate_dist
 
 
-def cpu_hop(adj, x, y, *, epi, self_rows, acc, acc_div):
-    """CPU stand-in for gnnrec_spmm_csr_f32 (oracle SpMM + the same epilogue order)."""
+def cpu_hop(adj, x, y, *, epi, self_rows, acc, acc_div, prev=None):
+    """CPU stand-in for gnnrec_spmm_tiled_f32 (oracle SpMM + the same epilogue order:
+    acc = (((self | acc) [+ acc on INIT|ADD]) [+ prev on ACC_X]) + y [/ div])."""
     yy = oracle.spmm(adj.row_ptr.numpy(), adj.col.numpy(), adj.val.numpy(), x.numpy())
+    if epi & (EPI_ACC_INIT | EPI_ACC_ADD):
+        b = (self_rows if epi & EPI_ACC_INIT else acc).numpy().copy()
+        if epi & EPI_ACC_INIT and epi & EPI_ACC_ADD:
+            b = b + acc.numpy()
+        if epi & EPI_ACC_X:
+            b = b + (prev if prev is not None else x[:adj.n_rows]).numpy()
+        b = b + yy
+        if epi & EPI_ACC_DIV:
+            b = b / np.float32(acc_div)
     if not (epi & EPI_NO_Y):
         y.copy_(torch.from_numpy(yy))
     if epi & (EPI_ACC_INIT | EPI_ACC_ADD):
-        b = (self_rows if epi & EPI_ACC_INIT else acc).numpy() + yy
-        if epi & EPI_ACC_DIV:
-            b = b / np.float32(acc_div)
         acc.copy_(torch.from_numpy(b.astype(np.float32)))
 
 
@@ -40,7 +47,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, K, balance, q, exchange="auto", chunks=1):
+def _worker(rank, world, port, K, balance, q, exchange="auto", chunks=1, deferred=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -51,9 +58,10 @@ def _worker(rank, world, port, K, balance, q, exchange="auto", chunks=1):
         x0 = torch.randn(full.shape[0], 32) * 0.1
         dg = DistributedGraph(full, rank, world, "cpu", balance=balance, exchange=exchange)
         xp = dg.pad_table(x0)
-        local = lightgcn_propagate_dist(dg, xp, K, hop_fn=cpu_hop, overlap_chunks=chunks)
+        local = lightgcn_propagate_dist(dg, xp, K, hop_fn=cpu_hop, overlap_chunks=chunks,
+                                        deferred=deferred)
         whole = lightgcn_propagate_dist(dg, xp, K, hop_fn=cpu_hop, gather_output=True,
-                                        overlap_chunks=chunks)
+                                        overlap_chunks=chunks, deferred=deferred)
         if rank == 0:
             ref = oracle.lightgcn(rp, col, val, x0.numpy(), K)
             q.put((whole.numpy(), ref, local.numpy(), ref[dg.row_begin:dg.row_end],
@@ -62,15 +70,23 @@ def _worker(rank, world, port, K, balance, q, exchange="auto", chunks=1):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,K,balance,exchange,chunks", [
-    (2, 3, "nnz", "auto", 1), (3, 2, "rows", "auto", 1), (2, 1, "nnz", "allgather", 1),
-    (4, 3, "nnz", "auto", 1), (4, 2, "nnz", "allgather", 1), (4, 3, "nnz", "p2p", 3),
-    (3, 3, "rows", "p2p", 4)])
-def test_sharded_propagation_matches_single_device(world, K, balance, exchange, chunks):
+@pytest.mark.parametrize("world,K,balance,exchange,chunks,deferred", [
+    (2, 3, "nnz", "auto", 1, False), (3, 2, "rows", "auto", 1, False),
+    (2, 1, "nnz", "allgather", 1, False), (4, 3, "nnz", "auto", 1, False),
+    (4, 2, "nnz", "allgather", 1, False), (4, 3, "nnz", "p2p", 3, False),
+    (3, 3, "rows", "p2p", 4, False),
+    # the deferred layer mean on shards (y1 parked in the output rows, hop 3's previous layer
+    # from the rank's own exchange piece): 2/3/4 ranks, both exchanges, chunked, K = 2, 3, 4
+    (2, 3, "nnz", "auto", 1, True), (4, 3, "nnz", "p2p", 3, True),
+    (3, 3, "rows", "allgather", 1, True), (4, 2, "nnz", "auto", 2, True),
+    (3, 4, "nnz", "p2p", 1, True), (1, 3, "nnz", "auto", 1, True)])
+def test_sharded_propagation_matches_single_device(world, K, balance, exchange, chunks,
+                                                   deferred):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, K, balance, q, exchange, chunks))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, K, balance, q, exchange, chunks,
+                                               deferred))
              for r in range(world)]
     for p in procs:
         p.start()

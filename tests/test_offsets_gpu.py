@@ -23,9 +23,11 @@ OFF = (1 << 31) + 4096          # a multiple of 4: the same 16-B alignment as th
 def case(cuda):
     rng = np.random.default_rng(23)
     nu, ni = 900, 700
-    u = np.concatenate([rng.integers(0, nu, 30000), np.zeros(600, np.int64), np.arange(nu)])
+    # power-law items, a hub user with 600 items, every node at least one edge
+    u = np.concatenate([rng.integers(0, nu, 30000), np.zeros(600, np.int64), np.arange(nu),
+                        rng.integers(0, nu, ni)])
     i = np.concatenate([np.minimum(rng.zipf(1.4, 30000) - 1, ni - 1), np.arange(600),
-                        rng.integers(0, ni, nu)])
+                        rng.integers(0, ni, nu), np.arange(ni)])
     g = CsrGraph.from_interactions(u, i, nu, ni)
     deg = np.diff(g.row_ptr.numpy())
     assert deg.max() > 600 and deg.min() >= 1

@@ -7,6 +7,7 @@
 //   hipcc --offload-arch=gfx950 -O3 tools/gather_probe2.hip -o tools/_var/gather_probe2
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 
 #define CHECK(x)                                                              \
   do {                                                                        \
@@ -119,7 +120,7 @@ int run(const float* t, size_t table_bytes, float* out, int cus) {
   return 0;
 }
 
-int main() {
+int main(int argc, char** argv) {
   int cus = 256;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const size_t max_bytes = (size_t)1 << 29;
@@ -128,7 +129,10 @@ int main() {
   CHECK(hipMalloc(&t, max_bytes));
   CHECK(hipMalloc(&out, 64));
   CHECK(hipMemset(t, 0, max_bytes));
+  // optional argument: one table size in MiB (PMC runs), else the three of the sweep
+  const size_t only = argc > 1 ? (size_t)atoi(argv[1]) << 20 : 0;
   for (size_t tb : {(size_t)2 << 20, (size_t)32 << 20, (size_t)512 << 20}) {
+    if (only && tb != only) continue;
     if (run<4, 8>(t, tb, out, cus)) return 1;
     if (run<4, 16>(t, tb, out, cus)) return 1;
     if (run<8, 8>(t, tb, out, cus)) return 1;
