@@ -50,7 +50,6 @@ constexpr int kGroups = GNNREC_TILED_GROUPS;      // slot streams per wave (8 la
 constexpr int kSteps = GNNREC_TILED_STEPS;        // steps per chunk
 constexpr int kTiledChunk = GNNREC_TILED_CHUNK;   // slots per chunk (one per lane)
 constexpr int kTiledTail = GNNREC_TILED_TAIL;
-constexpr int kChunkWords = 2 * GNNREC_TILED_CHUNK + GNNREC_TILED_HDR_WORDS;   // 132
 constexpr int kSlice = 32;                        // features per pass
 constexpr int kRowBytes = kSlice * 4;             // one LDS accumulator row, one gathered line
 constexpr int kRowBits = 11;
@@ -151,34 +150,19 @@ __device__ __forceinline__ float gbcastf(float v) {
 
 // The chunk header {step barriers before the chunk, chain mask lo, chain mask hi, panel base
 // column} is loaded with the slots as a vector load (lane l: word l % 4) and read back with
-// v_readlane: a scalar load would share lgkmcnt with the LDS chain and stall it. The plan is
-// ONE stream of chunks {64 x (slot word, value), 4 header words} read through a buffer
-// resource based at the wave's first chunk: the lane part of the offset is a constant VGPR
-// and the chunk part an SGPR (no per-load address math), one rsrc (SGPR pressure).
-struct PlanStream {
-  __amdgpu_buffer_rsrc_t r;   // the wave's chunks: kChunkWords words each
-  uint32_t lane_off;          // lane * 8: this lane's {word, value}
-  uint32_t hdr_off;           // the header word lane % 4
-};
-
-__device__ __forceinline__ PlanStream plan_stream(const uint32_t* plan, int64_t b, int lane) {
-  PlanStream p;
-  p.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(plan + b * kChunkWords), 0,
-                                          0x7FFFFFFF, 0x00020000);
-  p.lane_off = (uint32_t)lane * 8;
-  p.hdr_off = (uint32_t)(2 * kTiledChunk + (lane & 3)) * 4;
-  return p;
-}
-
-// chunk b + i of the wave (i < 2^21: a wave's chunks of one pass)
-__device__ __forceinline__ void tiled_slots(const PlanStream& p, int i, TiledSlots& m) {
-  if (GNNREC_TILED_EXP & 8) i &= 63;
-  const int so = i * (kChunkWords * 4);
-  // two adjacent dwords, merged into one buffer_load_dwordx2 by the compiler (the _b64
-  // builtin of this toolchain returned only the low dword)
-  m.w = __builtin_amdgcn_raw_buffer_load_b32(p.r, p.lane_off, so, 0);
-  m.v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(p.r, p.lane_off + 4, so, 0));
-  m.h = __builtin_amdgcn_raw_buffer_load_b32(p.r, p.hdr_off, so, 0);
+// v_readlane: a scalar load would share lgkmcnt with the LDS chain and stall it.
+// chunk c of the plan: this lane's slot word and value, and header word lane % 4 (three
+// coalesced vector loads; same-box A/B: separate 128-B-aligned arrays beat one interleaved
+// 528-B chunk stream by 4 %, profiles/r03/ab_interleaved_plan_vs_separate_fixed_range.txt)
+__device__ __forceinline__ void tiled_slots(const uint32_t* __restrict__ ss,
+                                            const float* __restrict__ sv,
+                                            const uint32_t* __restrict__ hdr, int64_t c, int lane,
+                                            TiledSlots& m) {
+  if (GNNREC_TILED_EXP & 8) c &= 63;
+  const int64_t i = c * kTiledChunk + lane;
+  m.w = ss[i];
+  m.v = sv[i];
+  m.h = hdr[4 * c + (lane & 3)];
 }
 
 template <int W>
@@ -187,15 +171,14 @@ __device__ __forceinline__ uint32_t hdr_word(const TiledSlots& m) {
 }
 
 // The gathers of a chunk read through a buffer whose base is its panel's first source row, so
-// lane offsets stay 32-bit for any table size; its range ends at the table's last row (in
-// 32-bit row units: all scalar arithmetic, no 64-bit compares).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const char* xs, uint32_t x_rows,
-                                                             uint32_t base, uint32_t row_bytes,
-                                                             uint32_t lim_rows) {
-  const uint32_t left = base < x_rows ? x_rows - base : 0u;
-  const uint32_t n = left >= lim_rows ? 0xFFFFFFFFu : left * row_bytes;
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(xs) + (uint64_t)base * row_bytes, 0,
-                                           (int)n, 0x00020000);
+// lane offsets stay 32-bit for any table size; its range ends at the table's last byte. (A
+// form in 32-bit row units was 5 % slower on the G100M hop: profiles/r03/bisect.jsonl.)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const char* xs, uint64_t xs_bytes,
+                                                             uint32_t base, uint32_t row_bytes) {
+  const uint64_t off = (uint64_t)base * row_bytes;
+  const uint64_t left = off < xs_bytes ? xs_bytes - off : 0;
+  const uint32_t n = left > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)left;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(xs) + off, 0, (int)n, 0x00020000);
 }
 
 // Rows [r0, r0 + rows) of a row-major fp32 table (row stride ld), from column slice * 32: the
@@ -394,7 +377,8 @@ __device__ __forceinline__ void run_ring(std::integer_sequence<int, I...>, F&& s
 }
 
 __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
-    const uint32_t* __restrict__ plan, const int64_t* __restrict__ wptr,
+    const uint32_t* __restrict__ ss, const float* __restrict__ sv,
+    const uint32_t* __restrict__ hdr, const int64_t* __restrict__ wptr,
     const int32_t* __restrict__ nsteps, int n_blocks, int nb_pad, int n_items, int R,
     const float* __restrict__ x, uint32_t x_rows32, uint32_t row_bytes,
     float* __restrict__ y, uint32_t ldy4, int n_rows, int epi, const float* __restrict__ self,
@@ -433,7 +417,7 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     GNNREC_TILED_STAMP(ev);
     const uint32_t soff = (uint32_t)slice * kRowBytes;
     const char* xs = reinterpret_cast<const char*>(x) + soff;
-    const uint32_t lim_rows = 0xFFFFFFFFu / row_bytes;   // rows whose bytes exceed 32 bits
+    const uint64_t xs_bytes = (uint64_t)x_rows32 * row_bytes - soff;
     const int64_t s = (int64_t)blk * kTiledWaves + w;
     const int64_t b = wptr[s], e = (GNNREC_TILED_EXP & 32) ? b : wptr[s + 1];
     int cur = 0;
@@ -443,21 +427,20 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
       // chunk c + kPlanAhead's slots, gathers chunk c + kGatherAhead and applies chunk c
       TiledSlots M[kMRing];
       f4 X[kXRing][kSteps];
-      const PlanStream ps = plan_stream(plan, b, lane);
       const int nc = (int)(e - b);   // this wave's chunks of the pass
       int c = 0;
 #pragma unroll
-      for (int j = 0; j < kPlanAhead; ++j) tiled_slots(ps, c + j, M[j]);
+      for (int j = 0; j < kPlanAhead; ++j) tiled_slots(ss, sv, hdr, b + c + j, lane, M[j]);
 #pragma unroll
       for (int j = 0; j < kGatherAhead; ++j)
-        tiled_gather(kSeq, chunk_rsrc(xs, x_rows32, hdr_word<3>(M[j]), row_bytes, lim_rows), q16,
+        tiled_gather(kSeq, chunk_rsrc(xs, xs_bytes, hdr_word<3>(M[j]), row_bytes), q16,
                      row_bytes, M[j], X[j]);
       auto stage = [&](auto ic) -> bool {
         constexpr int I = decltype(ic)::value;
-        tiled_slots(ps, c + kPlanAhead, M[(I + kPlanAhead) % kMRing]);
+        tiled_slots(ss, sv, hdr, b + c + kPlanAhead, lane, M[(I + kPlanAhead) % kMRing]);
         {
           const TiledSlots& mg = M[(I + kGatherAhead) % kMRing];
-          tiled_gather(kSeq, chunk_rsrc(xs, x_rows32, hdr_word<3>(mg), row_bytes, lim_rows), q16,
+          tiled_gather(kSeq, chunk_rsrc(xs, xs_bytes, hdr_word<3>(mg), row_bytes), q16,
                        row_bytes, mg, X[(I + kGatherAhead) % kXRing]);
         }
         const TiledSlots& ma = M[I % kMRing];
@@ -540,7 +523,9 @@ struct Run {
 };
 
 struct BlockPlan {
-  std::vector<uint32_t> stream[kTiledWaves];   // kChunkWords per chunk
+  std::vector<uint32_t> slot[kTiledWaves];
+  std::vector<float> val[kTiledWaves];
+  std::vector<uint32_t> hdr[kTiledWaves];   // 4 words per chunk
   int32_t nsteps = 0;
 };
 
@@ -670,20 +655,21 @@ void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_
           }
         }
         uint64_t cmask = 0;
-        std::vector<uint32_t>& o = out.stream[w];
         for (int q = 0; q < kGroups; ++q)       // lane 8 q + t: slot t of stream q
           for (int t = 0; t < kSteps; ++t) {
             const Slot& sl = hs[q][c + t];
             if (!sl.run) {
-              o.insert(o.end(), {x0 << kRowBits | (uint32_t)R, 0u});
+              out.slot[w].push_back(x0 << kRowBits | (uint32_t)R);
+              out.val[w].push_back(0.f);
               continue;
             }
             const int64_t k = sl.run->k + sl.t;
             if (t > 0 && hs[q][c + t - 1].run == sl.run) cmask |= 1ull << (kSteps * q + t);
-            o.insert(o.end(), {((uint32_t)col[k] - base) << kRowBits | (uint32_t)sl.run->row,
-                               __builtin_bit_cast(uint32_t, val[k])});
+            out.slot[w].push_back(((uint32_t)col[k] - base) << kRowBits | (uint32_t)sl.run->row);
+            out.val[w].push_back(val[k]);
           }
-        o.insert(o.end(), {bar, (uint32_t)cmask, (uint32_t)(cmask >> 32), base});
+        out.hdr[w].insert(out.hdr[w].end(),
+                          {bar, (uint32_t)cmask, (uint32_t)(cmask >> 32), base});
         bar = 0;
       }
       cur[w] = step;
@@ -738,40 +724,40 @@ extern "C" int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* co
   }
   int64_t tot = 0;
   for (const auto& bp : pl->blocks)
-    for (int w = 0; w < kTiledWaves; ++w) tot += (int64_t)bp.stream[w].size() / kChunkWords;
+    for (int w = 0; w < kTiledWaves; ++w) tot += (int64_t)bp.hdr[w].size() / 4;
   *n_chunks = tot;
   *n_blocks = pl->n_blocks;
   *plan = pl;
   return GNNREC_OK;
 }
 
-extern "C" int gnnrec_tiled_plan_emit(void* plan, uint32_t* stream, int64_t* wave_ptr,
-                                      int32_t* n_steps) {
-  GNNREC_REQUIRE(plan && stream && wave_ptr && n_steps, "tiled_emit: null pointer");
+extern "C" int gnnrec_tiled_plan_emit(void* plan, uint32_t* slot, float* val, uint32_t* hdr,
+                                      int64_t* wave_ptr, int32_t* n_steps) {
+  GNNREC_REQUIRE(plan && slot && val && hdr && wave_ptr && n_steps, "tiled_emit: null pointer");
   auto* pl = static_cast<TiledPlan*>(plan);
   const int64_t nb = pl->n_blocks;
   wave_ptr[0] = 0;
   for (int64_t b = 0; b < nb; ++b)
     for (int w = 0; w < kTiledWaves; ++w)
       wave_ptr[b * kTiledWaves + w + 1] =
-          wave_ptr[b * kTiledWaves + w] + (int64_t)pl->blocks[b].stream[w].size() / kChunkWords;
+          wave_ptr[b * kTiledWaves + w] + (int64_t)pl->blocks[b].hdr[w].size() / 4;
   for (int64_t b = 0; b < nb; ++b) {
     const BlockPlan& bp = pl->blocks[b];
     n_steps[b] = bp.nsteps;
-    for (int w = 0; w < kTiledWaves; ++w)
-      std::copy(bp.stream[w].begin(), bp.stream[w].end(),
-                stream + wave_ptr[b * kTiledWaves + w] * kChunkWords);
+    for (int w = 0; w < kTiledWaves; ++w) {
+      const int64_t c = wave_ptr[b * kTiledWaves + w];
+      std::copy(bp.slot[w].begin(), bp.slot[w].end(), slot + c * kTiledChunk);
+      std::copy(bp.val[w].begin(), bp.val[w].end(), val + c * kTiledChunk);
+      std::copy(bp.hdr[w].begin(), bp.hdr[w].end(), hdr + 4 * c);
+    }
   }
   // tail chunks for the last prefetches: harmless slots (row 0 of x, the scratch-row field)
   const int64_t end = wave_ptr[nb * kTiledWaves];
-  for (int64_t c = end; c < end + kTiledTail; ++c) {
-    uint32_t* o = stream + c * kChunkWords;
-    for (int l = 0; l < kTiledChunk; ++l) {
-      o[2 * l] = (uint32_t)kRowMask;
-      o[2 * l + 1] = 0u;
-    }
-    for (int q = 0; q < GNNREC_TILED_HDR_WORDS; ++q) o[2 * kTiledChunk + q] = 0u;
+  for (int64_t s = end * kTiledChunk; s < (end + kTiledTail) * kTiledChunk; ++s) {
+    slot[s] = (uint32_t)kRowMask;
+    val[s] = 0.f;
   }
+  for (int64_t s = 4 * end; s < 4 * (end + kTiledTail); ++s) hdr[s] = 0;
   return GNNREC_OK;
 }
 
@@ -810,7 +796,8 @@ extern "C" int gnnrec_spmm_tiled_supported(int32_t device, int32_t rows_per_bloc
   return ok;
 }
 
-extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* plan, const int64_t* wave_ptr,
+extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
+                                     const uint32_t* hdr, const int64_t* wave_ptr,
                                      const int32_t* n_steps, int64_t n_blocks,
                                      int32_t rows_per_block, const float* x, int64_t x_rows,
                                      int64_t ldx, float* y, int64_t ldy, int64_t n_rows, int32_t d,
@@ -852,7 +839,8 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* plan, const int64_t* wave_p
                  "spmm_tiled: output / self / acc row strides must be <= %lld",
                  (long long)kMaxLd);
   if (n_rows == 0) return GNNREC_OK;
-  GNNREC_REQUIRE(plan && wave_ptr && n_steps && x && sync, "spmm_tiled: null pointer");
+  GNNREC_REQUIRE(slot && val && hdr && wave_ptr && n_steps && x && sync,
+                 "spmm_tiled: null pointer");
   GNNREC_REQUIRE(aligned16(x) && ((epi & GNNREC_EPI_NO_Y) || aligned16(y)) &&
                      (!(epi & GNNREC_EPI_ACC_INIT) || aligned16(self)) &&
                      (!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) || aligned16(acc)),
@@ -875,7 +863,7 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* plan, const int64_t* wave_p
   if (hipMemsetAsync(sync, 0, GNNREC_TILED_SYNC_WORDS * sizeof(uint32_t), s) != hipSuccess)
     return check_launch("spmm_tiled (sync reset)");
   hipLaunchKernelGGL(tiled_hop_kernel, dim3((unsigned)grid), dim3(kTiledWaves * 64), lds, s,
-                     plan, wave_ptr, n_steps,
+                     slot, val, hdr, wave_ptr, n_steps,
                      (int)n_blocks, (int)nb_pad, (int)n_items, (int)rows_per_block, x,
                      (uint32_t)x_rows, (uint32_t)(ldx * 4), y, (uint32_t)(ldy * 4),
                      (int)n_rows, epi, self, (uint32_t)(ld_self * 4), acc, (uint32_t)(ld_acc * 4),

@@ -34,7 +34,6 @@ TILED_TAIL = 8
 TILED_MAX_ROWS = 1279
 TILED_SYNC_WORDS = 256
 TILED_HDR_WORDS = 4
-TILED_CHUNK_WORDS = 2 * TILED_CHUNK + TILED_HDR_WORDS   # one plan-stream chunk, uint32 words
 TILED_MAX_LDX = 1024
 TILED_MAX_PANEL = 1 << 20
 
@@ -57,10 +56,10 @@ _SIGNATURES = {
                                    _p, _i64, _p, _i64, _f32, _p, _i64, _i64, _p],
     "gnnrec_mark_active_rows": [_p, _p, _i64, _p, _i64, _p, _p],
     "gnnrec_tiled_plan_build": [_p, _p, _p, _i64, _i32, _i32, _i32, _i32, _p, _p, _p],
-    "gnnrec_tiled_plan_emit": [_p, _p, _p, _p],
+    "gnnrec_tiled_plan_emit": [_p, _p, _p, _p, _p, _p],
     "gnnrec_tiled_plan_free": [_p],
     "gnnrec_spmm_tiled_supported": [_i32, _i32],
-    "gnnrec_spmm_tiled_f32": [_p, _p, _p, _i64, _i32, _p, _i64, _i64, _p, _i64,
+    "gnnrec_spmm_tiled_f32": [_p, _p, _p, _p, _p, _i64, _i32, _p, _i64, _i64, _p, _i64,
                               _i64, _i32, _i32, _p, _i64, _p, _i64, _f32, _p, _i64, _p, _i32, _p],
     "gnnrec_row_nonzero_f32": [_p, _i64, _i64, _i32, _p, _p],
     "gnnrec_lightgcn_split_f32": [_p, _p, _p, _i64, _p, _i32, _i32, _p, _p, _p, _p, _i64, _p,

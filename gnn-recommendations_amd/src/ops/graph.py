@@ -389,18 +389,23 @@ class CsrGraph:
                                                  C.byref(n_blocks)), "gnnrec_tiled_plan_build")
             nb = n_blocks.value
             chunks = n_chunks.value + _lib.TILED_TAIL          # + tail chunks (prefetch)
-            stream = np.empty(chunks * _lib.TILED_CHUNK_WORDS, np.uint32)
+            slot = np.empty(chunks * _lib.TILED_CHUNK, np.uint32)
+            v = np.empty(chunks * _lib.TILED_CHUNK, np.float32)
+            hdr = np.empty(chunks * _lib.TILED_HDR_WORDS, np.uint32)
             wave_ptr = np.empty(nb * _lib.TILED_WAVES + 1, np.int64)
             n_steps = np.empty(max(nb, 1), np.int32)
             try:
-                _lib.check(L.gnnrec_tiled_plan_emit(h, stream.ctypes.data, wave_ptr.ctypes.data,
+                _lib.check(L.gnnrec_tiled_plan_emit(h, slot.ctypes.data, v.ctypes.data,
+                                                    hdr.ctypes.data, wave_ptr.ctypes.data,
                                                     n_steps.ctypes.data),
                            "gnnrec_tiled_plan_emit")
             finally:
                 L.gnnrec_tiled_plan_free(h)
             dev = self.device
             self._plans[key] = dict(
-                stream=torch.from_numpy(stream.view(np.int32)).to(dev),
+                slot=torch.from_numpy(slot.view(np.int32)).to(dev),
+                val=torch.from_numpy(v).to(dev),
+                hdr=torch.from_numpy(hdr.view(np.int32)).to(dev),
                 wave_ptr=torch.from_numpy(wave_ptr).to(dev),
                 n_steps=torch.from_numpy(n_steps).to(dev),
                 n_blocks=nb, rows_per_block=int(rows_per_block),

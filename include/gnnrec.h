@@ -149,16 +149,15 @@ int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col, const
  * gnnrec_tiled_plan_emit into caller buffers, then gnnrec_tiled_plan_free); the plan depends
  * on neither d nor the x table's stride. Per (block, wave) the plan is a run of chunks; a
  * chunk is GNNREC_TILED_STEPS steps x GNNREC_TILED_GROUPS streams = GNNREC_TILED_CHUNK slots,
- * stored as ONE stream of GNNREC_TILED_CHUNK_WORDS uint32 words per chunk (ABI 7; ABI 6 had
- * separate slot / value / header arrays and two 16-slot halves): words 2 l, 2 l + 1 = slot
- * l = 8 g + t (slot t of stream g): the slot word ((col - panel base) << 11 | local row; row
- * rows_per_block = a padding slot) and the fp32 value's bits; then hdr[4] = {step barriers
- * before the chunk, chain mask bits 0-31, bits 32-63 (bit 8 g + t = slot t of stream g
- * continues slot t-1's row), panel base column (every slot of a chunk lies in one panel of at
- * most 2^20 columns)}. Inside a stream a row appears in each group of 4 slots (steps 0-3, 4-7
- * of a chunk) as at most one run of consecutive slots. The stream holds (n_chunks +
- * GNNREC_TILED_TAIL) chunks (tail chunks read by the last prefetches); wave_ptr
- * [n_blocks * GNNREC_TILED_WAVES + 1] are chunk offsets; n_steps [n_blocks].
+ * entry 8 g + t = slot t of stream g (ABI 7; ABI 6 had two 16-slot halves); a slot is one
+ * uint32 word ((col - panel base) << 11 | local row; row rows_per_block = a padding slot) and
+ * one fp32 value; per chunk hdr[4] = {step barriers before the chunk, chain mask bits 0-31,
+ * bits 32-63 (bit 8 g + t = slot t of stream g continues slot t-1's row), panel base column
+ * (every slot of a chunk lies in one panel of at most 2^20 columns)}. Inside a stream a row
+ * appears in each group of 4 slots (steps 0-3, 4-7 of a chunk) as at most one run of
+ * consecutive slots. Slot arrays hold (n_chunks + GNNREC_TILED_TAIL) * GNNREC_TILED_CHUNK
+ * entries, hdr 4 * (n_chunks + GNNREC_TILED_TAIL) (tail chunks read by the last prefetches);
+ * wave_ptr [n_blocks * GNNREC_TILED_WAVES + 1] are chunk offsets; n_steps [n_blocks].
  * rows_per_block <= GNNREC_TILED_MAX_ROWS. gnnrec_spmm_tiled_f32 needs d % 32 == 0,
  * d <= ldx <= GNNREC_TILED_MAX_LDX (any table size), every table 16-B aligned with its
  * leading dimension a multiple of 4, `sync`: a device scratch of GNNREC_TILED_SYNC_WORDS
@@ -174,14 +173,14 @@ int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col, const
 #define GNNREC_TILED_MAX_ROWS 1279
 #define GNNREC_TILED_SYNC_WORDS 256
 #define GNNREC_TILED_HDR_WORDS 4
-#define GNNREC_TILED_CHUNK_WORDS (2 * GNNREC_TILED_CHUNK + GNNREC_TILED_HDR_WORDS)
 #define GNNREC_TILED_MAX_LDX 1024
 
 int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* col, const float* val,
                             int64_t n_rows, int32_t rows_per_block, int32_t panel,
                             int32_t sub_panel, int32_t n_threads, void** plan,
                             int64_t* n_chunks, int64_t* n_blocks);
-int gnnrec_tiled_plan_emit(void* plan, uint32_t* stream, int64_t* wave_ptr, int32_t* n_steps);
+int gnnrec_tiled_plan_emit(void* plan, uint32_t* slot, float* val, uint32_t* hdr,
+                           int64_t* wave_ptr, int32_t* n_steps);
 int gnnrec_tiled_plan_free(void* plan);
 
 /* 1 when `device` grants gnnrec_spmm_tiled_f32 the dynamic LDS of `rows_per_block` rows
@@ -189,8 +188,8 @@ int gnnrec_tiled_plan_free(void* plan);
  * then keeps the row-parallel hop (gnnrec_spmm_csr_masked_f32). */
 int gnnrec_spmm_tiled_supported(int32_t device, int32_t rows_per_block);
 
-int gnnrec_spmm_tiled_f32(const uint32_t* plan, const int64_t* wave_ptr,
-                          const int32_t* n_steps, int64_t n_blocks,
+int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val, const uint32_t* hdr,
+                          const int64_t* wave_ptr, const int32_t* n_steps, int64_t n_blocks,
                           int32_t rows_per_block, const float* x, int64_t x_rows, int64_t ldx,
                           float* y, int64_t ldy, int64_t n_rows, int32_t d, int32_t epi,
                           const float* self, int64_t ld_self, float* acc, int64_t ld_acc,

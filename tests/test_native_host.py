@@ -105,10 +105,9 @@ def _walk_tiled_plan(plan, n_rows, R):
     stream g; per-chunk {barriers, chain mask lo, hi, panel base}; slot word = (col - base) <<
     11 | row; a row at most one run per group of 4 slots of a stream; every slot of a chunk
     inside its panel)."""
-    st = plan["stream"].numpy().view(np.uint32).reshape(-1, _lib.TILED_CHUNK_WORDS)
-    sw = st[:, 0:2 * _lib.TILED_CHUNK:2].reshape(-1)              # slot words, chunk-major
-    val = st[:, 1:2 * _lib.TILED_CHUNK:2].reshape(-1).view(np.float32)
-    hdr = st[:, 2 * _lib.TILED_CHUNK:].reshape(-1)
+    sw = plan["slot"].numpy().view(np.uint32)
+    val = plan["val"].numpy()
+    hdr = plan["hdr"].numpy().view(np.uint32)
     panel = plan["panel"]
     wp = plan["wave_ptr"].numpy()
     ns = plan["n_steps"].numpy()
@@ -170,7 +169,8 @@ def test_tiled_plan_preserves_every_row_chain(R, panel, sub):
     n = G.shape[0]
     assert plan["n_blocks"] == (n + R - 1) // R
     assert plan["n_slots"] >= G.nnz
-    assert plan["stream"].numel() == (plan["n_chunks"] + _lib.TILED_TAIL) * _lib.TILED_CHUNK_WORDS
+    assert plan["slot"].numel() == (plan["n_chunks"] + _lib.TILED_TAIL) * _lib.TILED_CHUNK
+    assert plan["hdr"].numel() == 4 * (plan["n_chunks"] + _lib.TILED_TAIL)
     seq = _walk_tiled_plan(plan, n, R)
     rp, col, val = G.row_ptr.numpy(), G.col.numpy(), G.val.numpy()
     for r in range(n):
@@ -265,8 +265,10 @@ def test_tiled_plan_build_with_offsets_past_2_31():
                                              val.ctypes.data - 4 * shift, rp.size - 1, 37, 256,
                                              32, 2, C.byref(h), C.byref(nc), C.byref(nb)), "build")
         chunks = nc.value + _lib.TILED_TAIL
-        arrs = (np.empty(chunks * _lib.TILED_CHUNK_WORDS, np.uint32),
-                np.empty(nb.value * _lib.TILED_WAVES + 1, np.int64), np.empty(nb.value, np.int32))
+        arrs = (np.empty(chunks * _lib.TILED_CHUNK, np.uint32),
+                np.empty(chunks * _lib.TILED_CHUNK, np.float32),
+                np.empty(chunks * 4, np.uint32), np.empty(nb.value * _lib.TILED_WAVES + 1, np.int64),
+                np.empty(nb.value, np.int32))
         try:
             _lib.check(L.gnnrec_tiled_plan_emit(h, *(a.ctypes.data for a in arrs)), "emit")
         finally:

@@ -45,11 +45,11 @@ for spec in args:
     if FOLD:
         plan = dict(plan)
         rows = FOLD // (4 * LDX)     # slot words re-pointed into the first FOLD bytes
-        st = plan["stream"].clone().view(-1, 132)      # chunk: 64 x (word, value), 4 hdr
-        w = st[:, 0:128:2].long() & 0xFFFFFFFF
-        st[:, 0:128:2] = ((torch.remainder(w >> 11, rows) << 11) | (w & 2047)).int()
-        st[:, 131] = 0                                  # panel base
-        plan["stream"] = st.view(-1)
+        w = plan["slot"].long() & 0xFFFFFFFF
+        plan["slot"] = ((torch.remainder(w >> 11, rows) << 11) | (w & 2047)).int()
+        hdr = plan["hdr"].clone().view(-1, 4)
+        hdr[:, 3] = 0                                   # panel base
+        plan["hdr"] = hdr.view(-1)
     times = []
     for _ in range(12):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
