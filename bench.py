@@ -12,10 +12,12 @@ LightGCN.forward (lightgcn.py:76-95), eval mode.
 
 One step = one full propagation (K SpMM hops with the layer mean fused into their
 epilogues) with the operand and x0 already resident in HBM. value = K * nnz / t_step
-(edges/s, every stored nonzero one directed message). N > 1: destination-row shards over the
-SAME graph (strong scaling) with one RCCL exchange per hop — all-gather, or bipartite
-point-to-point with 1/4/8 overlap chunks, whichever whole steps time fastest before the
-timed region (src/ops/distributed.py); t_step = max over ranks.
+(edges/s, every stored nonzero one directed message). N > 1: the SAME graph (strong scaling)
+on a grid of F feature groups x N/F destination-row shards (RankGrid, src/ops/distributed.py:
+F = gcd(N, d/32) by default, so d = 64 on 2 GPUs runs two 32-feature halves with no exchange
+at all); within a feature group, one RCCL exchange per hop of that group's columns —
+all-gather, or bipartite point-to-point with 1/4/8 overlap chunks, whichever whole steps time
+fastest before the timed region; t_step = max over ranks.
 
 Also reported: roofline of the dominant kernel (the SpMM hop) from HIP events around every
 hop launch inside the timed region — `achieved`/`frac` on SURVEY §8(d)'s compulsory bytes
@@ -46,7 +48,7 @@ sys.path.insert(0, str(ROOT))
 from src.ops import CsrGraph  # noqa: E402
 from src.ops import functional as F  # noqa: E402
 from src.ops._lib import EPI_ACC_ADD, EPI_ACC_INIT, EPI_ACC_X, EPI_NO_Y  # noqa: E402
-from src.ops.distributed import (DistributedGraph, lightgcn_propagate_dist,  # noqa: E402
+from src.ops.distributed import (RankGrid, lightgcn_propagate_dist,  # noqa: E402
                                  make_work, _native_hop)
 
 METRIC = "edges/s + achieved HBM GB/s, LightGCN K=3 dim=64, 1/2/4/8 MI355X"
@@ -289,7 +291,7 @@ def cpu_baseline(g: CsrGraph, x0: torch.Tensor, K: int, n_users: int, gpu_hop1: 
                               "output_max_abs_diff": max_abs}}
 
 
-def verify(dg, full: CsrGraph, x0, x0_pad, K, out, device, rank) -> dict:
+def verify(dg, full: CsrGraph, x0, x0_pad, K, out, device, rank, cols) -> dict:
     """Full-size parity: this rank's rows of the timed (possibly sharded) propagation must equal,
     bit for bit, a single-device propagation of the whole graph (the oracle itself is checked
     against that kernel in tests/, at sizes it finishes in seconds)."""
@@ -297,7 +299,7 @@ def verify(dg, full: CsrGraph, x0, x0_pad, K, out, device, rank) -> dict:
     g1 = full.to(device)
     ref, _ = F.lightgcn_forward(g1, x0.to(device), K)
     mine = out
-    same = torch.equal(ref[dg.row_begin:dg.row_end], mine)
+    same = torch.equal(ref[dg.row_begin:dg.row_end, cols[0]:cols[1]], mine)
     res = {"bit_exact_vs_single_device": bool(same), "rows": int(mine.shape[0])}
     del g1, ref
     return res
@@ -323,6 +325,9 @@ def main(argv=None) -> int:
     ap.add_argument("--exchange", default="auto", choices=["auto", "allgather", "p2p"],
                     help="per-hop exchange: allgather, bipartite point-to-point, or auto "
                          "(time both before the timed region, keep the faster)")
+    ap.add_argument("--feature-groups", type=int, default=0,
+                    help="N > 1: F feature groups x N/F row shards (0 = the largest F dividing "
+                         "N and the d/32 feature slices; 1 = row shards only)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: test harness for several ranks sharing one GPU (host-staged "
                          "all-gather); the benchmark itself uses nccl = RCCL")
@@ -360,24 +365,27 @@ def main(argv=None) -> int:
     x0 = torch.randn(N, d, dtype=torch.float32) * 0.1  # nn.init.normal_(std=init_scale=0.1)
 
     t0 = time.perf_counter()
-    dg = DistributedGraph(full, rank, world, device,
-                          exchange="p2p" if a.exchange == "auto" else a.exchange)
+    grid = RankGrid(full, rank, world, device, d, a.feature_groups or None,
+                    exchange="p2p" if a.exchange == "auto" else a.exchange)
+    dg = grid.dg
     src = distinct_cols(dg.shard, dg.shard.shape[1])
-    x0_pad = dg.pad_table(x0)
-    work = make_work(dg, d, device)
+    x0_pad = grid.x0_table(x0)
+    d_loc = x0_pad.shape[1]          # this rank's feature columns (d / F)
+    work = make_work(dg, d_loc, device)
     # operand re-layout for the column-ordered hop (built once, outside the timed region)
     t1 = time.perf_counter()
     tiled = F.tiled_plan_for(dg.shard, x0_pad) is not None
     plan_s = time.perf_counter() - t1
     torch.cuda.synchronize()
-    log(f"rank {rank}: rows [{dg.row_begin},{dg.row_end}) nnz={dg.shard.nnz} src={src} "
+    log(f"rank {rank}: rows [{dg.row_begin},{dg.row_end}) cols [{grid.cols[0]},{grid.cols[1]}) "
+        f"nnz={dg.shard.nnz} src={src} "
         f"uploaded in {time.perf_counter() - t0:.1f}s (tiled plan {plan_s:.1f}s)")
     cpu_graph = full if (rank == 0 and world == 1 and not a.no_cpu_baseline) else None
     verify_graph = full if a.verify else None
     del full
 
     timer = HopTimer()
-    xtimer = ExchangeTimer(dg) if world > 1 else None
+    xtimer = ExchangeTimer(dg) if dg.world > 1 else None
     chunks, reserve = 1, 0
 
     def step():
@@ -386,8 +394,8 @@ def main(argv=None) -> int:
 
     # Exchange form (N > 1): time whole steps of each candidate before the timed region and
     # keep the fastest (same decision on every rank: max over ranks).
-    exchange_info = {"mode": dg.exchange_mode, "overlap_chunks": 1}
-    if world > 1:
+    exchange_info = {"mode": dg.exchange_mode if dg.world > 1 else "none", "overlap_chunks": 1}
+    if dg.world > 1:
         # (mode, overlap chunks, CUs a chunk kernel leaves to the concurrent RCCL kernels)
         cands = [("allgather", 1, 0)]
         if not bool(dg.needs.all()) and a.exchange in ("auto", "p2p"):
@@ -442,11 +450,11 @@ def main(argv=None) -> int:
     ms_per_step = elapsed / a.steps * 1e3
 
     durs = timer.durations_ms()
-    alg_bytes = float(hop_bytes_alg(dg.shard.nnz, dg.n_local, src, d))
+    alg_bytes = float(hop_bytes_alg(dg.shard.nnz, dg.n_local, src, d_loc))
     # column-ordered kernel: the deferred layer mean (lightgcn_propagate_dist), on shards too
     # unless the flag hop would be chunked (K > 3 with overlap chunks)
     deferred = tiled and K >= 2 and (K <= 3 or chunks == 1 or world == 1)
-    per_hop = hop_bytes(dg.shard.nnz, dg.n_local, src, d, K, world, deferred=deferred)
+    per_hop = hop_bytes(dg.shard.nnz, dg.n_local, src, d_loc, K, dg.world, deferred=deferred)
     launch_bytes = float(np.mean(per_hop))
     # kernel time per hop (= per launch at N=1; the sum of its chunk launches when the hop is
     # split into overlap chunks)
@@ -454,16 +462,18 @@ def main(argv=None) -> int:
     achieved = alg_bytes / (launch_ms * 1e-3) / 1e9
     achieved_fused = launch_bytes / (launch_ms * 1e-3) / 1e9
 
-    # cross-rank totals
-    nnz_total = torch.tensor([float(dg.shard.nnz)], dtype=torch.float64, device=device)
+    # cross-rank totals: an edge's d features are split over the F ranks of its row shard,
+    # so each rank contributes its nnz times its share of the features
+    nnz_total = torch.tensor([float(dg.shard.nnz) * d_loc / d], dtype=torch.float64,
+                             device=device)
     if world > 1:
         dist.all_reduce(nnz_total)
-    nnz_total = float(nnz_total.item())
+    nnz_total = float(round(nnz_total.item()))
     value = K * nnz_total / (ms_per_step * 1e-3)
 
     check = None
     if a.verify:
-        check = verify(dg, verify_graph, x0, x0_pad, K, out, device, rank)
+        check = verify(dg, verify_graph, x0, x0_pad, K, out, device, rank, grid.cols)
         if world > 1:
             ok = torch.tensor([1 if check["bit_exact_vs_single_device"] else 0], device=device)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
@@ -505,12 +515,13 @@ def main(argv=None) -> int:
                             + ("G100M" if nnz_total == G100M_NNZ else f"{a.users}x{a.items} synthetic"),
                 "graph": f"{a.users} users x {a.items} items, {a.pairs} pairs default_rng({a.seed}), deduplicated",
                 "nnz": int(nnz_total), "n_nodes": N, "n_layers": K, "dim": d,
-                "parallelism": f"dst-row shards x{world}" + (
+                "parallelism": (f"{grid.F} feature groups x " if grid.F > 1 else "")
+                + f"dst-row shards x{grid.R}" + (
                     f" + per-hop RCCL exchange ({exchange_info['mode']}, "
                     f"{exchange_info['overlap_chunks']} overlap chunks"
                     + (f", {exchange_info['reserved_cus']} CUs left to RCCL"
                        if exchange_info.get('reserved_cus') else "") + ")"
-                    if world > 1 else ""),
+                    if grid.R > 1 else ""),
             },
             "roofline": {
                 "bound": "hbm",
@@ -550,7 +561,8 @@ def main(argv=None) -> int:
             "edges_per_s_per_interaction": value / 2.0,
             "hbm_gbps_algorithmic_step": K * launch_bytes * world / (ms_per_step * 1e-3) / 1e9,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
-            "exchange": dict(exchange_info, recv_bytes_per_hop_per_rank=dg.recv_rows() * d * 4,
+            "exchange": dict(exchange_info, recv_bytes_per_hop_per_rank=dg.recv_rows() * d_loc * 4,
+                             feature_groups=grid.F, row_shards=grid.R,
                              # rank 0's compute-stream view per exchanged hop (K - 1 per step)
                              exchange_ms_per_hop=(float(np.sum(xtimer.durations_ms()))
                                                   / (a.steps * max(1, K - 1))) if xtimer else None,

@@ -22,9 +22,20 @@ user range); `gather_output=True` returns the full table.
 The local hop is injectable (`hop_fn`, default: the native gnnrec_spmm_csr_f32 wrapper) so
 the partition / gather / epilogue bookkeeping is testable on CPU ranks over gloo with the
 oracle as the local hop (tests/test_distributed.py).
+
+Feature groups (RankGrid): propagation is independent per feature column (y[:, f] = A x[:, f]
+with the same fmaf chain for every f), and the column-ordered kernel already runs a hop as
+d/32 independent 32-feature slices. So the ranks form a grid of F feature groups x R row
+shards (rank = r * F + f): rank (r, f) propagates columns [f d/F, (f+1) d/F) of its row
+shard, and the per-hop exchange runs only among the R ranks of its feature group, with 1/F
+of the row bytes. At F = world (d = 64: two GPUs) no hop exchanges anything. Every edge
+still costs one 128-B line per 32-feature slice on exactly one rank, so the per-rank kernel
+work is 1/world of the hop either way; the exchanged bytes per rank drop from
+(world-1)/world to (R-1)/R/F of the table.
 """
 from __future__ import annotations
 
+import math
 from typing import Callable, Optional
 
 import numpy as np
@@ -49,8 +60,14 @@ class DistributedGraph:
     """This rank's shard of the operand plus the padded layout helpers."""
 
     def __init__(self, full: CsrGraph, rank: int, world: int, device,
-                 balance: str = "nnz", group=None, exchange: str = "auto"):
+                 balance: str = "nnz", group=None, exchange: str = "auto",
+                 ranks: Optional[list] = None):
+        """rank / world: this rank's index among the `group` ranks that shard the rows;
+        ranks: their global ranks (point-to-point peers), default 0 .. world-1."""
         self.rank, self.world, self.group = rank, world, group
+        self.ranks = list(ranks) if ranks is not None else list(range(world))
+        if len(self.ranks) != world:
+            raise ValueError("ranks must list the global rank of every row shard")
         self.device = torch.device(device)
         self.shard = full.shard(rank, world, balance).to(self.device)
         info = self.shard.shard_info
@@ -123,11 +140,11 @@ class DistributedGraph:
             if q == me:
                 continue
             if self.needs[q, me]:
-                ops.append(dist.P2POp(dist.isend, src, q, self.group))
+                ops.append(dist.P2POp(dist.isend, src, self.ranks[q], self.group))
             if self.needs[me, q]:
                 dst = out[q * rp:(q + 1) * rp]
                 buf = torch.empty(dst.shape, dtype=dst.dtype) if staged else dst
-                ops.append(dist.P2POp(dist.irecv, buf, q, self.group))
+                ops.append(dist.P2POp(dist.irecv, buf, self.ranks[q], self.group))
                 landing.append((dst, buf))
         if self.needs[me, me]:
             out[me * rp:(me + 1) * rp].copy_(piece)
@@ -155,11 +172,11 @@ class DistributedGraph:
             if q == me:
                 continue
             if self.needs[q, me]:
-                ops.append(dist.P2POp(dist.isend, src, q, self.group))
+                ops.append(dist.P2POp(dist.isend, src, self.ranks[q], self.group))
             if self.needs[me, q]:
                 dst = out[q * rp + c0:q * rp + c1]
                 buf = torch.empty(dst.shape, dtype=dst.dtype) if staged else dst
-                ops.append(dist.P2POp(dist.irecv, buf, q, self.group))
+                ops.append(dist.P2POp(dist.irecv, buf, self.ranks[q], self.group))
                 if staged:
                     landing.append((dst, buf))
         if self.needs[me, me]:
@@ -185,6 +202,76 @@ class DistributedGraph:
             out.copy_(host)
         else:
             dist.all_gather_into_tensor(out, piece, group=self.group)
+
+
+def feature_groups_for(world: int, d: int, requested: Optional[int] = None) -> int:
+    """F of the rank grid: `requested` if it divides both world and the d/32 feature slices,
+    else (None) the largest such divisor, gcd(world, d/32); 1 when d % 32 != 0."""
+    slices = d // 32 if d % 32 == 0 else 1
+    if requested is None:
+        return math.gcd(world, slices)
+    F = int(requested)
+    if F < 1 or world % F or slices % F:
+        raise ValueError(f"feature_groups={F} must divide the world ({world}) and the "
+                         f"{slices} 32-feature slices of d={d}")
+    return F
+
+
+class RankGrid:
+    """F feature groups x R row shards (module doc): rank = r * F + f owns columns
+    `cols` of the rows of row shard r. `dg` is the row-shard DistributedGraph over the R
+    ranks of feature group f (its exchange runs in that process group); `col_group` joins
+    the F ranks of row shard r (gather_features). Every rank of the job must construct the
+    grid (process groups are created collectively, in the same order everywhere)."""
+
+    def __init__(self, full: CsrGraph, rank: int, world: int, device, d: int,
+                 feature_groups: Optional[int] = None, balance: str = "nnz",
+                 exchange: str = "auto"):
+        F = feature_groups_for(world, d, feature_groups)
+        R = world // F
+        self.F, self.R, self.d = F, R, d
+        self.f, self.r = rank % F, rank // F
+        self.cols = (self.f * d // F, (self.f + 1) * d // F)
+        row_group, self.col_group = None, None
+        if world > 1 and F > 1:
+            for f in range(F):
+                g = dist.new_group([r * F + f for r in range(R)])
+                if f == self.f:
+                    row_group = g
+            for r in range(R):
+                g = dist.new_group([r * F + f for f in range(F)])
+                if r == self.r:
+                    self.col_group = g
+        self.dg = DistributedGraph(full, self.r, R, device, balance, group=row_group,
+                                   exchange=exchange,
+                                   ranks=[r * F + self.f for r in range(R)])
+
+    def x0_table(self, x0: torch.Tensor) -> torch.Tensor:
+        """This rank's columns of the [N, d] initial table in the row shards' padded layout."""
+        c0, c1 = self.cols
+        return self.dg.pad_table(x0[:, c0:c1].contiguous())
+
+    def gather_features(self, local: torch.Tensor) -> torch.Tensor:
+        """[n, d/F] column block of this rank -> [n, d] rows of its row shard (all F column
+        blocks of the same rows, from the ranks of its row shard)."""
+        if self.F == 1:
+            return local
+        local = local.contiguous()
+        staged = local.is_cuda and dist.get_backend(self.col_group) == "gloo"
+        src = local.cpu() if staged else local
+        parts = [torch.empty_like(src) for _ in range(self.F)]
+        dist.all_gather(parts, src, group=self.col_group)
+        return torch.cat(parts, dim=1).to(local.device)
+
+
+def lightgcn_propagate_grid(grid: RankGrid, x0_cols: torch.Tensor, n_layers: int,
+                            **kw) -> torch.Tensor:
+    """lightgcn_propagate_dist on the rank grid: x0_cols = grid.x0_table(x0). Returns this
+    rank's [rows of its shard, d/F] block of mean(x0..xK); gather_output=True: the full
+    [N, d] table on every rank."""
+    gather = kw.pop("gather_output", False)
+    out = lightgcn_propagate_dist(grid.dg, x0_cols, n_layers, gather_output=gather, **kw)
+    return grid.gather_features(out) if gather else out
 
 
 def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers: int, *,

@@ -19,7 +19,8 @@ from conftest import golden_csr, load_golden
 
 from src.ops import CsrGraph
 from src.ops._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT, EPI_ACC_X, EPI_NO_Y
-from src.ops.distributed import DistributedGraph, lightgcn_propagate_dist
+from src.ops.distributed import (DistributedGraph, RankGrid, feature_groups_for,
+                                 lightgcn_propagate_dist, lightgcn_propagate_grid)
 
 
 def cpu_hop(adj, x, y, *, epi, self_rows, acc, acc_div, prev=None):
@@ -99,6 +100,74 @@ def test_sharded_propagation_matches_single_device(world, K, balance, exchange, 
         assert p.exitcode == 0
     np.testing.assert_array_equal(whole.view(np.uint32), ref.view(np.uint32))
     np.testing.assert_array_equal(local.view(np.uint32), ref_local.view(np.uint32))
+
+
+def _grid_worker(rank, world, port, K, d, F, exchange, deferred, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rp, col, val, nu, ni = golden_csr("g_small")
+        full = CsrGraph(torch.from_numpy(rp), torch.from_numpy(col), torch.from_numpy(val),
+                        (rp.size - 1, rp.size - 1), nu, ni, True)
+        torch.manual_seed(6)
+        x0 = torch.randn(full.shape[0], d) * 0.1
+        grid = RankGrid(full, rank, world, "cpu", d, F, exchange=exchange)
+        xc = grid.x0_table(x0)
+        local = lightgcn_propagate_grid(grid, xc, K, hop_fn=cpu_hop, deferred=deferred)
+        whole = lightgcn_propagate_grid(grid, xc, K, hop_fn=cpu_hop, gather_output=True,
+                                        deferred=deferred)
+        ref = oracle.lightgcn(rp, col, val, x0.numpy(), K)
+        c0, c1 = grid.cols
+        dg = grid.dg
+        q.put((rank, grid.F, grid.R, grid.f, grid.r, whole.numpy(), ref,
+               local.numpy(), ref[dg.row_begin:dg.row_end, c0:c1], dg.recv_rows()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,K,d,F,exchange,deferred", [
+    (2, 3, 64, None, "auto", False),       # F = 2: no exchange at all
+    (4, 3, 64, None, "auto", True),        # 2 feature groups x 2 row shards (p2p in group)
+    (4, 2, 64, 2, "allgather", False),
+    (4, 3, 128, None, "auto", True),       # F = 4
+    (4, 3, 64, 1, "auto", True),           # plain row shards through the grid
+    (3, 3, 96, 3, "auto", False)])
+def test_rank_grid_matches_single_device(world, K, d, F, exchange, deferred):
+    """Feature groups x row shards: every rank's column block of its rows, and the gathered
+    [N, d] table, bit-identical to the single-device oracle propagation."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_grid_worker, args=(r, world, port, K, d, F, exchange, deferred,
+                                                    q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want_F = feature_groups_for(world, d, F)
+    cells = set()
+    for rank, gF, gR, f, r, whole, ref, local, ref_local, recv in res:
+        assert (gF, gR) == (want_F, world // want_F) and rank == r * gF + f
+        cells.add((f, r))
+        np.testing.assert_array_equal(whole.view(np.uint32), ref.view(np.uint32))
+        np.testing.assert_array_equal(local.view(np.uint32), ref_local.view(np.uint32))
+        if gR == 1:
+            assert recv == 0
+    assert len(cells) == world
+
+
+def test_feature_groups_for():
+    assert feature_groups_for(2, 64) == 2 and feature_groups_for(8, 64) == 2
+    assert feature_groups_for(8, 128) == 4 and feature_groups_for(3, 64) == 1
+    assert feature_groups_for(4, 48) == 1            # d % 32 != 0: one group
+    assert feature_groups_for(4, 128, 2) == 2
+    with pytest.raises(ValueError):
+        feature_groups_for(4, 64, 4)                 # only 2 slices
+    with pytest.raises(ValueError):
+        feature_groups_for(6, 128, 4)                # does not divide the world
 
 
 def test_partition_bounds_balance_nnz():

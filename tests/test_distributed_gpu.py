@@ -93,6 +93,20 @@ def _work(rank, world, port, kind, exchange, q):
                 q.put((rank, mine.cpu().numpy(), emb1.detach()[dg.row_begin:dg.row_end].cpu().numpy(),
                        dg.exchange_mode))
                 return
+            if kind == "lightgcn_grid_tiled":
+                # 2 feature groups x 1 row shard: each rank propagates 32 of the 64 columns of
+                # every row, no exchange; gathered back to the full table
+                from src.ops import functional as F
+                from src.ops.distributed import RankGrid, lightgcn_propagate_grid
+                grid = RankGrid(full, rank, world, dev, 64)
+                assert (grid.F, grid.R) == (2, 1)
+                xc = grid.x0_table(m._initial_table())
+                assert xc.shape[1] == 32 and F.tiled_plan_for(grid.dg.shard, xc) is not None
+                mine = lightgcn_propagate_grid(grid, xc, 3, gather_output=True)
+                u, i = m(full.to(dev))
+                ref = torch.cat([u, i])
+                q.put((rank, mine.cpu().numpy(), ref.cpu().numpy(), "none"))
+                return
             if kind == "lightgcn":
                 mine = lightgcn_propagate_dist(dg, x0p, 3, overlap_chunks=3)
             elif kind.endswith("_tiled"):
@@ -122,6 +136,7 @@ def _work(rank, world, port, kind, exchange, q):
 
 @pytest.mark.parametrize("kind,exchange", [("lightgcn", "p2p"), ("lightgcn", "allgather"),
                                            ("lightgcn_tiled", "p2p"),
+                                           ("lightgcn_grid_tiled", "auto"),
                                            ("lightgcn_d128_tiled", "p2p"),
                                            ("ngcf_gs", "auto"), ("gat", "auto"),
                                            ("train", "auto")])

@@ -69,13 +69,20 @@ def zipf_ids(rng, n: int, count: int, a: float, chunk: int = 1 << 26) -> np.ndar
     return out
 
 
-def powerlaw_graph(n_users, n_items, n_pairs, a, seed, threads=16):
+def powerlaw_graph(n_users, n_items, n_pairs, a, seed, threads=16, device=None):
+    """device: build the operand in HBM (CsrGraph.from_interactions_device, bit-identical to
+    the host builder) and keep only the pair arrays on the host — the host builder's sort
+    buffers for 1B pairs are tens of GB of host memory."""
     rng = np.random.default_rng(seed)
     u = zipf_ids(rng, n_users, n_pairs, a)
     i = zipf_ids(rng, n_items, n_pairs, a)
     # min degree >= 1 (the reference's dense GAT turns an isolated node into all-NaN)
     u = np.concatenate([u, np.arange(n_users), rng.integers(0, n_users, n_items)])
     i = np.concatenate([i, rng.integers(0, n_items, n_users), np.arange(n_items)])
+    print(f"[bench_configs] {u.size} pairs sampled", file=sys.stderr, flush=True)
+    if device is not None:
+        return CsrGraph.from_interactions_device(u, i, n_users, n_items, binary=True,
+                                                 device=device)
     return CsrGraph.from_interactions(u, i, n_users, n_items, binary=True, n_threads=threads)
 
 
@@ -298,9 +305,11 @@ def main(argv=None):
         if 5 in a.configs:
             t0 = time.time()
             shape = (10_000_000, 10_000_000, 1_000_000_000) if a.g1b else (2_000_000, 2_000_000, 50_000_000)
-            g = powerlaw_graph(*shape, 0.9, 0, threads)
+            g = powerlaw_graph(*shape, 0.9, 0, threads, device=device if a.g1b else None)
             build_s = time.time() - t0
-            deg = (g.row_ptr[1:] - g.row_ptr[:-1]).numpy()
+            print(f"[bench_configs] operand built: {g.nnz} nnz in {build_s:.1f} s",
+                  file=sys.stderr, flush=True)
+            deg = (g.row_ptr[1:] - g.row_ptr[:-1]).cpu().numpy()
             torch.manual_seed(0)
             m = GAT(shape[0], shape[1], 64, 3, 4, 0.1, 0.2, 0.1).to(device).eval()
             dg = DistributedGraph(g, rank, world, device)
