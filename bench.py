@@ -164,9 +164,18 @@ def hop_bytes(nnz: int, rows: int, src: int, d: int, K: int, world: int,
     return out
 
 
+def _code_only(src: str) -> str:
+    """C/C++ source without comments and blank lines: a comment edit keeps the kernel key."""
+    import re
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    lines = (re.sub(r"//.*$", "", ln).rstrip() for ln in src.splitlines())
+    return "\n".join(ln for ln in lines if ln)
+
+
 def kernel_key(tiled_plan) -> str:
     """Identity of the hop kernel a PMC summary was measured on: SHA-256 of the kernel
-    sources that build it and of the plan parameters the launch uses. A summary whose key
+    sources that build it (code only, comments stripped) and of the plan parameters the
+    launch uses. A summary whose key
     differs from the running build is never reported (traffic: null)."""
     import hashlib
     h = hashlib.sha256()
@@ -174,7 +183,7 @@ def kernel_key(tiled_plan) -> str:
     files = ["common.h", "tiled.hip"] if tiled_plan is not None else ["common.h", "gather.h",
                                                                       "spmm.hip"]
     for f in files + ["../../include/gnnrec.h"]:
-        h.update((csrc / f).read_bytes())
+        h.update(_code_only((csrc / f).read_text()).encode())
     if tiled_plan is not None:
         h.update(json.dumps({k: tiled_plan[k] for k in sorted(tiled_plan)
                              if isinstance(tiled_plan[k], (int, float, str))},

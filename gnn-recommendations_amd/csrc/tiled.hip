@@ -4,8 +4,8 @@
 // (baselines/lightgcn.py:88,178) with y[r] = fmaf chain over the row's neighbours in ascending
 // column order from +0 — but a different schedule. The row-parallel hop gathers every
 // neighbour row from beyond L2 (G100M: 16x the compulsory bytes). Here one persistent
-// 1024-thread workgroup per CU owns R destination rows per pass with fp32 accumulators in
-// LDS, and its 16 waves walk the rows' edges PANEL BY PANEL in ascending source column
+// 512-thread workgroup per CU owns R destination rows per pass with fp32 accumulators in
+// LDS, and its 8 waves walk the rows' edges PANEL BY PANEL in ascending source column
 // (a step = one panel; a workgroup barrier between steps, so a row may move to another slot
 // stream from one step to the next without reordering its chain). The workgroups of a
 // blockIdx % 8 group (one XCD under round-robin placement — speed only, never correctness)
@@ -31,8 +31,8 @@
 // 64-bit chain mask = slot t of stream g continues slot t-1's row (take the register value);
 // SALU spreads the step's bits to lane masks. A chunk is applied as two groups of 4 steps
 // (reads of a group precede its writes; a row is at most one run of slots per group and
-// stream). Pipeline per wave: chunk c+2's slot loads, chunk c+1's 8 gathers and chunk c's LDS
-// chain in flight.
+// stream). Pipeline per wave: chunk c+5's slot loads, chunk c+2's 8 gathers and chunk c's LDS
+// chain in flight (plan ring kPlanAhead = 5, gather ring kGatherAhead = 2).
 #include <algorithm>
 #include <atomic>
 #include <mutex>
