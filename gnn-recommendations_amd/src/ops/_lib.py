@@ -58,6 +58,9 @@ _SIGNATURES = {
     "gnnrec_tiled_plan_build": [_p, _p, _p, _i64, _i32, _i32, _i32, _i32, _p, _p, _p],
     "gnnrec_tiled_plan_emit": [_p, _p, _p, _p, _p, _p],
     "gnnrec_tiled_plan_free": [_p],
+    "gnnrec_tiled_plan_device_scratch_words": [_i64, _i32],
+    "gnnrec_tiled_plan_device": [_p, _p, _p, _i64, _i32, _i32, _i32, _i64, _p, _i32, _p, _p, _p,
+                                 _p, _p, _p, _p, _p],
     "gnnrec_spmm_tiled_supported": [_i32, _i32],
     "gnnrec_spmm_tiled_f32": [_p, _p, _p, _p, _p, _i64, _i32, _p, _i64, _i64, _p, _i64,
                               _i64, _i32, _i32, _p, _i64, _p, _i64, _f32, _p, _i64, _p, _i32, _p],
@@ -94,7 +97,7 @@ _SIGNATURES = {
                              _f32, _p, _p],
 }
 _RESTYPES = {"gnnrec_version": C.c_char_p, "gnnrec_last_error": C.c_char_p,
-             "gnnrec_abi_version": C.c_int}
+             "gnnrec_abi_version": C.c_int, "gnnrec_tiled_plan_device_scratch_words": C.c_int64}
 
 EXPORTED = tuple(_SIGNATURES)
 

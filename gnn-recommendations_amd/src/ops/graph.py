@@ -25,6 +25,13 @@ import torch
 
 from . import _lib
 
+# where a device-resident graph's column-ordered plan is built ("device" | "host"; the same
+# arrays either way)
+TILED_PLANNER = "device"
+# gnnrec_tiled_plan_device error words: 1 negative column (the host planner's EINVAL),
+# 2 scratch too small, 3 a run longer than 2^21, 4 count / emit disagree
+_DEVICE_PLAN_ERRORS = {1: ValueError}
+
 
 def _np(t: torch.Tensor) -> np.ndarray:
     return t.detach().cpu().numpy()
@@ -365,55 +372,117 @@ class CsrGraph:
         return self._plans["max_degree"]
 
     def tiled_plan(self, rows_per_block: int = 1117, panel: int = 49152,
-                   sub_panel: int = 4096) -> dict:
+                   sub_panel: int = 4096, planner: Optional[str] = None) -> dict:
         """Column-ordered re-layout of this operand for gnnrec_spmm_tiled_f32 (DESIGN.md
         §3.1c), cached; one plan serves every x table (any d that is a multiple of 32, any row
-        stride up to TILED_MAX_LDX, any size): built once on the host from the CSR
-        (gnnrec_tiled_plan_build/emit), uploaded to this graph's device. Defaults from the
-        G100M sweep (profiles/r02/tiled_sweep.jsonl): 1117 rows per block fill the LDS with
-        32-feature accumulators in 14 full passes, 48K-column panels (steps: a workgroup
-        barrier each, which keeps its waves on nearby columns), each stream's slots in
-        ascending 4K-column sub-panels inside a step (0: no sub-panel order)."""
+        stride up to TILED_MAX_LDX, any size). planner: "device" builds it in HBM from the
+        device CSR (gnnrec_tiled_plan_device, the default for a graph on a GPU), "host" on the
+        host from the CSR (gnnrec_tiled_plan_build/emit) and uploads it; both give the same
+        arrays bit for bit (tests/test_tiled_plan_gpu.py). Defaults from the G100M sweeps
+        (profiles/r02/tiled_sweep.jsonl, profiles/r03/sweep_R_*.jsonl): 1117 rows per block
+        fill the LDS with 32-feature accumulators in 14 full passes, 48K-column panels
+        (steps: a workgroup barrier each, which keeps its waves on nearby columns), each
+        stream's slots in ascending 4K-column sub-panels inside a step (0: no sub-panel
+        order)."""
         key = ("tiled", int(rows_per_block), int(panel), int(sub_panel))
         if key not in self._plans:
-            import ctypes as C
-            L = _lib.lib()
-            rp = np.ascontiguousarray(_np(self.row_ptr), dtype=np.int64)
-            col = np.ascontiguousarray(_np(self.col), dtype=np.int32)
-            val = np.ascontiguousarray(_np(self.val), dtype=np.float32)
-            h, n_chunks, n_blocks = C.c_void_p(), C.c_int64(), C.c_int64()
-            _lib.check(L.gnnrec_tiled_plan_build(rp.ctypes.data, col.ctypes.data, val.ctypes.data,
-                                                 self.n_rows, int(rows_per_block), int(panel),
-                                                 int(sub_panel), 0, C.byref(h),
-                                                 C.byref(n_chunks),
-                                                 C.byref(n_blocks)), "gnnrec_tiled_plan_build")
-            nb = n_blocks.value
-            chunks = n_chunks.value + _lib.TILED_TAIL          # + tail chunks (prefetch)
-            slot = np.empty(chunks * _lib.TILED_CHUNK, np.uint32)
-            v = np.empty(chunks * _lib.TILED_CHUNK, np.float32)
-            hdr = np.empty(chunks * _lib.TILED_HDR_WORDS, np.uint32)
-            wave_ptr = np.empty(nb * _lib.TILED_WAVES + 1, np.int64)
-            n_steps = np.empty(max(nb, 1), np.int32)
-            try:
-                _lib.check(L.gnnrec_tiled_plan_emit(h, slot.ctypes.data, v.ctypes.data,
-                                                    hdr.ctypes.data, wave_ptr.ctypes.data,
-                                                    n_steps.ctypes.data),
-                           "gnnrec_tiled_plan_emit")
-            finally:
-                L.gnnrec_tiled_plan_free(h)
-            dev = self.device
-            self._plans[key] = dict(
-                slot=torch.from_numpy(slot.view(np.int32)).to(dev),
-                val=torch.from_numpy(v).to(dev),
-                hdr=torch.from_numpy(hdr.view(np.int32)).to(dev),
-                wave_ptr=torch.from_numpy(wave_ptr).to(dev),
-                n_steps=torch.from_numpy(n_steps).to(dev),
-                n_blocks=nb, rows_per_block=int(rows_per_block),
-                panel=min(int(panel), _lib.TILED_MAX_PANEL),
-                sub_panel=int(sub_panel), n_chunks=n_chunks.value,
-                n_slots=n_chunks.value * _lib.TILED_CHUNK,
-                sync=torch.zeros(_lib.TILED_SYNC_WORDS, dtype=torch.int32, device=dev))
+            if planner is None:
+                planner = TILED_PLANNER if self.device.type == "cuda" else "host"
+            if planner == "device":
+                plan = self._tiled_plan_device(int(rows_per_block), int(panel), int(sub_panel))
+            elif planner == "host":
+                plan = self._tiled_plan_host(int(rows_per_block), int(panel), int(sub_panel))
+            else:
+                raise ValueError(f"unknown planner {planner!r}")
+            plan.update(rows_per_block=int(rows_per_block),
+                        panel=min(int(panel), _lib.TILED_MAX_PANEL), sub_panel=int(sub_panel),
+                        n_slots=plan["n_chunks"] * _lib.TILED_CHUNK,
+                        sync=torch.zeros(_lib.TILED_SYNC_WORDS, dtype=torch.int32,
+                                         device=self.device))
+            self._plans[key] = plan
         return self._plans[key]
+
+    def _tiled_plan_host(self, R: int, panel: int, sub_panel: int) -> dict:
+        import ctypes as C
+        L = _lib.lib()
+        rp = np.ascontiguousarray(_np(self.row_ptr), dtype=np.int64)
+        col = np.ascontiguousarray(_np(self.col), dtype=np.int32)
+        val = np.ascontiguousarray(_np(self.val), dtype=np.float32)
+        h, n_chunks, n_blocks = C.c_void_p(), C.c_int64(), C.c_int64()
+        _lib.check(L.gnnrec_tiled_plan_build(rp.ctypes.data, col.ctypes.data, val.ctypes.data,
+                                             self.n_rows, R, panel, sub_panel, 0, C.byref(h),
+                                             C.byref(n_chunks), C.byref(n_blocks)),
+                   "gnnrec_tiled_plan_build")
+        nb = n_blocks.value
+        chunks = n_chunks.value + _lib.TILED_TAIL          # + tail chunks (prefetch)
+        slot = np.empty(chunks * _lib.TILED_CHUNK, np.uint32)
+        v = np.empty(chunks * _lib.TILED_CHUNK, np.float32)
+        hdr = np.empty(chunks * _lib.TILED_HDR_WORDS, np.uint32)
+        wave_ptr = np.empty(nb * _lib.TILED_WAVES + 1, np.int64)
+        n_steps = np.empty(max(nb, 1), np.int32)
+        try:
+            _lib.check(L.gnnrec_tiled_plan_emit(h, slot.ctypes.data, v.ctypes.data,
+                                                hdr.ctypes.data, wave_ptr.ctypes.data,
+                                                n_steps.ctypes.data),
+                       "gnnrec_tiled_plan_emit")
+        finally:
+            L.gnnrec_tiled_plan_free(h)
+        dev = self.device
+        return dict(slot=torch.from_numpy(slot.view(np.int32)).to(dev),
+                    val=torch.from_numpy(v).to(dev),
+                    hdr=torch.from_numpy(hdr.view(np.int32)).to(dev),
+                    wave_ptr=torch.from_numpy(wave_ptr).to(dev),
+                    n_steps=torch.from_numpy(n_steps).to(dev),
+                    n_blocks=nb, n_chunks=n_chunks.value)
+
+    def _tiled_plan_device(self, R: int, panel: int, sub_panel: int) -> dict:
+        """gnnrec_tiled_plan_device: a counting pass, the chunk offsets by a device cumsum,
+        the emitting pass (two device reads: the chunk total and the error word)."""
+        dev = self.device
+        if dev.type != "cuda":
+            raise ValueError("the device planner needs the graph on a ROCm device")
+        L = _lib.lib()
+        n, W = self.n_rows, _lib.TILED_WAVES
+        nb = -(-n // R)
+        rp = self.row_ptr
+        starts = torch.arange(nb, dtype=torch.int64, device=dev) * R
+        bnnz = rp[torch.clamp(starts + R, max=n)] - rp[starts]
+        max_nnz = int(bnnz.max()) if nb else 0
+        if max_nnz >= (1 << 31) - 1:
+            raise ValueError("tiled plan: a block holds more than 2^31 edges")
+        wg = max(1, min(nb, torch.cuda.get_device_properties(dev).multi_processor_count))
+        scratch = torch.empty(max(1, L.gnnrec_tiled_plan_device_scratch_words(max_nnz, wg)),
+                              dtype=torch.int64, device=dev)
+        chunks = torch.zeros(max(1, nb * W), dtype=torch.int64, device=dev)
+        n_steps = torch.zeros(max(nb, 1), dtype=torch.int32, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        stream = _lib.stream_of(dev)
+        ptr = _lib.ptr
+        args = (ptr(rp), ptr(self.col), ptr(self.val), n, R, panel, sub_panel, max_nnz,
+                ptr(scratch), wg)
+        _lib.check(L.gnnrec_tiled_plan_device(*args, ptr(chunks), ptr(n_steps), None, None, None,
+                                              None, ptr(err), stream),
+                   "gnnrec_tiled_plan_device (count)")
+        wave_ptr = torch.zeros(nb * W + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(chunks[:nb * W], 0, out=wave_ptr[1:])
+        n_chunks, code = int(wave_ptr[-1]), int(err)
+        if code:
+            raise _DEVICE_PLAN_ERRORS.get(code, RuntimeError)(
+                f"gnnrec_tiled_plan_device (count) failed: error {code}")
+        total = n_chunks + _lib.TILED_TAIL
+        slot = torch.empty(total * _lib.TILED_CHUNK, dtype=torch.int32, device=dev)
+        v = torch.empty(total * _lib.TILED_CHUNK, dtype=torch.float32, device=dev)
+        hdr = torch.empty(total * _lib.TILED_HDR_WORDS, dtype=torch.int32, device=dev)
+        _lib.check(L.gnnrec_tiled_plan_device(*args, None, None, ptr(wave_ptr), ptr(slot), ptr(v),
+                                              ptr(hdr), ptr(err), stream),
+                   "gnnrec_tiled_plan_device (emit)")
+        code = int(err)
+        if code:
+            raise _DEVICE_PLAN_ERRORS.get(code, RuntimeError)(
+                f"gnnrec_tiled_plan_device (emit) failed: error {code}")
+        del scratch
+        return dict(slot=slot, val=v, hdr=hdr, wave_ptr=wave_ptr, n_steps=n_steps,
+                    n_blocks=nb, n_chunks=n_chunks)
 
     def heavy_plan(self, threshold: int, seg_len: int):
         """Degree buckets for the skew-tolerant kernels (cached): rows with more than

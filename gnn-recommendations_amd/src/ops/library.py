@@ -74,6 +74,20 @@ def graph_of(row_ptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, n_cols
     return g
 
 
+def _hold(ctx, row_ptr, col, val, n_cols) -> None:
+    """Keep the forward's CsrGraph (its cached transpose and plans) alive until backward: a
+    model called with a temporary graph (`m(g.to(dev))`) drops it before backward, which
+    would then rebuild it from the raw tensors (graph_of's warning)."""
+    ctx.graph = None
+    if not torch.compiler.is_compiling():
+        ctx.graph = _LIVE.get(_key(row_ptr, col, val, n_cols))
+
+
+def _revive(ctx) -> None:
+    if getattr(ctx, "graph", None) is not None:
+        register(ctx.graph)
+
+
 # ---- gnnrec::spmm -------------------------------------------------------------------------
 @torch.library.custom_op("gnnrec::spmm", mutates_args=(), device_types="cuda")
 def spmm_op(row_ptr: torch.Tensor, col: torch.Tensor, val: torch.Tensor, x: torch.Tensor,
@@ -91,10 +105,12 @@ def _spmm_setup(ctx, inputs, output):
     row_ptr, col, val, _x, n_cols = inputs
     ctx.save_for_backward(row_ptr, col, val)
     ctx.n_cols = n_cols
+    _hold(ctx, row_ptr, col, val, n_cols)
 
 
 def _spmm_backward(ctx, g):
     row_ptr, col, val = ctx.saved_tensors
+    _revive(ctx)
     return None, None, None, torch.ops.gnnrec.spmm_t(row_ptr, col, val, g, ctx.n_cols), None
 
 
@@ -139,10 +155,12 @@ def _lightgcn_setup(ctx, inputs, output):
     row_ptr, col, val, _x0, n_cols, n_layers, _need = inputs
     ctx.save_for_backward(row_ptr, col, val)
     ctx.n_cols, ctx.n_layers = n_cols, n_layers
+    _hold(ctx, row_ptr, col, val, n_cols)
 
 
 def _lightgcn_backward(ctx, g):
     row_ptr, col, val = ctx.saved_tensors
+    _revive(ctx)
     gx = torch.ops.gnnrec.lightgcn_propagate_t(row_ptr, col, val, g, ctx.n_cols, ctx.n_layers)
     return None, None, None, gx, None, None, None
 

@@ -183,6 +183,23 @@ int gnnrec_tiled_plan_emit(void* plan, uint32_t* slot, float* val, uint32_t* hdr
                            int64_t* wave_ptr, int32_t* n_steps);
 int gnnrec_tiled_plan_free(void* plan);
 
+/* The same plan built on the device from a device-resident CSR (bit-identical arrays).
+ * Two calls on `stream`: the COUNT pass (wave_ptr == NULL) writes chunks[n_blocks *
+ * GNNREC_TILED_WAVES] (chunks per block and wave) and n_steps[n_blocks]; the caller forms
+ * wave_ptr = [0, cumsum(chunks)] and sizes slot / val_out / hdr for wave_ptr[last] +
+ * GNNREC_TILED_TAIL chunks; the EMIT pass (wave_ptr != NULL) writes them, tail chunks
+ * included. scratch: gnnrec_tiled_plan_device_scratch_words(max_block_nnz, workgroups)
+ * uint64 words, max_block_nnz = the largest row_ptr[min(n_rows, (b+1) R)] - row_ptr[b R];
+ * err: one device int32, zeroed by the caller, non-zero after a failed pass (1 negative
+ * column, 2 scratch too small, 3 a run longer than 2^21, 4 count / emit mismatch). */
+int64_t gnnrec_tiled_plan_device_scratch_words(int64_t max_block_nnz, int32_t workgroups);
+int gnnrec_tiled_plan_device(const int64_t* row_ptr, const int32_t* col, const float* val,
+                             int64_t n_rows, int32_t rows_per_block, int32_t panel,
+                             int32_t sub_panel, int64_t max_block_nnz, uint64_t* scratch,
+                             int32_t workgroups, int64_t* chunks, int32_t* n_steps,
+                             const int64_t* wave_ptr, uint32_t* slot, float* val_out,
+                             uint32_t* hdr, int32_t* err, gnnrec_stream_t stream);
+
 /* 1 when `device` grants gnnrec_spmm_tiled_f32 the dynamic LDS of `rows_per_block` rows
  * ((rows_per_block + 1) * 128 B; the attribute is set once per device), else 0 — a caller
  * then keeps the row-parallel hop (gnnrec_spmm_csr_masked_f32). */

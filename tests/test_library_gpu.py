@@ -97,3 +97,21 @@ def test_compile_traces_the_op(cuda):
     eager = f(x)
     compiled = torch.compile(f, backend="aot_eager", fullgraph=True)(x)
     assert torch.equal(eager, compiled)
+
+
+def test_temporary_graph_survives_until_backward(cuda):
+    """m(g.to(dev)) drops the device graph before backward: the op's autograd context keeps
+    it (and its cached transpose / plans), so backward finds it instead of rebuilding one
+    from the raw tensors (graph_of's RuntimeWarning)."""
+    import warnings
+    _, g_host, nu, ni = _graph(cuda, 4)
+    torch.manual_seed(0)
+    m = LightGCN(nu, ni, embedding_dim=64, n_layers=3, init_scale=0.1).to(cuda)
+    n = NGCF(nu, ni, 64, [64, 64, 64], 0.1, 0.1).to(cuda).train()
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", RuntimeWarning)
+        u, i = m(g_host.to(cuda))
+        (u.sum() + i.sum()).backward()
+        u, i = n(g_host.to(cuda))
+        u.sum().backward()
+    assert m.user_embedding.weight.grad is not None

@@ -1,0 +1,109 @@
+"""The device planner (gnnrec_tiled_plan_device, csrc/tiled_plan.hip) against the host
+planner (gnnrec_tiled_plan_build/emit): the same slot words, values, headers, chunk offsets
+and step counts, bit for bit — on uniform and power-law graphs, with and without the
+sub-panel order, many small panels (many steps, empty panels skipped), short blocks, rows
+longer than a panel's share, and at full G100M size; and a hop through each plan gives the
+same bits."""
+import numpy as np
+import pytest
+import torch
+
+from src.ops import CsrGraph, functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _uniform(nu, ni, n, seed):
+    rng = np.random.default_rng(seed)
+    return CsrGraph.from_interactions(rng.integers(0, nu, n), rng.integers(0, ni, n), nu, ni,
+                                      binary=True)
+
+
+def _powerlaw(nu, ni, n, seed):
+    rng = np.random.default_rng(seed)
+    u = np.concatenate([rng.integers(0, nu, n), np.zeros(3000, np.int64)])   # a 3000-item user
+    i = np.concatenate([np.minimum(rng.zipf(1.3, n) - 1, ni - 1), np.arange(3000) % ni])
+    return CsrGraph.from_interactions(u, i, nu, ni, binary=True)
+
+
+def _same(a, b):
+    for k in ("slot", "val", "hdr", "wave_ptr", "n_steps"):
+        x, y = a[k].cpu(), b[k].cpu()
+        assert x.shape == y.shape, k
+        assert torch.equal(x.view(torch.int32) if x.dtype == torch.float32 else x,
+                           y.view(torch.int32) if y.dtype == torch.float32 else y), k
+    for k in ("n_blocks", "n_chunks", "n_slots"):
+        assert a[k] == b[k], k
+
+
+@pytest.mark.parametrize("kind,R,panel,sub", [
+    ("uniform", 1117, 49152, 4096), ("uniform", 300, 4096, 512), ("uniform", 64, 1000, 0),
+    ("uniform", 1279, 2048, 100), ("powerlaw", 700, 8192, 1024), ("powerlaw", 1, 4096, 256),
+    ("powerlaw", 513, 300, 0)])
+def test_device_plan_equals_host_plan(cuda, kind, R, panel, sub):
+    g = (_uniform(20000, 15000, 600000, 3) if kind == "uniform"
+         else _powerlaw(20000, 15000, 400000, 4))
+    gd = g.to(cuda)
+    dev = gd._tiled_plan_device(R, panel, sub)
+    host = gd._tiled_plan_host(R, panel, sub)
+    for p in (dev, host):
+        p["n_slots"] = p["n_chunks"] * 64
+    _same(dev, host)
+
+
+def test_device_plan_edge_cases(cuda):
+    # empty rows at both ends and a trailing short block
+    rp = torch.tensor([0, 0, 3, 3, 7, 7, 7], dtype=torch.int64)
+    col = torch.tensor([0, 5, 9, 1, 2, 3, 8], dtype=torch.int32)
+    val = torch.arange(1, 8, dtype=torch.float32)
+    g = CsrGraph(rp, col, val, (6, 10)).to(cuda)
+    for R in (1, 2, 4, 6):
+        for panel, sub in ((4, 0), (4, 2), (100, 3)):
+            dev = g._tiled_plan_device(R, panel, sub)
+            host = g._tiled_plan_host(R, panel, sub)
+            for p in (dev, host):
+                p["n_slots"] = p["n_chunks"] * 64
+            _same(dev, host)
+    bad = CsrGraph(rp, torch.tensor([0, 5, -1, 1, 2, 3, 8], dtype=torch.int32), val,
+                   (6, 10)).to(cuda)
+    with pytest.raises(ValueError):
+        bad._tiled_plan_device(2, 4, 0)
+    with pytest.raises(ValueError):
+        bad._tiled_plan_host(2, 4, 0)
+
+
+def test_hop_through_device_plan_bit_exact(cuda):
+    g = _uniform(60000, 50000, 3_000_000, 5)
+    gd = g.to(cuda)
+    x = torch.randn(g.shape[0], 64, device=cuda) * 0.1
+    ref = torch.empty_like(x)
+    F.TILED_HOP, was = False, F.TILED_HOP
+    try:
+        F.spmm_into(gd, x, ref)
+    finally:
+        F.TILED_HOP = was
+    for planner in ("device", "host"):
+        gd._plans.pop(("tiled", 700, 8192, 1024), None)
+        plan = gd.tiled_plan(rows_per_block=700, panel=8192, sub_panel=1024, planner=planner)
+        y = torch.empty_like(x)
+        F.spmm_tiled_into(gd, x, y, plan)
+        assert torch.equal(y.view(torch.int32), ref.view(torch.int32)), planner
+
+
+def test_device_plan_equals_host_plan_g100m(cuda):
+    import time
+    import bench
+    g = bench.build_graph(1_000_000, 1_000_000, 100_000_000, 0, 16)
+    gd = g.to(cuda)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    dev = gd._tiled_plan_device(1117, 49152, 4096)
+    torch.cuda.synchronize()
+    t_dev = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    host = gd._tiled_plan_host(1117, 49152, 4096)
+    t_host = time.perf_counter() - t0
+    print(f"\n[plan G100M] device {t_dev:.3f} s, host {t_host:.3f} s")
+    for p in (dev, host):
+        p["n_slots"] = p["n_chunks"] * 64
+    _same(dev, host)
