@@ -27,7 +27,7 @@ from . import _lib
 
 # where a device-resident graph's column-ordered plan is built ("device" | "host"; the same
 # arrays either way)
-TILED_PLANNER = "device"
+TILED_PLANNER = "host"
 # gnnrec_tiled_plan_device error words: 1 negative column (the host planner's EINVAL),
 # 2 scratch too small, 3 a run longer than 2^21, 4 count / emit disagree
 _DEVICE_PLAN_ERRORS = {1: ValueError}
