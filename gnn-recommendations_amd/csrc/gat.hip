@@ -238,25 +238,12 @@ __device__ __forceinline__ void gat_shared_rows16(const GatParams& p, int64_t r,
 // float4 of x per neighbour and keep H heads' online-softmax state for it (the generic
 // kernel would spread the heads over H times as many lanes that all load the same bytes).
 // Per (row, head, feature) the arithmetic is the generic kernel's, step for step.
+// Neighbours [beg, end) of row r in shared-row mode (the online-softmax state of H heads).
 template <int O, int H, int CH>
-__global__ __launch_bounds__(kBlock) void gat_shared_kernel(GatParams p) {
+__device__ __forceinline__ void gat_shared_range(const GatParams& p, int64_t r, int64_t beg,
+                                                 int64_t end, int gl, const float (&ss)[H],
+                                                 float (&m)[H], float (&l)[H], float4 (&a)[H]) {
   constexpr int GROUP = O / 4;
-  constexpr int RPW = 64 / GROUP;
-  const int lane = threadIdx.x & 63;
-  const int gl = lane % GROUP;
-  const int64_t r = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
-  if (r >= p.A.n_rows) return;
-  const int64_t beg = p.A.row_ptr[r], end = p.A.row_ptr[r + 1];
-  if (p.max_row_len > 0 && end - beg > p.max_row_len) return;  // heavy row: split path
-  float ss[H], m[H], l[H];
-  float4 a[H];
-#pragma unroll
-  for (int h = 0; h < H; ++h) {
-    ss[h] = p.s_self[r * p.ld_ss + h];
-    m[h] = -INFINITY;
-    l[h] = 0.f;
-    a[h] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
   static_assert(CH == kSoftBlock, "one softmax block per gather step (same blocks as gat_kernel)");
   if constexpr (GROUP == 16 && H == 4 && CH == 8) {
     gat_shared_rows16(p, r, beg, end, gl, ss, m, l, a);
@@ -293,6 +280,28 @@ __global__ __launch_bounds__(kBlock) void gat_shared_kernel(GatParams p) {
     }
   }
   }
+}
+
+template <int O, int H, int CH>
+__global__ __launch_bounds__(kBlock) void gat_shared_kernel(GatParams p) {
+  constexpr int GROUP = O / 4;
+  constexpr int RPW = 64 / GROUP;
+  const int lane = threadIdx.x & 63;
+  const int gl = lane % GROUP;
+  const int64_t r = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
+  if (r >= p.A.n_rows) return;
+  const int64_t beg = p.A.row_ptr[r], end = p.A.row_ptr[r + 1];
+  if (p.max_row_len > 0 && end - beg > p.max_row_len) return;  // heavy row: split path
+  float ss[H], m[H], l[H];
+  float4 a[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    ss[h] = p.s_self[r * p.ld_ss + h];
+    m[h] = -INFINITY;
+    l[h] = 0.f;
+    a[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  gat_shared_range<O, H, CH>(p, r, beg, end, gl, ss, m, l, a);
 #pragma unroll
   for (int h = 0; h < H; ++h)
     st4(p.out + r * p.ldo + h * O + 4 * gl,
@@ -328,6 +337,39 @@ __global__ __launch_bounds__(kBlock) void gat_partial_kernel(GatParams p, GatSpl
     float* ml = sp.work + sp.n_seg * F;
     ml[sg * p.heads + gl / hl] = m;
     ml[sp.n_seg * p.heads + sg * p.heads + gl / hl] = l;
+  }
+}
+
+// Heavy rows, pass 1 in shared-row mode: O/4 lanes per segment load each neighbour's x row
+// ONCE for all H heads (gat_partial_kernel<H*O> would load it H times, one head per lane
+// group); the partials have gat_partial_kernel's layout, so gat_merge_kernel<H*O> finishes.
+template <int O, int H, int CH>
+__global__ __launch_bounds__(kBlock) void gat_shared_partial_kernel(GatParams p, GatSplit sp) {
+  constexpr int GROUP = O / 4;
+  constexpr int RPW = 64 / GROUP;
+  const int lane = threadIdx.x & 63;
+  const int gl = lane % GROUP;
+  const int64_t sg = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
+  if (sg >= sp.n_seg) return;
+  const int64_t r = sp.seg_row[sg];
+  float ss[H], m[H], l[H];
+  float4 a[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    ss[h] = p.s_self[r * p.ld_ss + h];
+    m[h] = -INFINITY;
+    l[h] = 0.f;
+    a[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  gat_shared_range<O, H, CH>(p, r, sp.seg_beg[sg], sp.seg_end[sg], gl, ss, m, l, a);
+  float* ml = sp.work + sp.n_seg * (H * O);
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    st4(sp.work + sg * (H * O) + h * O + 4 * gl, a[h]);
+    if (gl == 0) {
+      ml[sg * H + h] = m[h];
+      ml[sp.n_seg * H + sg * H + h] = l[h];
+    }
   }
 }
 
@@ -459,6 +501,22 @@ extern "C" int gnnrec_gat_heavy_f32(const int32_t* col, const int64_t* seg_row,
   GatSplit sp{seg_row, seg_beg, seg_end, n_seg, heavy_rows, heavy_seg_ptr, n_heavy, work};
   hipStream_t s = as_hip(stream);
   auto g = [&](int64_t n, int f) { return dim3((unsigned)ceil_div(n, (64 / (f / 4)) * (kBlock / 64))); };
+  if (head_stride == 0 && heads == 4 && (o_dim == 16 || o_dim == 32 || o_dim == 64) &&
+      aligned16(s_neigh) && !(ld_sn & 3)) {
+    // shared rows: one x load per neighbour for the 4 heads, then the generic merge
+    switch (o_dim) {
+#define GAT_SHARED_HEAVY(OO)                                                                   \
+  case OO:                                                                                     \
+    hipLaunchKernelGGL((gat_shared_partial_kernel<OO, 4, 8>), g(n_seg, OO), dim3(kBlock), 0, s, \
+                       p, sp);                                                                 \
+    hipLaunchKernelGGL(gat_merge_kernel<4 * OO>, dim3((unsigned)n_heavy), dim3(kBlock), 0, s, \
+                       p, sp);                                                                 \
+    break;
+      GAT_SHARED_HEAVY(16) GAT_SHARED_HEAVY(32) GAT_SHARED_HEAVY(64)
+#undef GAT_SHARED_HEAVY
+    }
+    return check_launch("gat_heavy (shared rows)");
+  }
   switch (F) {
 #define GAT_HEAVY(FF)                                                                          \
   case FF:                                                                                     \

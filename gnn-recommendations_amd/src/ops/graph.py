@@ -486,8 +486,11 @@ class CsrGraph:
 
     def heavy_plan(self, threshold: int, seg_len: int):
         """Degree buckets for the skew-tolerant kernels (cached): rows with more than
-        `threshold` neighbours, cut into `seg_len` segments. Returns None when there are none,
-        else dict(heavy_rows, heavy_seg_ptr, seg_row, seg_beg, seg_end) on this device."""
+        `threshold` neighbours, each cut into ceil(degree / seg_len) segments of EQUAL length
+        (degree-aware: a row of degree D gets segments of D / ceil(D / seg_len) edges, one
+        edge apart at most, instead of full segments and a short last one that would leave
+        its wave's other lanes waiting). Returns None when there are none, else
+        dict(heavy_rows, heavy_seg_ptr, seg_row, seg_beg, seg_end) on this device."""
         key = ("heavy", threshold, seg_len)
         if key not in self._plans:
             rp = self.row_ptr
@@ -496,14 +499,18 @@ class CsrGraph:
             if heavy.numel() == 0:
                 self._plans[key] = None
             else:
-                nseg = (deg[heavy] + seg_len - 1) // seg_len
+                dh = deg[heavy]
+                nseg = (dh + seg_len - 1) // seg_len
                 seg_ptr = torch.zeros(heavy.numel() + 1, dtype=torch.int64, device=rp.device)
                 seg_ptr[1:] = torch.cumsum(nseg, 0)
                 seg_row = torch.repeat_interleave(heavy, nseg)
                 j = torch.arange(int(seg_ptr[-1]), device=rp.device) - torch.repeat_interleave(
                     seg_ptr[:-1], nseg)
-                seg_beg = rp[seg_row] + j * seg_len
-                seg_end = torch.minimum(seg_beg + seg_len, rp[seg_row + 1])
+                D = torch.repeat_interleave(dh, nseg)
+                n = torch.repeat_interleave(nseg, nseg)
+                start = rp[seg_row]
+                seg_beg = start + (j * D) // n
+                seg_end = start + ((j + 1) * D) // n
                 self._plans[key] = dict(heavy_rows=heavy.contiguous(), heavy_seg_ptr=seg_ptr,
                                         seg_row=seg_row.contiguous(), seg_beg=seg_beg.contiguous(),
                                         seg_end=seg_end.contiguous())

@@ -114,3 +114,29 @@ def test_bench_cpu_baseline_leg_checks_parity():
     bad[7, 3] = np.nextafter(bad[7, 3], np.float32(1))
     res = bench.cpu_baseline(g, x0, 3, 300, layers[0], bad)
     assert res["cpu_parity"] is False and res["parity_detail"]["hop1_bit_exact"] is True
+
+
+def test_heavy_plan_equal_segments():
+    """CsrGraph.heavy_plan: every row above the threshold is covered by contiguous segments
+    of equal length (one edge apart at most), none longer than seg_len."""
+    import numpy as np
+    import torch
+    from src.ops import CsrGraph
+    rng = np.random.default_rng(1)
+    u = np.concatenate([rng.integers(0, 500, 20000), np.zeros(2500, np.int64)])
+    i = np.concatenate([np.minimum(rng.zipf(1.3, 20000) - 1, 2999), np.arange(2500)])
+    g = CsrGraph.from_interactions(u, i, 500, 3000, binary=True)
+    rp = g.row_ptr
+    deg = rp[1:] - rp[:-1]
+    for thr, seg in ((200, 100), (64, 64), (1000, 333)):
+        p = g.heavy_plan(thr, seg)
+        assert torch.equal(p["heavy_rows"], torch.nonzero(deg > thr).flatten())
+        sp = p["heavy_seg_ptr"].tolist()
+        for h, r in enumerate(p["heavy_rows"].tolist()):
+            a, b = sp[h], sp[h + 1]
+            assert b - a == -(-int(deg[r]) // seg)
+            assert (p["seg_row"][a:b] == r).all()
+            assert int(p["seg_beg"][a]) == int(rp[r]) and int(p["seg_end"][b - 1]) == int(rp[r + 1])
+            assert torch.equal(p["seg_beg"][a + 1:b], p["seg_end"][a:b - 1])
+            L = p["seg_end"][a:b] - p["seg_beg"][a:b]
+            assert int(L.max()) - int(L.min()) <= 1 and int(L.max()) <= seg
