@@ -680,6 +680,74 @@ void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_
   out.nsteps = step;
 }
 
+// Pinned rows (panel = 0): each row stays in ONE slot stream for the whole pass (LPT of the
+// rows by degree), so no step needs a barrier and a wave pads its streams once per pass
+// instead of once per step; each stream walks its rows' edges in (sub-panel, row) order and
+// the waves keep to nearby columns by that order alone. A chunk's base is its smallest
+// column; false when a chunk's slots span kMaxPanel columns or more (the slot word holds 20
+// bits of offset): the caller then plans with panels.
+bool build_block_pinned(const int64_t* rp, const int32_t* col, const float* val, int64_t n_rows,
+                        int R, int sub_panel, int64_t b, BlockPlan& out) {
+  const int64_t r0 = b * R, r1 = std::min<int64_t>(n_rows, r0 + R);
+  std::vector<Run> runs;
+  for (int64_t r = r0; r < r1; ++r)
+    if (rp[r + 1] > rp[r]) runs.push_back({0, (int32_t)(r - r0), rp[r], (int32_t)(rp[r + 1] - rp[r])});
+  std::vector<const Run*> g;
+  for (const Run& e : runs) g.push_back(&e);
+  std::stable_sort(g.begin(), g.end(), [](const Run* a, const Run* c) { return a->n > c->n; });
+  int64_t load[kVirt] = {};
+  std::vector<const Run*> wl[kVirt];
+  for (const Run* e : g) {
+    int v = 0;
+    for (int q = 1; q < kVirt; ++q)
+      if (load[q] < load[v]) v = q;
+    load[v] += e->n;
+    wl[v].push_back(e);
+  }
+  std::vector<Slot> hs[kGroups];
+  for (int w = 0; w < kTiledWaves; ++w) {
+    size_t n = 0;
+    for (int q = 0; q < kGroups; ++q) {
+      stream_slots(wl[kGroups * w + q], col, sub_panel, hs[q]);
+      n = std::max(n, hs[q].size());
+    }
+    for (int q = 0; q < kGroups; ++q) hs[q].resize(n, Slot{nullptr, 0});
+    for (size_t c = 0; c < n; c += kSteps) {
+      uint32_t base = UINT32_MAX, top = 0, x0 = 0;
+      bool first = true;
+      for (int q = 0; q < kTiledChunk; ++q) {
+        const Slot& sl = hs[q / kSteps][c + q % kSteps];
+        if (!sl.run) continue;
+        const uint32_t cc = (uint32_t)col[sl.run->k + sl.t];
+        base = std::min(base, cc);
+        top = std::max(top, cc);
+        if (first) x0 = cc;
+        first = false;
+      }
+      if (first) base = top = x0 = 0;
+      if (top - base >= (uint32_t)kMaxPanel) return false;
+      x0 -= base;
+      uint64_t cmask = 0;
+      for (int q = 0; q < kGroups; ++q)
+        for (int t = 0; t < kSteps; ++t) {
+          const Slot& sl = hs[q][c + t];
+          if (!sl.run) {
+            out.slot[w].push_back(x0 << kRowBits | (uint32_t)R);
+            out.val[w].push_back(0.f);
+            continue;
+          }
+          const int64_t k = sl.run->k + sl.t;
+          if (t > 0 && hs[q][c + t - 1].run == sl.run) cmask |= 1ull << (kSteps * q + t);
+          out.slot[w].push_back(((uint32_t)col[k] - base) << kRowBits | (uint32_t)sl.run->row);
+          out.val[w].push_back(val[k]);
+        }
+      out.hdr[w].insert(out.hdr[w].end(), {0u, (uint32_t)cmask, (uint32_t)(cmask >> 32), base});
+    }
+  }
+  out.nsteps = 1;   // the pass-end barrier only
+  return true;
+}
+
 }  // namespace
 }  // namespace gnnrec
 
@@ -692,8 +760,10 @@ extern "C" int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* co
   GNNREC_REQUIRE(row_ptr && plan && n_chunks && n_blocks && n_rows >= 0, "tiled_plan: bad args");
   GNNREC_REQUIRE(rows_per_block >= 1 && rows_per_block <= GNNREC_TILED_MAX_ROWS,
                  "tiled_plan: rows_per_block must be in [1, %d]", GNNREC_TILED_MAX_ROWS);
-  GNNREC_REQUIRE(panel >= 1 && sub_panel >= 0, "tiled_plan: bad panel / sub_panel");
+  GNNREC_REQUIRE((panel >= 1 && sub_panel >= 0) || (panel == 0 && sub_panel >= 1),
+                 "tiled_plan: bad panel / sub_panel (panel 0 = pinned rows needs a sub-panel)");
   panel = std::min(panel, kMaxPanel);   // a slot word holds 20 bits of column offset
+  const bool pinned = panel == 0;
   const int64_t nnz = n_rows > 0 ? row_ptr[n_rows] - row_ptr[0] : 0;
   GNNREC_REQUIRE(nnz == 0 || (col && val), "tiled_plan: null col/val");
   auto* pl = new (std::nothrow) TiledPlan;
@@ -703,14 +773,18 @@ extern "C" int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* co
   int t = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
   t = std::max(1, std::min<int>(t, (int)std::max<int64_t>(1, pl->n_blocks)));
   std::atomic<int64_t> next{0};
-  std::atomic<bool> bad_col{false};
+  std::atomic<bool> bad_col{false}, too_wide{false};
   auto worker = [&] {
     for (int64_t b; (b = next.fetch_add(1)) < pl->n_blocks;) {
       const int64_t r0 = b * rows_per_block, r1 = std::min<int64_t>(n_rows, r0 + rows_per_block);
       for (int64_t k = row_ptr[r0]; k < row_ptr[r1]; ++k)
         if (col[k] < 0) bad_col = true;
       if (bad_col) continue;
-      build_block(row_ptr, col, val, n_rows, rows_per_block, panel, sub_panel, b, pl->blocks[b]);
+      if (!pinned)
+        build_block(row_ptr, col, val, n_rows, rows_per_block, panel, sub_panel, b, pl->blocks[b]);
+      else if (!build_block_pinned(row_ptr, col, val, n_rows, rows_per_block, sub_panel, b,
+                                   pl->blocks[b]))
+        too_wide = true;
     }
   };
   std::vector<std::thread> pool;
@@ -721,6 +795,11 @@ extern "C" int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* co
     delete pl;
     set_error("tiled_plan: negative column index");
     return GNNREC_EINVAL;
+  }
+  if (too_wide) {
+    delete pl;
+    set_error("tiled_plan: pinned rows: a chunk spans 2^20 columns or more (plan with panels)");
+    return GNNREC_EUNSUPPORTED;
   }
   int64_t tot = 0;
   for (const auto& bp : pl->blocks)

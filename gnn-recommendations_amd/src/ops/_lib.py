@@ -26,7 +26,9 @@ EPI_ACC_DIV = 4
 EPI_NO_Y = 8
 EPI_ACC_X = 16
 # column-ordered hop plan layout (include/gnnrec.h GNNREC_TILED_*)
-TILED_WAVES = 8
+# (experiment builds of tiled.hip may use another wave count: tools/build_variant.sh; the
+# planner, the kernel and this value must agree)
+TILED_WAVES = int(os.environ.get("GNNREC_TILED_WAVES", "8"))
 TILED_GROUPS = 8
 TILED_STEPS = 8
 TILED_CHUNK = 64

@@ -386,8 +386,9 @@ class CsrGraph:
         order)."""
         key = ("tiled", int(rows_per_block), int(panel), int(sub_panel))
         if key not in self._plans:
-            if planner is None:
-                planner = TILED_PLANNER if self.device.type == "cuda" else "host"
+            if planner is None:   # panel 0 (pinned rows): host planner only
+                planner = (TILED_PLANNER if self.device.type == "cuda" and int(panel) > 0
+                           else "host")
             if planner == "device":
                 plan = self._tiled_plan_device(int(rows_per_block), int(panel), int(sub_panel))
             elif planner == "host":

@@ -124,7 +124,7 @@ def _walk_tiled_plan(plan, n_rows, R):
                 cur += int(hdr[4 * c])
                 cm = int(hdr[4 * c + 1]) | (int(hdr[4 * c + 2]) << 32)
                 pbase = int(hdr[4 * c + 3])
-                assert pbase % panel == 0
+                assert panel == 0 or pbase % panel == 0     # panel 0: pinned rows, any base
                 for g in range(NG):
                     base = c * CH + g * S
                     rows = [int(sw[base + t]) & 2047 for t in range(S)]
@@ -143,7 +143,7 @@ def _walk_tiled_plan(plan, n_rows, R):
                         assert chain == (1 if (t > 0 and rows[t - 1] == row) else 0)
                         assert owner.setdefault((cur, row), (w, g)) == (w, g)
                         rel = int(sw[base + t]) >> 11
-                        assert rel < panel
+                        assert rel < (panel or (1 << 20))
                         events.append((cur, w, c, t, row, pbase + rel, val[base + t]))
             assert cur <= max(ns[b] - 1, 0)
         # inside a step a row is on one stream, which applies its slots in chunk / step order
@@ -155,12 +155,14 @@ def _walk_tiled_plan(plan, n_rows, R):
 
 @pytest.mark.parametrize("R,panel,sub", [(1117, 32768, 0), (1117, 131072, 4096), (37, 5, 2),
                                          (37, 64, 8), (1, 1, 0), (16, 1 << 30, 64),
-                                         (1279, 4096, 512), (1277, 131072, 4096)])
+                                         (1279, 4096, 512), (1277, 131072, 4096),
+                                         (1117, 0, 4096), (37, 0, 2), (1, 0, 1), (500, 0, 64)])
 def test_tiled_plan_preserves_every_row_chain(R, panel, sub):
     """The column-ordered plan visits each row's neighbours exactly in CSR order (ascending
     columns: the fmaf order that makes the hop bit-exact), once each, one slot stream per row
     and step, a row at most one run of slots per 4-slot group of a stream (sub-panel order
-    interleaves rows), with chain bits exactly on run continuations inside a chunk."""
+    interleaves rows), with chain bits exactly on run continuations inside a chunk. panel 0:
+    pinned rows (one stream per row for the whole pass, no step barriers)."""
     rng = np.random.default_rng(R + panel + sub)
     u = np.concatenate([rng.integers(0, 700, 6000), np.zeros(300, np.int64)])  # a long row
     i = np.concatenate([rng.integers(0, 900, 6000), np.arange(300)])
