@@ -35,7 +35,7 @@ def _graph():
 def _model(kind, nu, ni, dev):
     from src.models import GAT, LightGCN, NGCFGroupShuffle
     torch.manual_seed(7)
-    if kind in ("lightgcn", "train", "lightgcn_tiled"):
+    if kind in ("lightgcn", "train", "lightgcn_tiled", "lightgcn_grid_tiled"):
         m = LightGCN(nu, ni, 64, 3, 0.1)
     elif kind == "lightgcn_d128_tiled":
         m = LightGCN(nu, ni, 128, 3, 0.1)
