@@ -80,7 +80,10 @@ def _hold(ctx, row_ptr, col, val, n_cols) -> None:
     would then rebuild it from the raw tensors (graph_of's warning)."""
     ctx.graph = None
     if not torch.compiler.is_compiling():
-        ctx.graph = _LIVE.get(_key(row_ptr, col, val, n_cols))
+        try:
+            ctx.graph = _LIVE.get(_key(row_ptr, col, val, n_cols))
+        except RuntimeError:   # fake / functional tensors (AOT tracing): nothing to hold
+            ctx.graph = None
 
 
 def _revive(ctx) -> None:
