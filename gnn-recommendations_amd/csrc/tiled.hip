@@ -186,7 +186,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const char* xs, uin
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* p, int64_t r0,
                                                             int64_t ld, int slice, int rows) {
   const float* b = p ? p + r0 * ld + (int64_t)slice * kSlice : p;
-  const uint32_t n = (p && rows > 0) ? (uint32_t)(rows - 1) * (uint32_t)ld * 4u + kRowBytes : 0u;
+  const uint32_t n = p ? (uint32_t)(rows - 1) * (uint32_t)ld * 4u + kRowBytes : 0u;
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(b), 0, (int)n, 0x00020000);
 }
 
@@ -300,7 +300,7 @@ __device__ __forceinline__ void tiled_apply(float* acc, uint32_t q16, const Tile
 // (((b0 [+ b1]) [+ b2]) + y) [/ div] — b0 = x0 (ACC_INIT) or the running sum (ACC_ADD);
 // INIT|ADD: b0 = x0, b1 = the acc rows (an earlier layer parked there); ACC_X: the hop's
 // input row (the previous layer) last. NB = 0: y only.
-template <int NB, int B, int STRIDE, class Wait>
+template <int NB, int B, class Wait>
 __device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, uint32_t q16,
                                                __amdgpu_buffer_rsrc_t ry, uint32_t ly,
                                                __amdgpu_buffer_rsrc_t rb0, uint32_t lb0,
@@ -308,7 +308,7 @@ __device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, 
                                                __amdgpu_buffer_rsrc_t rb2, uint32_t lb2,
                                                __amdgpu_buffer_rsrc_t ra, uint32_t la,
                                                bool div, float acc_div, Wait wait) {
-  constexpr int kStride = STRIDE;   // rows between a group's rows
+  constexpr int kStride = kGroups * kTiledWaves;
   const __amdgpu_buffer_rsrc_t rb[3] = {rb0, rb1, rb2};
   const uint32_t lb[3] = {lb0, lb1, lb2};
   f4 base[NB > 0 ? NB : 1][B];
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     const uint32_t* __restrict__ ss, const float* __restrict__ sv,
     const uint32_t* __restrict__ hdr, const int64_t* __restrict__ wptr,
     const int32_t* __restrict__ nsteps, int n_blocks, int nb_pad, int n_items, int R,
-    int wave_rows, const float* __restrict__ x, uint32_t x_rows32, uint32_t row_bytes,
+    const float* __restrict__ x, uint32_t x_rows32, uint32_t row_bytes,
     float* __restrict__ y, uint32_t ldy4, int n_rows, int epi, const float* __restrict__ self,
     uint32_t ls4, float* __restrict__ accg, uint32_t la4, float acc_div,
     const float* __restrict__ prev, uint32_t lp4, unsigned* __restrict__ sync,
@@ -397,20 +397,13 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
 #ifdef GNNREC_TILED_TRACE
   int ev = 0;
 #endif
-  // wave partitions (wave_rows > 0, a plan without step barriers): wave w owns accumulator
-  // rows [w0, w0 + wave_rows); it zeroes, fills and drains them by itself, so the waves of a
-  // workgroup never wait for each other and one wave's pass-end epilogue (HBM rows) overlaps
-  // the others' gathers. The pass-start meeting then counts waves.
-  const bool wmode = wave_rows > 0;
-  const int w0 = wmode ? w * wave_rows : 0;
-  const int wlim = wmode ? max(0, min(wave_rows, R - w0)) : R;   // own LDS rows
   for (int item = blockIdx.x; item < n_items; item += gridDim.x, ++pass) {
-    if ((wmode ? lane == 0 : threadIdx.x == 0) && pass > 0 && meet_ticks > 0) {
+    if (threadIdx.x == 0 && pass > 0 && meet_ticks > 0) {
       // pass start: report the finished pass, wait (bounded) for the group's others
       __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned target = (unsigned)(G * pass * (wmode ? kTiledWaves : 1));
       const unsigned long long t0 = wall_clock64();
-      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
+      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                 (unsigned)(G * pass) &&
              wall_clock64() - t0 < meet_ticks)
         __builtin_amdgcn_s_sleep(2);
     }
@@ -418,13 +411,9 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     if (blk >= n_blocks) continue;   // padding item (uniform over the workgroup)
     {
       const f4 z = {0.f, 0.f, 0.f, 0.f};
-      if (wmode) {
-        for (int i = w0 * (kSlice / 4) + lane; i < (w0 + wlim) * (kSlice / 4); i += 64) acc4[i] = z;
-      } else {
-        for (int i = threadIdx.x; i < (R + 1) * (kSlice / 4); i += kTiledWaves * 64) acc4[i] = z;
-        __syncthreads();
-      }
+      for (int i = threadIdx.x; i < (R + 1) * (kSlice / 4); i += kTiledWaves * 64) acc4[i] = z;
     }
+    __syncthreads();
     GNNREC_TILED_STAMP(ev);
     const uint32_t soff = (uint32_t)slice * kRowBytes;
     const char* xs = reinterpret_cast<const char*>(x) + soff;
@@ -472,19 +461,17 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
       run_ring(std::make_integer_sequence<int, kRingUnroll>{}, stage);
     }
     if (GNNREC_TILED_EXP & 1) *reinterpret_cast<f4*>(reinterpret_cast<char*>(acc) + R * kRowBytes + q16) = sink;
-    const int ns = wmode ? 0 : nsteps[blk];   // wave partitions: no barrier at all
+    const int ns = nsteps[blk];
     auto wait = [&]() {
       for (int i = cur; i < ns; ++i) {  // this wave's remaining steps + the last
         __syncthreads();
         GNNREC_TILED_STAMP(ev);
       }
     };
-    // epilogue: group g of wave w owns rows i = 8w + g + 64j of the block (see
-    // tiled_epilogue); wave partitions: rows w0 + g + 8j of its own range
-    const int r0 = blk * R + w0;
-    const int nv = wmode ? max(0, min(wlim, n_rows - r0)) : min(R, n_rows - r0);
-    const int rl = wmode ? (lane >> 3) : kGroups * w + (lane >> 3);
-    const float* accw = acc + w0 * kSlice;
+    // epilogue: group g of wave w owns rows i = 8w + g + 128j (see tiled_epilogue)
+    const int r0 = blk * R;
+    const int nv = min(R, n_rows - r0);
+    const int rl = kGroups * w + (lane >> 3);
     const __amdgpu_buffer_rsrc_t ry = rows_rsrc((epi & GNNREC_EPI_NO_Y) ? nullptr : y, r0,
                                                 ldy4 / 4, slice, nv);
     // base inputs in layer order: x0 (INIT), the acc rows (ADD), the previous layer (ACC_X:
@@ -499,15 +486,9 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     const __amdgpu_buffer_rsrc_t rb0 = init ? rs : racc, rb1 = (init && add) ? racc : rx;
     const uint32_t lb0 = init ? ls : la, lb1 = (init && add) ? la : lp4;
     const bool div = (epi & GNNREC_EPI_ACC_DIV) != 0;
-#define GNNREC_TILED_EPI(NB, B, DIV)                                                        \
-  do {                                                                                       \
-    if (wmode)                                                                               \
-      tiled_epilogue<NB, B, kGroups>(accw, wlim, rl, q16, ry, ly, rb0, lb0, rb1, lb1, rx, lp4, \
-                                     racc, la, DIV, acc_div, wait);                          \
-    else                                                                                     \
-      tiled_epilogue<NB, B, kGroups * kTiledWaves>(acc, R, rl, q16, ry, ly, rb0, lb0, rb1,   \
-                                                   lb1, rx, lp4, racc, la, DIV, acc_div, wait); \
-  } while (0)
+#define GNNREC_TILED_EPI(NB, B, DIV) \
+  tiled_epilogue<NB, B>(acc, R, rl, q16, ry, ly, rb0, lb0, rb1, lb1, rx, lp4, racc, la, DIV, \
+                        acc_div, wait)
     if (nb == 0)
       GNNREC_TILED_EPI(0, kEpiBatch, false);
     else if (nb == 1)
@@ -517,10 +498,10 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     else
       GNNREC_TILED_EPI(3, kEpiBatch3, div);
 #undef GNNREC_TILED_EPI
-    if (!wmode) __syncthreads();
+    __syncthreads();
   }
   // finished: never hold the group back again
-  if ((wmode ? lane == 0 : threadIdx.x == 0) && meet_ticks > 0)
+  if (threadIdx.x == 0 && meet_ticks > 0)
     __hip_atomic_fetch_add(ctr, 1u << 24, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -699,80 +680,6 @@ void build_block(const int64_t* rp, const int32_t* col, const float* val, int64_
   out.nsteps = step;
 }
 
-// Pinned rows (panel = 0): each row stays in ONE slot stream for the whole pass (LPT of the
-// rows by degree), so no step needs a barrier and a wave pads its streams once per pass
-// instead of once per step; each stream walks its rows' edges in (sub-panel, row) order and
-// the waves keep to nearby columns by that order alone. A chunk's base is its smallest
-// column; false when a chunk's slots span kMaxPanel columns or more (the slot word holds 20
-// bits of offset): the caller then plans with panels.
-// wave_rows > 0 (wave partitions): wave w owns the block's rows [w wave_rows, (w+1)
-// wave_rows) and LPT deals them over ITS 8 streams only, so a wave's accumulator rows are a
-// private LDS range: the kernel then needs no barrier at all and each wave runs its own
-// epilogue as soon as its slots are done (gnnrec_spmm_tiled_f32's wave_rows).
-bool build_block_pinned(const int64_t* rp, const int32_t* col, const float* val, int64_t n_rows,
-                        int R, int sub_panel, int wave_rows, int64_t b, BlockPlan& out) {
-  const int64_t r0 = b * R, r1 = std::min<int64_t>(n_rows, r0 + R);
-  std::vector<Run> runs;
-  for (int64_t r = r0; r < r1; ++r)
-    if (rp[r + 1] > rp[r]) runs.push_back({0, (int32_t)(r - r0), rp[r], (int32_t)(rp[r + 1] - rp[r])});
-  std::vector<const Run*> g;
-  for (const Run& e : runs) g.push_back(&e);
-  std::stable_sort(g.begin(), g.end(), [](const Run* a, const Run* c) { return a->n > c->n; });
-  int64_t load[kVirt] = {};
-  std::vector<const Run*> wl[kVirt];
-  for (const Run* e : g) {
-    const int lo = wave_rows > 0 ? kGroups * (e->row / wave_rows) : 0;
-    const int hi = wave_rows > 0 ? lo + kGroups : kVirt;
-    int v = lo;
-    for (int q = lo + 1; q < hi; ++q)
-      if (load[q] < load[v]) v = q;
-    load[v] += e->n;
-    wl[v].push_back(e);
-  }
-  std::vector<Slot> hs[kGroups];
-  for (int w = 0; w < kTiledWaves; ++w) {
-    size_t n = 0;
-    for (int q = 0; q < kGroups; ++q) {
-      stream_slots(wl[kGroups * w + q], col, sub_panel, hs[q]);
-      n = std::max(n, hs[q].size());
-    }
-    for (int q = 0; q < kGroups; ++q) hs[q].resize(n, Slot{nullptr, 0});
-    for (size_t c = 0; c < n; c += kSteps) {
-      uint32_t base = UINT32_MAX, top = 0, x0 = 0;
-      bool first = true;
-      for (int q = 0; q < kTiledChunk; ++q) {
-        const Slot& sl = hs[q / kSteps][c + q % kSteps];
-        if (!sl.run) continue;
-        const uint32_t cc = (uint32_t)col[sl.run->k + sl.t];
-        base = std::min(base, cc);
-        top = std::max(top, cc);
-        if (first) x0 = cc;
-        first = false;
-      }
-      if (first) base = top = x0 = 0;
-      if (top - base >= (uint32_t)kMaxPanel) return false;
-      x0 -= base;
-      uint64_t cmask = 0;
-      for (int q = 0; q < kGroups; ++q)
-        for (int t = 0; t < kSteps; ++t) {
-          const Slot& sl = hs[q][c + t];
-          if (!sl.run) {
-            out.slot[w].push_back(x0 << kRowBits | (uint32_t)R);
-            out.val[w].push_back(0.f);
-            continue;
-          }
-          const int64_t k = sl.run->k + sl.t;
-          if (t > 0 && hs[q][c + t - 1].run == sl.run) cmask |= 1ull << (kSteps * q + t);
-          out.slot[w].push_back(((uint32_t)col[k] - base) << kRowBits | (uint32_t)sl.run->row);
-          out.val[w].push_back(val[k]);
-        }
-      out.hdr[w].insert(out.hdr[w].end(), {0u, (uint32_t)cmask, (uint32_t)(cmask >> 32), base});
-    }
-  }
-  out.nsteps = 1;   // the pass-end barrier only
-  return true;
-}
-
 }  // namespace
 }  // namespace gnnrec
 
@@ -785,12 +692,8 @@ extern "C" int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* co
   GNNREC_REQUIRE(row_ptr && plan && n_chunks && n_blocks && n_rows >= 0, "tiled_plan: bad args");
   GNNREC_REQUIRE(rows_per_block >= 1 && rows_per_block <= GNNREC_TILED_MAX_ROWS,
                  "tiled_plan: rows_per_block must be in [1, %d]", GNNREC_TILED_MAX_ROWS);
-  GNNREC_REQUIRE((panel >= 1 && sub_panel >= 0) || (panel <= 0 && sub_panel >= 1),
-                 "tiled_plan: bad panel / sub_panel (panel <= 0 = pinned rows needs a sub-panel)");
+  GNNREC_REQUIRE(panel >= 1 && sub_panel >= 0, "tiled_plan: bad panel / sub_panel");
   panel = std::min(panel, kMaxPanel);   // a slot word holds 20 bits of column offset
-  if (panel < 0) panel = -1;
-  const bool pinned = panel <= 0;   // 0: pinned rows, < 0: pinned wave partitions
-  const int wave_rows = panel < 0 ? (rows_per_block + kTiledWaves - 1) / kTiledWaves : 0;
   const int64_t nnz = n_rows > 0 ? row_ptr[n_rows] - row_ptr[0] : 0;
   GNNREC_REQUIRE(nnz == 0 || (col && val), "tiled_plan: null col/val");
   auto* pl = new (std::nothrow) TiledPlan;
@@ -800,18 +703,14 @@ extern "C" int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* co
   int t = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
   t = std::max(1, std::min<int>(t, (int)std::max<int64_t>(1, pl->n_blocks)));
   std::atomic<int64_t> next{0};
-  std::atomic<bool> bad_col{false}, too_wide{false};
+  std::atomic<bool> bad_col{false};
   auto worker = [&] {
     for (int64_t b; (b = next.fetch_add(1)) < pl->n_blocks;) {
       const int64_t r0 = b * rows_per_block, r1 = std::min<int64_t>(n_rows, r0 + rows_per_block);
       for (int64_t k = row_ptr[r0]; k < row_ptr[r1]; ++k)
         if (col[k] < 0) bad_col = true;
       if (bad_col) continue;
-      if (!pinned)
-        build_block(row_ptr, col, val, n_rows, rows_per_block, panel, sub_panel, b, pl->blocks[b]);
-      else if (!build_block_pinned(row_ptr, col, val, n_rows, rows_per_block, sub_panel,
-                                   wave_rows, b, pl->blocks[b]))
-        too_wide = true;
+      build_block(row_ptr, col, val, n_rows, rows_per_block, panel, sub_panel, b, pl->blocks[b]);
     }
   };
   std::vector<std::thread> pool;
@@ -822,11 +721,6 @@ extern "C" int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* co
     delete pl;
     set_error("tiled_plan: negative column index");
     return GNNREC_EINVAL;
-  }
-  if (too_wide) {
-    delete pl;
-    set_error("tiled_plan: pinned rows: a chunk spans 2^20 columns or more (plan with panels)");
-    return GNNREC_EUNSUPPORTED;
   }
   int64_t tot = 0;
   for (const auto& bp : pl->blocks)
@@ -905,8 +799,7 @@ extern "C" int gnnrec_spmm_tiled_supported(int32_t device, int32_t rows_per_bloc
 extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
                                      const uint32_t* hdr, const int64_t* wave_ptr,
                                      const int32_t* n_steps, int64_t n_blocks,
-                                     int32_t rows_per_block, int32_t wave_rows,
-                                     const float* x, int64_t x_rows,
+                                     int32_t rows_per_block, const float* x, int64_t x_rows,
                                      int64_t ldx, float* y, int64_t ldy, int64_t n_rows, int32_t d,
                                      int32_t epi, const float* self, int64_t ld_self, float* acc,
                                      int64_t ld_acc, float acc_div, const float* prev,
@@ -916,9 +809,6 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
                  (int)d);
   GNNREC_REQUIRE(rows_per_block >= 1 && rows_per_block <= GNNREC_TILED_MAX_ROWS,
                  "spmm_tiled: bad rows_per_block");
-  GNNREC_REQUIRE(wave_rows == 0 || (wave_rows >= (rows_per_block + kTiledWaves - 1) / kTiledWaves &&
-                                    wave_rows <= rows_per_block),
-                 "spmm_tiled: wave_rows must be 0 or cover the block's rows with its waves");
   GNNREC_REQUIRE(n_rows >= 0 && n_blocks == (n_rows + rows_per_block - 1) / rows_per_block,
                  "spmm_tiled: n_blocks does not match n_rows / rows_per_block");
   GNNREC_REQUIRE(ldx >= d && ldx % 4 == 0 && x_rows >= 0 && ldx * 4 <= kMaxRowBytes,
@@ -974,8 +864,7 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
     return check_launch("spmm_tiled (sync reset)");
   hipLaunchKernelGGL(tiled_hop_kernel, dim3((unsigned)grid), dim3(kTiledWaves * 64), lds, s,
                      slot, val, hdr, wave_ptr, n_steps,
-                     (int)n_blocks, (int)nb_pad, (int)n_items, (int)rows_per_block,
-                     (int)wave_rows, x,
+                     (int)n_blocks, (int)nb_pad, (int)n_items, (int)rows_per_block, x,
                      (uint32_t)x_rows, (uint32_t)(ldx * 4), y, (uint32_t)(ldy * 4),
                      (int)n_rows, epi, self, (uint32_t)(ld_self * 4), acc, (uint32_t)(ld_acc * 4),
                      acc_div, prev, (uint32_t)(ld_prev * 4), sync,

@@ -17,7 +17,7 @@ import torch  # noqa: F401  (load order: torch's HIP runtime first)
 
 _PKG_ROOT = Path(__file__).resolve().parents[2]
 LIB_PATH = Path(os.environ.get("GNNREC_LIB", _PKG_ROOT / "lib" / "libgnnrec.so"))
-ABI_VERSION = 8
+ABI_VERSION = 7
 
 # gnnrec.h epilogue flags
 EPI_ACC_INIT = 1
@@ -26,9 +26,7 @@ EPI_ACC_DIV = 4
 EPI_NO_Y = 8
 EPI_ACC_X = 16
 # column-ordered hop plan layout (include/gnnrec.h GNNREC_TILED_*)
-# (experiment builds of tiled.hip may use another wave count: tools/build_variant.sh; the
-# planner, the kernel and this value must agree)
-TILED_WAVES = int(os.environ.get("GNNREC_TILED_WAVES", "8"))
+TILED_WAVES = 8
 TILED_GROUPS = 8
 TILED_STEPS = 8
 TILED_CHUNK = 64
@@ -64,7 +62,7 @@ _SIGNATURES = {
     "gnnrec_tiled_plan_device": [_p, _p, _p, _i64, _i32, _i32, _i32, _i64, _p, _i32, _p, _p, _p,
                                  _p, _p, _p, _p, _p],
     "gnnrec_spmm_tiled_supported": [_i32, _i32],
-    "gnnrec_spmm_tiled_f32": [_p, _p, _p, _p, _p, _i64, _i32, _i32, _p, _i64, _i64, _p, _i64,
+    "gnnrec_spmm_tiled_f32": [_p, _p, _p, _p, _p, _i64, _i32, _p, _i64, _i64, _p, _i64,
                               _i64, _i32, _i32, _p, _i64, _p, _i64, _f32, _p, _i64, _p, _i32, _p],
     "gnnrec_row_nonzero_f32": [_p, _i64, _i64, _i32, _p, _p],
     "gnnrec_lightgcn_split_f32": [_p, _p, _p, _i64, _p, _i32, _i32, _p, _p, _p, _p, _i64, _p,

@@ -386,19 +386,16 @@ class CsrGraph:
         order)."""
         key = ("tiled", int(rows_per_block), int(panel), int(sub_panel))
         if key not in self._plans:
-            if planner is None:   # panel <= 0 (pinned rows): host planner only
-                planner = (TILED_PLANNER if self.device.type == "cuda" and int(panel) > 0
-                           else "host")
+            if planner is None:
+                planner = TILED_PLANNER if self.device.type == "cuda" else "host"
             if planner == "device":
                 plan = self._tiled_plan_device(int(rows_per_block), int(panel), int(sub_panel))
             elif planner == "host":
                 plan = self._tiled_plan_host(int(rows_per_block), int(panel), int(sub_panel))
             else:
                 raise ValueError(f"unknown planner {planner!r}")
-            W = _lib.TILED_WAVES
             plan.update(rows_per_block=int(rows_per_block),
                         panel=min(int(panel), _lib.TILED_MAX_PANEL), sub_panel=int(sub_panel),
-                        wave_rows=(-(-int(rows_per_block) // W) if int(panel) < 0 else 0),
                         n_slots=plan["n_chunks"] * _lib.TILED_CHUNK,
                         sync=torch.zeros(_lib.TILED_SYNC_WORDS, dtype=torch.int32,
                                          device=self.device))

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GNNREC_ABI_VERSION 8
+#define GNNREC_ABI_VERSION 7
 
 typedef struct ihipStream_t* gnnrec_stream_t;
 
@@ -158,11 +158,6 @@ int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col, const
  * consecutive slots. Slot arrays hold (n_chunks + GNNREC_TILED_TAIL) * GNNREC_TILED_CHUNK
  * entries, hdr 4 * (n_chunks + GNNREC_TILED_TAIL) (tail chunks read by the last prefetches);
  * wave_ptr [n_blocks * GNNREC_TILED_WAVES + 1] are chunk offsets; n_steps [n_blocks].
- * panel >= 1 cuts the columns into panels (a step each, a workgroup barrier between steps);
- * panel 0 pins every row to one stream for the whole pass (one step, no barrier until the
- * pass end); panel < 0 pins rows to streams of the wave that owns their range of
- * ceil(rows_per_block / GNNREC_TILED_WAVES) rows — launch that plan with that wave_rows (ABI
- * 8; 0 otherwise): its waves then never wait for each other.
  * rows_per_block <= GNNREC_TILED_MAX_ROWS. gnnrec_spmm_tiled_f32 needs d % 32 == 0,
  * d <= ldx <= GNNREC_TILED_MAX_LDX (any table size), every table 16-B aligned with its
  * leading dimension a multiple of 4, `sync`: a device scratch of GNNREC_TILED_SYNC_WORDS
@@ -212,8 +207,7 @@ int gnnrec_spmm_tiled_supported(int32_t device, int32_t rows_per_block);
 
 int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val, const uint32_t* hdr,
                           const int64_t* wave_ptr, const int32_t* n_steps, int64_t n_blocks,
-                          int32_t rows_per_block, int32_t wave_rows, const float* x,
-                          int64_t x_rows, int64_t ldx,
+                          int32_t rows_per_block, const float* x, int64_t x_rows, int64_t ldx,
                           float* y, int64_t ldy, int64_t n_rows, int32_t d, int32_t epi,
                           const float* self, int64_t ld_self, float* acc, int64_t ld_acc,
                           float acc_div, const float* prev, int64_t ld_prev, uint32_t* sync,
