@@ -27,7 +27,7 @@ from . import _lib
 
 # where a device-resident graph's column-ordered plan is built ("device" | "host"; the same
 # arrays either way)
-TILED_PLANNER = "host"
+TILED_PLANNER = "device"
 # gnnrec_tiled_plan_device error words: 1 negative column (the host planner's EINVAL),
 # 2 scratch too small, 3 a run longer than 2^21, 4 count / emit disagree
 _DEVICE_PLAN_ERRORS = {1: ValueError}
@@ -450,7 +450,10 @@ class CsrGraph:
         max_nnz = int(bnnz.max()) if nb else 0
         if max_nnz >= (1 << 31) - 1:
             raise ValueError("tiled plan: a block holds more than 2^31 edges")
-        wg = max(1, min(nb, torch.cuda.get_device_properties(dev).multi_processor_count))
+        # one 64-lane workgroup per block at a time: up to 4 per CU, scratch at most ~4 GB
+        per_wg = 8 * L.gnnrec_tiled_plan_device_scratch_words(max_nnz, 1)
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        wg = max(1, min(nb, 4 * cus, (4 << 30) // max(per_wg, 1)))
         scratch = torch.empty(max(1, L.gnnrec_tiled_plan_device_scratch_words(max_nnz, wg)),
                               dtype=torch.int64, device=dev)
         chunks = torch.zeros(max(1, nb * W), dtype=torch.int64, device=dev)
