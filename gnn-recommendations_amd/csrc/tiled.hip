@@ -193,6 +193,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* p, int6
 __device__ __forceinline__ f4 load4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
+#ifndef GNNREC_TILED_EPI_LOAD_AUX
+#define GNNREC_TILED_EPI_LOAD_AUX 2   // nt: hop 3 3.92 -> 3.87 ms (profiles/r03/exp_epi_load_policy.jsonl)
+#endif
+// the epilogue's base rows, read once per hop: non-temporal (aux 2), so they do not evict the
+// gathered lines the next pass reuses from L2
+__device__ __forceinline__ f4 load4_base(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0,
+                                                                      GNNREC_TILED_EPI_LOAD_AUX));
+}
 __device__ __forceinline__ void store4(f4 v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
   __builtin_amdgcn_raw_buffer_store_b128(
       __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), r, off, 0,
@@ -327,7 +336,7 @@ __device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, 
     for (int q = 0; q < B; ++q)
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        base[j][q] = load4(rb[j], ob[j]);
+        base[j][q] = load4_base(rb[j], ob[j]);
         ob[j] += kStride * lb[j];
       }
   };
