@@ -160,7 +160,7 @@ __device__ __forceinline__ void tiled_slots(const uint32_t* __restrict__ ss,
                                             TiledSlots& m) {
   if (GNNREC_TILED_EXP & 8) c &= 63;
   const int64_t i = c * kTiledChunk + lane;
-  m.w = ss[i];
+  m.w = ss[i];   // default policy: nt plan loads measured 1 % slower (exp_plan_nt.jsonl)
   m.v = sv[i];
   m.h = hdr[4 * c + (lane & 3)];
 }
