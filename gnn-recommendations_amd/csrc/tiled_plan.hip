@@ -17,9 +17,8 @@
 //      (deferred repeats, padding), into per-workgroup scratch;
 //   5. per wave of the block: chunks of 8 steps x 8 streams, header and chain mask (two
 //      ballots), written at the offsets a counting pass of the same kernel produced.
-// A stream's lists live in LDS when every stream of the step holds at most 64 slots, else
-// in per-workgroup scratch: 6 * max_block_nnz + 512 words (slot lists, their ping-pong copy
-// and the padded sequences, at most 4 entries per slot + 7).
+// Scratch per workgroup: 6 * max_block_nnz + 512 words (slot lists, their ping-pong copy and
+// the padded sequences, at most 4 entries per slot + 7).
 #include <climits>
 
 #include "common.h"
@@ -122,215 +121,10 @@ __device__ void bitonic64(uint32_t* s, int n, int lane) {
     }
 }
 
-// A stream's slot lists live in LDS while every stream of the step holds at most kFastCap
-// slots (the common case: ~45 at G100M), else in the workgroup's global scratch. Entries
-// name (row, edge): global uint64 {edge << 11 | row}; LDS uint32 {row << 21 | edge - the
-// row's cursor}; a run: global {edge << 32 | left << 11 | row}, LDS {row << 21 | left} (its
-// next edge = cursor + run length - left). ~0 = padding.
-constexpr int kFastCap = 64;                 // slots per stream and step on the fast path
-constexpr int kLaneWords = 8 * kFastCap;     // S [0, 64) | D [64, 128) | O [128, 512)
-static_assert(kLaneWords - 2 * kFastCap >= 4 * kFastCap + 7, "padded sequence fits");
-
-// dynamic LDS of tiled_plan_kernel: cursors, ends, run lengths, keys, the lanes' lists, owners
-constexpr int kPlanLds = 4 * 3 * kPMaxRows + 4 * kPKeys + 4 * 64 * kLaneWords + kPKeys;
-static_assert(kPlanLds <= 160 * 1024, "LDS");
-
-template <bool FAST>
-struct Ent;
-template <>
-struct Ent<false> {
-  using T = uint64_t;
-  static __device__ __forceinline__ T slot(int row, int32_t k, const int32_t*) {
-    return ((uint64_t)(uint32_t)k << kPRowBits) | (uint32_t)row;
-  }
-  static __device__ __forceinline__ int row(T e) { return (int)(e & kPRowMask); }
-  static __device__ __forceinline__ int32_t edge(T e, const int32_t*) {
-    return (int32_t)(e >> kPRowBits);
-  }
-  static __device__ __forceinline__ T run(int row, int32_t k, uint32_t left, const int32_t*,
-                                          const int32_t*) {
-    return ((uint64_t)(uint32_t)k << 32) | ((uint64_t)left << kPRowBits) | (uint32_t)row;
-  }
-  static __device__ __forceinline__ int run_row(T e) { return (int)(e & kPRowMask); }
-  static __device__ __forceinline__ uint32_t run_left(T e) {
-    return (uint32_t)((e >> kPRowBits) & kPNMax);
-  }
-  static __device__ __forceinline__ int32_t run_edge(T e, const int32_t*, const int32_t*) {
-    return (int32_t)(e >> 32);
-  }
-  static constexpr T kPad = ~0ull;
-};
-template <>
-struct Ent<true> {
-  using T = uint32_t;
-  static __device__ __forceinline__ T slot(int row, int32_t k, const int32_t* pos) {
-    return ((uint32_t)row << 21) | (uint32_t)(k - pos[row]);
-  }
-  static __device__ __forceinline__ int row(T e) { return (int)(e >> 21); }
-  static __device__ __forceinline__ int32_t edge(T e, const int32_t* pos) {
-    return pos[e >> 21] + (int32_t)(e & 0x1FFFFFu);
-  }
-  static __device__ __forceinline__ T run(int row, int32_t, uint32_t left, const int32_t*,
-                                          const int32_t*) {
-    return ((uint32_t)row << 21) | left;
-  }
-  static __device__ __forceinline__ int run_row(T e) { return (int)(e >> 21); }
-  static __device__ __forceinline__ uint32_t run_left(T e) { return e & 0x1FFFFFu; }
-  static __device__ __forceinline__ int32_t run_edge(T e, const int32_t* pos, const int32_t* len) {
-    return pos[e >> 21] + len[e >> 21] - (int32_t)(e & 0x1FFFFFu);
-  }
-  static constexpr T kPad = ~0u;
-};
-
-// Steps 4 of the kernel for this lane's stream: its runs (assignment order), their slots in
-// (sub-panel, row, edge) order in S, then the 4-slot groups with the one-run rule and the
-// padding into O; returns the padded length. Rn / D share a region (runs are consumed first).
-template <bool FAST>
-__device__ int stream_slots_dev(const PlanArgs& a, const int32_t* col, int lane, int nk,
-                                const uint32_t* s_key, const uint8_t* s_asg,
-                                const int32_t* s_pos, const int32_t* s_len, uint32_t load,
-                                typename Ent<FAST>::T* S, typename Ent<FAST>::T* D,
-                                typename Ent<FAST>::T* O) {
-  using E = Ent<FAST>;
-  using T = typename E::T;
-  T* const Rn = D;
-  int nrun = 0;
-  for (int idx = 0; idx < nk; ++idx)
-    if (s_asg[idx] == lane) {
-      const uint32_t key = s_key[idx];
-      const int i = (int)(key & kPRowMask);
-      const uint32_t n = (uint32_t)(kPNMax - (int)(key >> kPRowBits));
-      Rn[nrun++] = E::run(i, s_pos[i], n, s_pos, s_len);
-    }
-  int ns = 0;
-  if (a.sub > 0) {
-    for (int x = 1; x < nrun; ++x) {   // runs by row (one run per row and step)
-      const T e = Rn[x];
-      int y = x - 1;
-      while (y >= 0 && E::run_row(Rn[y]) > E::run_row(e)) {
-        Rn[y + 1] = Rn[y];
-        --y;
-      }
-      Rn[y + 1] = e;
-    }
-    int left = (int)load;
-    while (left > 0) {
-      int smin = INT_MAX;
-      for (int x = 0; x < nrun; ++x) {
-        const T e = Rn[x];
-        if (E::run_left(e)) smin = min(smin, col[E::run_edge(e, s_pos, s_len)] / a.sub);
-      }
-      for (int x = 0; x < nrun; ++x) {
-        const T e = Rn[x];
-        int32_t k = E::run_edge(e, s_pos, s_len);
-        uint32_t n = E::run_left(e);
-        const int row = E::run_row(e);
-        while (n > 0 && col[k] / a.sub == smin) {
-          S[ns++] = E::slot(row, k, s_pos);
-          ++k;
-          --n;
-          --left;
-        }
-        Rn[x] = E::run(row, k, n, s_pos, s_len);
-      }
-    }
-  } else {
-    for (int x = 0; x < nrun; ++x) {
-      const T e = Rn[x];
-      const int32_t k = E::run_edge(e, s_pos, s_len);
-      const uint32_t n = E::run_left(e);
-      for (uint32_t t = 0; t < n; ++t) S[ns++] = E::slot(E::run_row(e), k + (int32_t)t, s_pos);
-    }
-  }
-  // groups of kPA: a row once per group as one run, repeats deferred; padded
-  int L = 0;
-  T* src = S;
-  T* dst = D;
-  int m = ns;
-  while (m > 0) {
-    int n = 0, last = -1, nin = 0, nbl = 0, dc = 0;
-    int ing[kPA], blk[kPA];
-    for (int q = 0; q < m; ++q) {
-      const T sl = src[q];
-      if (n == kPA) {
-        for (int z = q; z < m; ++z) dst[dc++] = src[z];
-        break;
-      }
-      const int r = E::row(sl);
-      bool isb = false, seen = false;
-      for (int z = 0; z < nbl; ++z) isb |= blk[z] == r;
-      for (int z = 0; z < nin; ++z) seen |= ing[z] == r;
-      const bool rep = seen && r != last;
-      if (isb || rep) {
-        if (rep && !isb) blk[nbl++] = r;
-        dst[dc++] = sl;
-        continue;
-      }
-      O[L++] = sl;
-      if (!seen) ing[nin++] = r;
-      last = r;
-      ++n;
-    }
-    if (dc > 0)
-      for (; n < kPA; ++n) O[L++] = E::kPad;
-    T* t = src;
-    src = dst;
-    dst = t;
-    m = dc;
-  }
-  while (L % kPS) O[L++] = E::kPad;
-  return L;
-}
-
-// Step 5 for wave w of the block: its chunks from the 8 streams' padded sequences.
-template <bool FAST>
-__device__ void emit_chunks(const PlanArgs& a, const int32_t* col, const float* val, int lane,
-                            int w, int nc, int64_t P, uint32_t bar, uint32_t base, int L,
-                            const typename Ent<FAST>::T* Ov, int64_t ostride,
-                            const int32_t* s_pos) {
-  using E = Ent<FAST>;
-  using T = typename E::T;
-  const int t = lane & 7;
-  const int v = kPG * w + (lane >> 3);   // stream of this lane's slot (lane = 8 g + t)
-  const int Lq = __shfl(L, v);
-  const T* Oq = Ov + (FAST ? v * ostride : (int64_t)shfl64((uint64_t)ostride, v));
-  for (int c = 0; c < nc; ++c) {
-    const int idx = c * kPS + t;
-    const T e = idx < Lq ? Oq[idx] : E::kPad;
-    const bool real = e != E::kPad;
-    const uint64_t rm = __ballot(real);
-    const int32_t ke = real ? E::edge(e, s_pos) : 0;
-    const int32_t kf = __shfl(ke, rm ? __ffsll((long long)rm) - 1 : 0);
-    const uint32_t x0 = rm ? (uint32_t)col[kf] - base : 0u;
-    const T ep = (t > 0 && idx - 1 < Lq) ? Oq[idx - 1] : E::kPad;
-    const uint64_t cm = __ballot(t > 0 && real && ep != E::kPad && E::row(ep) == E::row(e));
-    uint32_t word;
-    float vv;
-    if (real) {
-      word = (((uint32_t)col[ke] - base) << kPRowBits) | (uint32_t)E::row(e);
-      vv = val[ke];
-    } else {
-      word = (x0 << kPRowBits) | (uint32_t)a.R;
-      vv = 0.f;
-    }
-    const int64_t o = (P + c) * GNNREC_TILED_CHUNK + lane;
-    a.slot[o] = word;
-    a.vout[o] = vv;
-    if (lane < GNNREC_TILED_HDR_WORDS)
-      a.hdr[(P + c) * GNNREC_TILED_HDR_WORDS + lane] =
-          lane == 0 ? (c == 0 ? bar : 0u)
-                    : lane == 1 ? (uint32_t)cm : lane == 2 ? (uint32_t)(cm >> 32) : base;
-  }
-}
-
 __global__ __launch_bounds__(64) void tiled_plan_kernel(PlanArgs a, int emit) {
-  extern __shared__ uint32_t s_dyn[];   // kPlanLds bytes (tiled_plan_lds)
-  int32_t* const s_pos = reinterpret_cast<int32_t*>(s_dyn);
-  int32_t* const s_end = s_pos + kPMaxRows;
-  int32_t* const s_len = s_end + kPMaxRows;
-  uint32_t* const s_key = reinterpret_cast<uint32_t*>(s_len + kPMaxRows);
-  uint32_t* const s_lane = s_key + kPKeys;   // 64 lanes x kLaneWords: the fast-path lists
-  uint8_t* const s_asg = reinterpret_cast<uint8_t*>(s_lane + 64 * kLaneWords);
+  __shared__ int32_t s_pos[kPMaxRows], s_end[kPMaxRows], s_len[kPMaxRows];
+  __shared__ uint32_t s_key[kPKeys];
+  __shared__ uint8_t s_asg[kPKeys];
   const int lane = threadIdx.x;
   uint64_t* const A = a.scratch + (int64_t)blockIdx.x * (6 * a.cap + 512);
   uint64_t* const A2 = A + a.cap;
@@ -409,9 +203,7 @@ __global__ __launch_bounds__(64) void tiled_plan_kernel(PlanArgs a, int emit) {
         }
       }
       __syncthreads();
-      // 4. this stream's slots and groups: in LDS when every stream holds <= kFastCap
-      //    slots, else in the workgroup's scratch at A[aoff, aoff + load)
-      const bool fast = wave_max32((int)load) <= kFastCap;
+      // 4. this stream's slots: A[aoff, aoff + load) in (sub-panel, row, edge) order
       int aoff = (int)load;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
@@ -419,15 +211,98 @@ __global__ __launch_bounds__(64) void tiled_plan_kernel(PlanArgs a, int emit) {
         if (lane >= o) aoff += y;
       }
       aoff -= (int)load;
+      uint64_t* const Rn = A2 + aoff;   // the stream's runs {edge << 32 | n << 11 | row}
+      uint64_t* const S = A + aoff;
+      int nrun = 0;
+      for (int idx = 0; idx < nk; ++idx)
+        if (s_asg[idx] == lane) {
+          const uint32_t key = s_key[idx];
+          const int i = (int)(key & kPRowMask);
+          const uint32_t n = (uint32_t)(kPNMax - (int)(key >> kPRowBits));
+          Rn[nrun++] = ((uint64_t)(uint32_t)s_pos[i] << 32) | ((uint64_t)n << kPRowBits) | (uint32_t)i;
+        }
+      int ns = 0;
+      if (a.sub > 0) {
+        for (int x = 1; x < nrun; ++x) {   // runs by row (one run per row and step)
+          const uint64_t e = Rn[x];
+          int y = x - 1;
+          while (y >= 0 && (Rn[y] & kPRowMask) > (e & kPRowMask)) {
+            Rn[y + 1] = Rn[y];
+            --y;
+          }
+          Rn[y + 1] = e;
+        }
+        int left = (int)load;
+        while (left > 0) {
+          int smin = INT_MAX;
+          for (int x = 0; x < nrun; ++x) {
+            const uint64_t e = Rn[x];
+            if ((e >> kPRowBits) & kPNMax) smin = min(smin, col[(int32_t)(e >> 32)] / a.sub);
+          }
+          for (int x = 0; x < nrun; ++x) {
+            const uint64_t e = Rn[x];
+            int32_t k = (int32_t)(e >> 32);
+            uint32_t n = (uint32_t)((e >> kPRowBits) & kPNMax);
+            const uint32_t row = (uint32_t)(e & kPRowMask);
+            while (n > 0 && col[k] / a.sub == smin) {
+              S[ns++] = ((uint64_t)(uint32_t)k << kPRowBits) | row;
+              ++k;
+              --n;
+              --left;
+            }
+            Rn[x] = ((uint64_t)(uint32_t)k << 32) | ((uint64_t)n << kPRowBits) | row;
+          }
+        }
+      } else {
+        for (int x = 0; x < nrun; ++x) {
+          const uint64_t e = Rn[x];
+          const int32_t k = (int32_t)(e >> 32);
+          const uint32_t n = (uint32_t)((e >> kPRowBits) & kPNMax);
+          for (uint32_t t = 0; t < n; ++t)
+            S[ns++] = ((uint64_t)(uint32_t)(k + (int32_t)t) << kPRowBits) | (e & kPRowMask);
+        }
+      }
+      // groups of kPA: a row once per group as one run, repeats deferred; padded
       const int64_t boff = 4 * (int64_t)aoff + 8 * lane;
-      uint32_t* const lw = s_lane + lane * kLaneWords;
-      const int L = fast ? stream_slots_dev<true>(a, col, lane, nk, s_key, s_asg, s_pos, s_len,
-                                                  load, lw, lw + kFastCap, lw + 2 * kFastCap)
-                         : stream_slots_dev<false>(a, col, lane, nk, s_key, s_asg, s_pos, s_len,
-                                                   load, A + aoff, A2 + aoff, B + boff);
-      __syncthreads();
+      uint64_t* const O = B + boff;
+      int L = 0;
+      uint64_t* src = S;
+      uint64_t* dst = A2 + aoff;
+      int m = ns;
+      while (m > 0) {
+        int n = 0, last = -1, nin = 0, nbl = 0, dc = 0;
+        int ing[kPA], blk[kPA];
+        for (int q = 0; q < m; ++q) {
+          const uint64_t sl = src[q];
+          if (n == kPA) {
+            for (int z = q; z < m; ++z) dst[dc++] = src[z];
+            break;
+          }
+          const int r = (int)(sl & kPRowMask);
+          bool isb = false, seen = false;
+          for (int z = 0; z < nbl; ++z) isb |= blk[z] == r;
+          for (int z = 0; z < nin; ++z) seen |= ing[z] == r;
+          const bool rep = seen && r != last;
+          if (isb || rep) {
+            if (rep && !isb) blk[nbl++] = r;
+            dst[dc++] = sl;
+            continue;
+          }
+          O[L++] = sl;
+          if (!seen) ing[nin++] = r;
+          last = r;
+          ++n;
+        }
+        if (dc > 0)
+          for (; n < kPA; ++n) O[L++] = kPPad;
+        uint64_t* t = src;
+        src = dst;
+        dst = t;
+        m = dc;
+      }
+      while (L % kPS) O[L++] = kPPad;
       // 5. chunks of each wave of the block
-      const int q = lane >> 3;
+      const int q = lane >> 3, t = lane & 7;
       for (int w = 0; w < kPW; ++w) {
         int nw = (q == w) ? L : 0;   // lanes 8w .. 8w+7 hold the wave's streams' lengths
         nw = wave_max32(nw);
@@ -442,11 +317,38 @@ __global__ __launch_bounds__(64) void tiled_plan_kernel(PlanArgs a, int emit) {
             return;
           }
           const uint32_t bar = (uint32_t)(step - __shfl(curw, w));
-          if (fast)
-            emit_chunks<true>(a, col, val, lane, w, nc, P, bar, base, L, s_lane + 2 * kFastCap,
-                              kLaneWords, s_pos);
-          else
-            emit_chunks<false>(a, col, val, lane, w, nc, P, bar, base, L, B, boff, s_pos);
+          const int v = kPG * w + (lane >> 3);   // stream of this lane's slot (lane = 8 g + t)
+          const int Lq = __shfl(L, v);
+          const int64_t bq = (int64_t)shfl64((uint64_t)boff, v);
+          for (int c = 0; c < nc; ++c) {
+            const int idx = c * kPS + t;
+            const uint64_t e = idx < Lq ? B[bq + idx] : kPPad;
+            const bool real = e != kPPad;
+            const uint64_t rm = __ballot(real);
+            uint32_t x0 = 0;
+            const uint64_t ef = shfl64(e, rm ? __ffsll((long long)rm) - 1 : 0);
+            if (rm) x0 = (uint32_t)col[(int32_t)(ef >> kPRowBits)] - base;
+            const uint64_t ep = (t > 0 && idx - 1 < Lq) ? B[bq + idx - 1] : kPPad;
+            const uint64_t cm =
+                __ballot(t > 0 && real && ep != kPPad && (ep & kPRowMask) == (e & kPRowMask));
+            uint32_t word;
+            float vv;
+            if (real) {
+              const int32_t k = (int32_t)(e >> kPRowBits);
+              word = (((uint32_t)col[k] - base) << kPRowBits) | (uint32_t)(e & kPRowMask);
+              vv = val[k];
+            } else {
+              word = (x0 << kPRowBits) | (uint32_t)a.R;
+              vv = 0.f;
+            }
+            const int64_t o = (P + c) * GNNREC_TILED_CHUNK + lane;
+            a.slot[o] = word;
+            a.vout[o] = vv;
+            if (lane < GNNREC_TILED_HDR_WORDS)
+              a.hdr[(P + c) * GNNREC_TILED_HDR_WORDS + lane] =
+                  lane == 0 ? (c == 0 ? bar : 0u)
+                            : lane == 1 ? (uint32_t)cm : lane == 2 ? (uint32_t)(cm >> 32) : base;
+          }
           if (lane == w) pw += nc;
         }
         if (lane == w) curw = step;
@@ -511,12 +413,7 @@ extern "C" int gnnrec_tiled_plan_device(const int64_t* row_ptr, const int32_t* c
   if (nb > 0) {
     GNNREC_REQUIRE(col && val, "tiled_plan_device: null col / val");
     const int grid = (int)std::min<int64_t>(nb, workgroups);
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&tiled_plan_kernel),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, kPlanLds) != hipSuccess) {
-      set_error("tiled_plan_device: the device refuses %d B of LDS per workgroup", kPlanLds);
-      return GNNREC_EHIP;
-    }
-    hipLaunchKernelGGL(tiled_plan_kernel, dim3(grid), dim3(64), kPlanLds, s, a, emit ? 1 : 0);
+    hipLaunchKernelGGL(tiled_plan_kernel, dim3(grid), dim3(64), 0, s, a, emit ? 1 : 0);
     if (int rc = check_launch("tiled_plan_device")) return rc;
   }
   if (emit) {

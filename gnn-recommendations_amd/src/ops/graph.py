@@ -450,11 +450,10 @@ class CsrGraph:
         max_nnz = int(bnnz.max()) if nb else 0
         if max_nnz >= (1 << 31) - 1:
             raise ValueError("tiled plan: a block holds more than 2^31 edges")
-        # one 64-lane workgroup per block at a time, one per CU (its LDS holds the streams'
-        # lists), global scratch for steps whose streams outgrow it: at most ~4 GB
+        # one 64-lane workgroup per block at a time: up to 4 per CU, scratch at most ~4 GB
         per_wg = 8 * L.gnnrec_tiled_plan_device_scratch_words(max_nnz, 1)
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        wg = max(1, min(nb, cus, (4 << 30) // max(per_wg, 1)))
+        wg = max(1, min(nb, 4 * cus, (4 << 30) // max(per_wg, 1)))
         scratch = torch.empty(max(1, L.gnnrec_tiled_plan_device_scratch_words(max_nnz, wg)),
                               dtype=torch.int64, device=dev)
         chunks = torch.zeros(max(1, nb * W), dtype=torch.int64, device=dev)
