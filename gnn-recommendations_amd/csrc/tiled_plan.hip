@@ -17,8 +17,9 @@
 //      (deferred repeats, padding), into per-workgroup scratch;
 //   5. per wave of the block: chunks of 8 steps x 8 streams, header and chain mask (two
 //      ballots), written at the offsets a counting pass of the same kernel produced.
-// Scratch per workgroup: 6 * max_block_nnz + 512 words (slot lists, their ping-pong copy and
-// the padded sequences, at most 4 entries per slot + 7).
+// Scratch per workgroup: 6 * cap + 512 words (slot lists, their ping-pong copy and the padded
+// sequences, at most 4 entries per slot + 7) for steps of at most `cap` slots (error 2, and
+// the caller retries with a larger cap, beyond).
 #include <climits>
 
 #include "common.h"
@@ -56,7 +57,7 @@ struct PlanArgs {
   int R, panel, sub;
   int64_t n_blocks;
   uint64_t* scratch;
-  int64_t cap;          // max slots of a block (slot-list region of one workgroup)
+  int64_t cap;          // max slots of a step (slot-list region of one workgroup)
   int64_t* chunks;      // count pass: chunks per (block, wave)
   int32_t* nsteps;      // count pass: steps per block
   const int64_t* wave_ptr;   // emit pass: chunk offsets
@@ -137,7 +138,7 @@ __global__ __launch_bounds__(64) void tiled_plan_kernel(PlanArgs a, int emit) {
     const int32_t* col = a.col + kb;   // the block's edges, relative offsets
     const float* val = a.val + kb;
     const int64_t nnzb = a.rp[r1] - kb;
-    if (nnzb > a.cap) {                // the caller sized the scratch from row_ptr
+    if (nnzb >= INT32_MAX) {
       if (lane == 0) fail(a.err, 2);
       return;
     }
@@ -211,6 +212,12 @@ __global__ __launch_bounds__(64) void tiled_plan_kernel(PlanArgs a, int emit) {
         if (lane >= o) aoff += y;
       }
       aoff -= (int)load;
+      // the step's slots must fit the scratch regions (sized for a step, not a block: the
+      // caller retries with a larger cap when this fails)
+      if (__shfl(aoff + (int)load, 63) > a.cap) {
+        if (lane == 0) fail(a.err, 2);
+        return;
+      }
       uint64_t* const Rn = A2 + aoff;   // the stream's runs {edge << 32 | n << 11 | row}
       uint64_t* const S = A + aoff;
       int nrun = 0;

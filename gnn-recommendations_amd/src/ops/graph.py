@@ -31,6 +31,12 @@ TILED_PLANNER = "device"
 # gnnrec_tiled_plan_device error words: 1 negative column (the host planner's EINVAL),
 # 2 scratch too small, 3 a run longer than 2^21, 4 count / emit disagree
 _DEVICE_PLAN_ERRORS = {1: ValueError}
+# slots of one step (a panel of a block) the device planner's scratch is sized for first
+TILED_PLAN_STEP_CAP = 32768
+
+
+class _ScratchTooSmall(Exception):
+    pass
 
 
 def _np(t: torch.Tensor) -> np.ndarray:
@@ -437,11 +443,13 @@ class CsrGraph:
 
     def _tiled_plan_device(self, R: int, panel: int, sub_panel: int) -> dict:
         """gnnrec_tiled_plan_device: a counting pass, the chunk offsets by a device cumsum,
-        the emitting pass (two device reads: the chunk total and the error word)."""
+        the emitting pass (device reads: the chunk total and the error word). The scratch is
+        sized for steps of up to `cap` slots — a step is one panel of one block, far smaller
+        than the block — so every block can have its own workgroup; a step beyond it fails
+        the pass (error 2) and the pass is re-run with the block bound."""
         dev = self.device
         if dev.type != "cuda":
             raise ValueError("the device planner needs the graph on a ROCm device")
-        L = _lib.lib()
         n, W = self.n_rows, _lib.TILED_WAVES
         nb = -(-n // R)
         rp = self.row_ptr
@@ -450,19 +458,36 @@ class CsrGraph:
         max_nnz = int(bnnz.max()) if nb else 0
         if max_nnz >= (1 << 31) - 1:
             raise ValueError("tiled plan: a block holds more than 2^31 edges")
-        # one 64-lane workgroup per block at a time: up to 4 per CU, scratch at most ~4 GB
-        per_wg = 8 * L.gnnrec_tiled_plan_device_scratch_words(max_nnz, 1)
+        cap = min(max_nnz, TILED_PLAN_STEP_CAP)
+        try:
+            return self._tiled_plan_device_pass(R, panel, sub_panel, nb, cap)
+        except _ScratchTooSmall:
+            return self._tiled_plan_device_pass(R, panel, sub_panel, nb, max_nnz)
+
+    def _tiled_plan_device_pass(self, R, panel, sub_panel, nb, cap) -> dict:
+        dev = self.device
+        L = _lib.lib()
+        n, W = self.n_rows, _lib.TILED_WAVES
+        per_wg = 8 * L.gnnrec_tiled_plan_device_scratch_words(cap, 1)
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        wg = max(1, min(nb, 4 * cus, (4 << 30) // max(per_wg, 1)))
-        scratch = torch.empty(max(1, L.gnnrec_tiled_plan_device_scratch_words(max_nnz, wg)),
+        # one 64-lane workgroup per block (LDS: up to 6 per CU), scratch at most ~4 GB
+        wg = max(1, min(nb, 6 * cus, (4 << 30) // max(per_wg, 1)))
+        scratch = torch.empty(max(1, L.gnnrec_tiled_plan_device_scratch_words(cap, wg)),
                               dtype=torch.int64, device=dev)
         chunks = torch.zeros(max(1, nb * W), dtype=torch.int64, device=dev)
         n_steps = torch.zeros(max(nb, 1), dtype=torch.int32, device=dev)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
         stream = _lib.stream_of(dev)
         ptr = _lib.ptr
-        args = (ptr(rp), ptr(self.col), ptr(self.val), n, R, panel, sub_panel, max_nnz,
+        args = (ptr(self.row_ptr), ptr(self.col), ptr(self.val), n, R, panel, sub_panel, cap,
                 ptr(scratch), wg)
+
+        def failed(what, code):
+            if code == 2:
+                raise _ScratchTooSmall()
+            raise _DEVICE_PLAN_ERRORS.get(code, RuntimeError)(
+                f"gnnrec_tiled_plan_device ({what}) failed: error {code}")
+
         _lib.check(L.gnnrec_tiled_plan_device(*args, ptr(chunks), ptr(n_steps), None, None, None,
                                               None, ptr(err), stream),
                    "gnnrec_tiled_plan_device (count)")
@@ -470,8 +495,7 @@ class CsrGraph:
         torch.cumsum(chunks[:nb * W], 0, out=wave_ptr[1:])
         n_chunks, code = int(wave_ptr[-1]), int(err)
         if code:
-            raise _DEVICE_PLAN_ERRORS.get(code, RuntimeError)(
-                f"gnnrec_tiled_plan_device (count) failed: error {code}")
+            failed("count", code)
         total = n_chunks + _lib.TILED_TAIL
         slot = torch.empty(total * _lib.TILED_CHUNK, dtype=torch.int32, device=dev)
         v = torch.empty(total * _lib.TILED_CHUNK, dtype=torch.float32, device=dev)
@@ -481,8 +505,7 @@ class CsrGraph:
                    "gnnrec_tiled_plan_device (emit)")
         code = int(err)
         if code:
-            raise _DEVICE_PLAN_ERRORS.get(code, RuntimeError)(
-                f"gnnrec_tiled_plan_device (emit) failed: error {code}")
+            failed("emit", code)
         del scratch
         return dict(slot=slot, val=v, hdr=hdr, wave_ptr=wave_ptr, n_steps=n_steps,
                     n_blocks=nb, n_chunks=n_chunks)

@@ -189,9 +189,11 @@ int gnnrec_tiled_plan_free(void* plan);
  * wave_ptr = [0, cumsum(chunks)] and sizes slot / val_out / hdr for wave_ptr[last] +
  * GNNREC_TILED_TAIL chunks; the EMIT pass (wave_ptr != NULL) writes them, tail chunks
  * included. scratch: gnnrec_tiled_plan_device_scratch_words(max_block_nnz, workgroups)
- * uint64 words, max_block_nnz = the largest row_ptr[min(n_rows, (b+1) R)] - row_ptr[b R];
- * err: one device int32, zeroed by the caller, non-zero after a failed pass (1 negative
- * column, 2 scratch too small, 3 a run longer than 2^21, 4 count / emit mismatch). */
+ * uint64 words where max_block_nnz bounds the edges of one step of a block (always safe:
+ * the largest row_ptr[min(n_rows, (b+1) R)] - row_ptr[b R]; a smaller bound that a step
+ * exceeds fails the pass with error 2, to be retried with a larger one); err: one device
+ * int32, zeroed by the caller, non-zero after a failed pass (1 negative column, 2 scratch
+ * too small, 3 a run longer than 2^21, 4 count / emit mismatch). */
 int64_t gnnrec_tiled_plan_device_scratch_words(int64_t max_block_nnz, int32_t workgroups);
 int gnnrec_tiled_plan_device(const int64_t* row_ptr, const int32_t* col, const float* val,
                              int64_t n_rows, int32_t rows_per_block, int32_t panel,

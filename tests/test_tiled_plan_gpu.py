@@ -107,3 +107,16 @@ def test_device_plan_equals_host_plan_g100m(cuda):
     for p in (dev, host):
         p["n_slots"] = p["n_chunks"] * 64
     _same(dev, host)
+
+
+def test_device_plan_retries_a_small_step_cap(cuda, monkeypatch):
+    """A step larger than the scratch's step cap fails the pass (error 2) and the planner
+    re-runs it with the block bound: the same arrays."""
+    from src.ops import graph as G
+    monkeypatch.setattr(G, "TILED_PLAN_STEP_CAP", 16)
+    g = _uniform(20000, 15000, 600000, 3).to(cuda)
+    dev = g._tiled_plan_device(700, 8192, 1024)
+    host = g._tiled_plan_host(700, 8192, 1024)
+    for p in (dev, host):
+        p["n_slots"] = p["n_chunks"] * 64
+    _same(dev, host)
