@@ -84,16 +84,30 @@ __device__ __forceinline__ uint64_t wave_min64(uint64_t x) {
   return x;
 }
 
+// a 64-lane reduction by DPP inside each 16-lane row (xor 1, xor 2, half-row and row
+// mirrors), then the 4 rows by v_readlane: no LDS round trips (every lane must be active)
+template <class Op>
+__device__ __forceinline__ int wave_reduce_dpp(int x, Op op) {
+  x = op(x, __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false));    // quad_perm [1,0,3,2]
+  x = op(x, __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false));    // quad_perm [2,3,0,1]
+  x = op(x, __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false));   // row_half_mirror
+  x = op(x, __builtin_amdgcn_mov_dpp(x, 0x140, 0xF, 0xF, false));   // row_mirror
+  return op(op(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)),
+            op(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
+}
+
 __device__ __forceinline__ int wave_min32(int x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o));
-  return x;
+  return wave_reduce_dpp(x, [](int a, int b) { return min(a, b); });
 }
 
 __device__ __forceinline__ int wave_max32(int x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o));
-  return x;
+  return wave_reduce_dpp(x, [](int a, int b) { return max(a, b); });
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+  return (uint32_t)wave_reduce_dpp((int)x, [](int a, int b) {
+    return (int)min((uint32_t)a, (uint32_t)b);
+  });
 }
 
 __device__ __forceinline__ void fail(int32_t* err, int code) {
@@ -197,7 +211,10 @@ __global__ __launch_bounds__(64) void tiled_plan_kernel(PlanArgs a, int emit) {
       for (int idx = 0; idx < nk; ++idx) {
         const uint32_t key = s_key[idx];
         const int n = kPNMax - (int)(key >> kPRowBits);
-        const int v = (int)(wave_min64(((uint64_t)load << 6) | (uint32_t)lane) & 63);
+        // loads below 2^26 (nnzb bounds them): one 32-bit DPP min of load << 6 | lane
+        const int v = nnzb < (1 << 26)
+                          ? (int)(wave_min_u32((load << 6) | (uint32_t)lane) & 63)
+                          : (int)(wave_min64(((uint64_t)load << 6) | (uint32_t)lane) & 63);
         if (lane == v) {
           load += (uint32_t)n;
           s_asg[idx] = (uint8_t)v;
