@@ -130,9 +130,20 @@ __device__ unsigned long long* g_tiled_trace;
 
 struct TiledSlots {   // this lane's slot of the chunk: stream lane / 8, step lane % 8
   uint32_t w;         // slot word: (column - panel base) << kRowBits | local row
-  float v;
+  float v;            // the slot's value (a factored plan: formed at the gather stage)
   uint32_t h;         // word (lane % 4) of the chunk header
+  uint32_t c;         // a factored plan: the slot's column class
 };
+
+// Factored plans (ABI 8, DESIGN.md §3.1c "plan values"): every value of the operand is
+// fl(row_factor[r] * class_table[k]) for its column's class k (the symmetric normalisation:
+// fl(dis_r * dis_c), graph_builder.py:119-126), so a slot carries a 1-byte class instead of
+// its 4-byte value. The block's row factors and the class table sit in LDS after the
+// accumulator rows; the value is formed once per chunk per lane — the same fp32 product the
+// operand's builder stored, so the same bits.
+constexpr int kMaxClasses = GNNREC_TILED_MAX_CLASSES;
+static_assert(GNNREC_TILED_MAX_ROWS_FACTORED * (kRowBytes + 4) + kRowBytes + 4 +
+                      kMaxClasses * 4 <= 160 * 1024, "LDS of a factored plan");
 
 // Slot t of every stream to the stream's 8 lanes: within a 16-lane DPP row, lanes 0-7 (stream
 // 2k) take row lane t, lanes 8-15 (stream 2k+1) row lane 8 + t.
@@ -154,15 +165,28 @@ __device__ __forceinline__ float gbcastf(float v) {
 // chunk c of the plan: this lane's slot word and value, and header word lane % 4 (three
 // coalesced vector loads; same-box A/B: separate 128-B-aligned arrays beat one interleaved
 // 528-B chunk stream by 4 %, profiles/r03/ab_interleaved_plan_vs_separate_fixed_range.txt)
+template <bool FACT>
 __device__ __forceinline__ void tiled_slots(const uint32_t* __restrict__ ss,
                                             const float* __restrict__ sv,
+                                            const uint8_t* __restrict__ sc,
                                             const uint32_t* __restrict__ hdr, int64_t c, int lane,
                                             TiledSlots& m) {
   if (GNNREC_TILED_EXP & 8) c &= 63;
   const int64_t i = c * kTiledChunk + lane;
   m.w = ss[i];   // default policy: nt plan loads measured 1 % slower (exp_plan_nt.jsonl)
-  m.v = sv[i];
+  if constexpr (FACT)
+    m.c = sc[i];
+  else
+    m.v = sv[i];
   m.h = hdr[4 * c + (lane & 3)];
+}
+
+// a factored plan's slot value (rows past the block's, e.g. of prefetched chunks beyond the
+// wave's range, read the scratch row's 0 factor)
+template <bool FACT>
+__device__ __forceinline__ void slot_value(TiledSlots& m, const float* rfl, const float* ctl,
+                                           uint32_t R) {
+  if constexpr (FACT) m.v = __fmul_rn(rfl[min(m.w & kRowMask, R)], ctl[m.c]);
 }
 
 template <int W>
@@ -385,9 +409,11 @@ __device__ __forceinline__ void run_ring(std::integer_sequence<int, I...>, F&& s
     if ((stage(std::integral_constant<int, I>{}) || ...)) break;
 }
 
+template <bool FACT>
 __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     const uint32_t* __restrict__ ss, const float* __restrict__ sv,
-    const uint32_t* __restrict__ hdr, const int64_t* __restrict__ wptr,
+    const uint8_t* __restrict__ sc, const float* __restrict__ rowf,
+    const float* __restrict__ ctab, int n_classes, const uint32_t* __restrict__ hdr, const int64_t* __restrict__ wptr,
     const int32_t* __restrict__ nsteps, int n_blocks, int nb_pad, int n_items, int R,
     const float* __restrict__ x, uint32_t x_rows32, uint32_t row_bytes,
     float* __restrict__ y, uint32_t ldy4, int n_rows, int epi, const float* __restrict__ self,
@@ -396,6 +422,12 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     unsigned meet_ticks) {
   extern __shared__ f4 acc4[];   // [(R+1)][32] floats: row R is the padding slots' scratch row
   float* acc = reinterpret_cast<float*>(acc4);
+  // factored plans: the block's row factors [R+1] (row R: 0) and the class table [kMaxClasses]
+  float* rfl = acc + (R + 1) * kSlice;
+  float* ctl = rfl + (R + 1);
+  if constexpr (FACT)
+    for (int i = threadIdx.x; i < kMaxClasses; i += kTiledWaves * 64)
+      ctl[i] = i < n_classes ? ctab[i] : 0.f;   // read after the first pass-start barrier
   constexpr auto kSeq = std::make_integer_sequence<int, kSteps>{};
   const int lane = threadIdx.x & 63;
   const uint32_t q16 = (uint32_t)(lane & 7) * 16;
@@ -421,6 +453,11 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     {
       const f4 z = {0.f, 0.f, 0.f, 0.f};
       for (int i = threadIdx.x; i < (R + 1) * (kSlice / 4); i += kTiledWaves * 64) acc4[i] = z;
+      if constexpr (FACT) {
+        const int r0 = blk * R;
+        for (int i = threadIdx.x; i <= R; i += kTiledWaves * 64)
+          rfl[i] = (i < R && r0 + i < n_rows) ? rowf[r0 + i] : 0.f;
+      }
     }
     __syncthreads();
     GNNREC_TILED_STAMP(ev);
@@ -439,18 +476,21 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
       const int nc = (int)(e - b);   // this wave's chunks of the pass
       int c = 0;
 #pragma unroll
-      for (int j = 0; j < kPlanAhead; ++j) tiled_slots(ss, sv, hdr, b + c + j, lane, M[j]);
+      for (int j = 0; j < kPlanAhead; ++j) tiled_slots<FACT>(ss, sv, sc, hdr, b + c + j, lane, M[j]);
 #pragma unroll
-      for (int j = 0; j < kGatherAhead; ++j)
+      for (int j = 0; j < kGatherAhead; ++j) {
         tiled_gather(kSeq, chunk_rsrc(xs, xs_bytes, hdr_word<3>(M[j]), row_bytes), q16,
                      row_bytes, M[j], X[j]);
+        slot_value<FACT>(M[j], rfl, ctl, (uint32_t)R);
+      }
       auto stage = [&](auto ic) -> bool {
         constexpr int I = decltype(ic)::value;
-        tiled_slots(ss, sv, hdr, b + c + kPlanAhead, lane, M[(I + kPlanAhead) % kMRing]);
+        tiled_slots<FACT>(ss, sv, sc, hdr, b + c + kPlanAhead, lane, M[(I + kPlanAhead) % kMRing]);
         {
-          const TiledSlots& mg = M[(I + kGatherAhead) % kMRing];
+          TiledSlots& mg = M[(I + kGatherAhead) % kMRing];
           tiled_gather(kSeq, chunk_rsrc(xs, xs_bytes, hdr_word<3>(mg), row_bytes), q16,
                        row_bytes, mg, X[(I + kGatherAhead) % kXRing]);
+          slot_value<FACT>(mg, rfl, ctl, (uint32_t)R);
         }
         const TiledSlots& ma = M[I % kMRing];
         const int bar = (int)hdr_word<0>(ma);
@@ -784,9 +824,11 @@ int tiled_lds_attribute(int dev) {
   std::lock_guard<std::mutex> lock(mu);
   if ((int)done.size() <= dev) done.resize(dev + 1, 0);
   if (done[dev] == 0) {
-    const hipError_t e = hipFuncSetAttribute((const void*)tiled_hop_kernel,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             160 * 1024);
+    hipError_t e = hipFuncSetAttribute((const void*)tiled_hop_kernel<false>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)tiled_hop_kernel<true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     done[dev] = e == hipSuccess ? 1 : -1;
     if (e != hipSuccess) (void)hipGetLastError();
   }
@@ -806,6 +848,8 @@ extern "C" int gnnrec_spmm_tiled_supported(int32_t device, int32_t rows_per_bloc
 }
 
 extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
+                                     const uint8_t* slot_class, const float* row_factor,
+                                     const float* class_table, int32_t n_classes,
                                      const uint32_t* hdr, const int64_t* wave_ptr,
                                      const int32_t* n_steps, int64_t n_blocks,
                                      int32_t rows_per_block, const float* x, int64_t x_rows,
@@ -843,12 +887,18 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
   GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_DIV) || (epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)),
                  "spmm_tiled: ACC_DIV needs ACC_INIT or ACC_ADD");
   GNNREC_REQUIRE(meet_us >= 0 && meet_us <= 100000, "spmm_tiled: meet_us must be in [0, 1e5]");
+  const bool fact = slot_class != nullptr;
+  GNNREC_REQUIRE(!fact || (row_factor && class_table && n_classes >= 1 &&
+                           n_classes <= kMaxClasses &&
+                           rows_per_block <= GNNREC_TILED_MAX_ROWS_FACTORED),
+                 "spmm_tiled: a factored plan needs row_factor, class_table, 1 <= n_classes <= "
+                 "%d and rows_per_block <= %d", kMaxClasses, GNNREC_TILED_MAX_ROWS_FACTORED);
   constexpr int64_t kMaxLd = ((int64_t)1 << 32) / (4 * 4096);   // epilogue row offsets: 32-bit
   GNNREC_REQUIRE(ldy <= kMaxLd && ld_self <= kMaxLd && ld_acc <= kMaxLd && ld_prev <= kMaxLd,
                  "spmm_tiled: output / self / acc row strides must be <= %lld",
                  (long long)kMaxLd);
   if (n_rows == 0) return GNNREC_OK;
-  GNNREC_REQUIRE(slot && val && hdr && wave_ptr && n_steps && x && sync,
+  GNNREC_REQUIRE(slot && (val || fact) && hdr && wave_ptr && n_steps && x && sync,
                  "spmm_tiled: null pointer");
   GNNREC_REQUIRE(aligned16(x) && ((epi & GNNREC_EPI_NO_Y) || aligned16(y)) &&
                      (!(epi & GNNREC_EPI_ACC_INIT) || aligned16(self)) &&
@@ -859,7 +909,8 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 256;
-  const size_t lds = (size_t)(rows_per_block + 1) * kRowBytes;
+  const size_t lds = (size_t)(rows_per_block + 1) * kRowBytes +
+                     (fact ? (size_t)(rows_per_block + 1) * 4 + kMaxClasses * 4 : 0);
   if (lds > 64 * 1024 && tiled_lds_attribute(dev) < 0) {
     set_error("spmm_tiled: the device refused %zu bytes of dynamic LDS", lds);
     return GNNREC_EHIP;
@@ -871,12 +922,76 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
                  "spmm_tiled: too many blocks / rows");
   if (hipMemsetAsync(sync, 0, GNNREC_TILED_SYNC_WORDS * sizeof(uint32_t), s) != hipSuccess)
     return check_launch("spmm_tiled (sync reset)");
-  hipLaunchKernelGGL(tiled_hop_kernel, dim3((unsigned)grid), dim3(kTiledWaves * 64), lds, s,
-                     slot, val, hdr, wave_ptr, n_steps,
+  hipLaunchKernelGGL(fact ? tiled_hop_kernel<true> : tiled_hop_kernel<false>, dim3((unsigned)grid),
+                     dim3(kTiledWaves * 64), lds, s, slot, val, slot_class, row_factor,
+                     class_table, (int)n_classes, hdr, wave_ptr, n_steps,
                      (int)n_blocks, (int)nb_pad, (int)n_items, (int)rows_per_block, x,
                      (uint32_t)x_rows, (uint32_t)(ldx * 4), y, (uint32_t)(ldy * 4),
                      (int)n_rows, epi, self, (uint32_t)(ld_self * 4), acc, (uint32_t)(ld_acc * 4),
                      acc_div, prev, (uint32_t)(ld_prev * 4), sync,
                      (unsigned)meet_us * 100u /* wall_clock64 runs at 100 MHz */);
   return check_launch("spmm_tiled");
+}
+
+// ---- factored plans (ABI 8) ----------------------------------------------------------------
+namespace gnnrec {
+namespace {
+// One workgroup per (block, wave) run of chunks: each real slot's class is its column's class,
+// and its value must be fl(row_factor[row] * class_table[class]) bit for bit — any slot that
+// is not counts one mismatch (the caller then keeps the explicit values). Padding slots
+// (row field = rows_per_block) get class 0; their products land in the scratch row.
+__global__ __launch_bounds__(256) void tiled_factor_kernel(
+    const uint32_t* __restrict__ slot, const float* __restrict__ val,
+    const uint32_t* __restrict__ hdr, const int64_t* __restrict__ wave_ptr, int R,
+    int64_t n_rows, int64_t n_cols, const float* __restrict__ rowf,
+    const uint8_t* __restrict__ col_class, const float* __restrict__ ctab, int n_classes,
+    uint8_t* __restrict__ cls, unsigned* __restrict__ bad) {
+  const int64_t s = blockIdx.x;
+  const int64_t blk = s / kTiledWaves;
+  const int64_t e = wave_ptr[s + 1] * kTiledChunk;
+  unsigned miss = 0;
+  for (int64_t i = wave_ptr[s] * kTiledChunk + threadIdx.x; i < e; i += blockDim.x) {
+    const uint32_t w = slot[i];
+    const uint32_t row = w & kRowMask;
+    uint8_t k = 0;
+    if (row < (uint32_t)R) {
+      const int64_t col = (int64_t)hdr[4 * (i / kTiledChunk) + 3] + (w >> kRowBits);
+      const int64_t r = blk * R + row;
+      bool ok = col < n_cols && r < n_rows;
+      if (ok) {
+        k = col_class[col];
+        ok = k < n_classes &&
+             __float_as_uint(__fmul_rn(rowf[r], ctab[k])) == __float_as_uint(val[i]);
+      }
+      miss += ok ? 0u : 1u;
+    }
+    cls[i] = k;
+  }
+  if (miss) atomicAdd(bad, miss);
+}
+}  // namespace
+}  // namespace gnnrec
+
+extern "C" int gnnrec_tiled_plan_factor(const uint32_t* slot, const float* val,
+                                        const uint32_t* hdr, const int64_t* wave_ptr,
+                                        int64_t n_blocks, int32_t rows_per_block, int64_t n_rows,
+                                        int64_t n_cols, const float* row_factor,
+                                        const uint8_t* col_class, const float* class_table,
+                                        int32_t n_classes, uint8_t* slot_class,
+                                        uint32_t* mismatches, gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(n_blocks >= 0 && rows_per_block >= 1 &&
+                     rows_per_block <= GNNREC_TILED_MAX_ROWS && n_rows >= 0 && n_cols >= 0,
+                 "tiled_factor: bad sizes");
+  GNNREC_REQUIRE(n_classes >= 1 && n_classes <= kMaxClasses,
+                 "tiled_factor: n_classes must be in [1, %d]", kMaxClasses);
+  if (n_blocks == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(slot && val && hdr && wave_ptr && row_factor && col_class && class_table &&
+                     slot_class && mismatches,
+                 "tiled_factor: null pointer");
+  const int64_t segs = n_blocks * kTiledWaves;
+  GNNREC_REQUIRE(segs < INT32_MAX, "tiled_factor: too many blocks");
+  hipLaunchKernelGGL(tiled_factor_kernel, dim3((unsigned)segs), dim3(256), 0, as_hip(stream),
+                     slot, val, hdr, wave_ptr, (int)rows_per_block, n_rows, n_cols, row_factor,
+                     col_class, class_table, (int)n_classes, slot_class, mismatches);
+  return check_launch("tiled_factor");
 }

@@ -17,7 +17,7 @@ import torch  # noqa: F401  (load order: torch's HIP runtime first)
 
 _PKG_ROOT = Path(__file__).resolve().parents[2]
 LIB_PATH = Path(os.environ.get("GNNREC_LIB", _PKG_ROOT / "lib" / "libgnnrec.so"))
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # gnnrec.h epilogue flags
 EPI_ACC_INIT = 1
@@ -36,6 +36,8 @@ TILED_SYNC_WORDS = 256
 TILED_HDR_WORDS = 4
 TILED_MAX_LDX = 1024
 TILED_MAX_PANEL = 1 << 20
+TILED_MAX_CLASSES = 256
+TILED_MAX_ROWS_FACTORED = 1232
 
 _p = C.c_void_p
 _i64 = C.c_int64
@@ -62,7 +64,10 @@ _SIGNATURES = {
     "gnnrec_tiled_plan_device": [_p, _p, _p, _i64, _i32, _i32, _i32, _i64, _p, _i32, _p, _p, _p,
                                  _p, _p, _p, _p, _p],
     "gnnrec_spmm_tiled_supported": [_i32, _i32],
-    "gnnrec_spmm_tiled_f32": [_p, _p, _p, _p, _p, _i64, _i32, _p, _i64, _i64, _p, _i64,
+    "gnnrec_tiled_plan_factor": [_p, _p, _p, _p, _i64, _i32, _i64, _i64, _p, _p, _p, _i32, _p,
+                                 _p, _p],
+    "gnnrec_spmm_tiled_f32": [_p, _p, _p, _p, _p, _i32, _p, _p, _p, _i64, _i32, _p, _i64, _i64,
+                              _p, _i64,
                               _i64, _i32, _i32, _p, _i64, _p, _i64, _f32, _p, _i64, _p, _i32, _p],
     "gnnrec_row_nonzero_f32": [_p, _i64, _i64, _i32, _p, _p],
     "gnnrec_lightgcn_split_f32": [_p, _p, _p, _i64, _p, _i32, _i32, _p, _p, _p, _p, _i64, _p,

@@ -185,7 +185,10 @@ def spmm_tiled_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], p
     _require_device(adj, x, y, self_rows, acc, prev)
     d = x.shape[1]
     check(_lib.lib().gnnrec_spmm_tiled_f32(
-        ptr(plan["slot"]), ptr(plan["val"]), ptr(plan["hdr"]), ptr(plan["wave_ptr"]), ptr(plan["n_steps"]), plan["n_blocks"], plan["rows_per_block"],
+        ptr(plan["slot"]), ptr(plan.get("val")), ptr(plan.get("cls")),
+        ptr(plan.get("row_factor")), ptr(plan.get("class_table")), int(plan.get("n_classes", 0)),
+        ptr(plan["hdr"]), ptr(plan["wave_ptr"]), ptr(plan["n_steps"]), plan["n_blocks"],
+        plan["rows_per_block"],
         ptr(x), x.shape[0], x.stride(0), ptr(y), y.stride(0) if y is not None else d, adj.n_rows,
         d, epi, ptr(self_rows), self_rows.stride(0) if self_rows is not None else d, ptr(acc),
         acc.stride(0) if acc is not None else d, float(acc_div), ptr(prev),

@@ -33,6 +33,10 @@ TILED_PLANNER = "device"
 _DEVICE_PLAN_ERRORS = {1: ValueError}
 # slots of one step (a panel of a block) the device planner's scratch is sized for first
 TILED_PLAN_STEP_CAP = 32768
+# factored plans (gnnrec_tiled_plan_factor, DESIGN.md §3.1c "plan values"): a device graph's
+# plan carries 1-byte column classes instead of fp32 values whenever every value is
+# fl(dis_r * dis_c) with dis from the row counts and at most TILED_MAX_CLASSES distinct dis
+TILED_FACTOR = True
 
 
 class _ScratchTooSmall(Exception):
@@ -110,6 +114,9 @@ class CsrGraph:
                      self.col.to(device, non_blocking=non_blocking),
                      self.val.to(device, non_blocking=non_blocking), self.shape, self.n_users,
                      self.n_items, self.symmetric, self.shard_info)
+        f = self._plans.get("degree_factors")
+        if f is not None:   # a shard's factors come from its full graph (shard())
+            g._plans["degree_factors"] = tuple(t.to(device) for t in f)
         return g
 
     def cuda(self, device=None) -> "CsrGraph":
@@ -346,6 +353,16 @@ class CsrGraph:
         g = CsrGraph(rp_t, col_t, val_t, (hi - lo, rows_pad * world),
                      self.n_users, self.n_items, False,
                      ShardInfo(rank, world, lo, hi, rows_pad, bounds))
+        f = self.degree_factors() if world > 1 else None
+        if f is not None:
+            # the full graph's factors in the shard's layout: its rows, and the column classes
+            # moved to the padded gather layout (padding columns are never referenced)
+            rowf, cc, table = (t.cpu() for t in f)
+            pad = torch.zeros(rows_pad * world, dtype=torch.uint8)
+            for q in range(world):
+                pad[q * rows_pad:q * rows_pad + bounds[q + 1] - bounds[q]] = \
+                    cc[bounds[q]:bounds[q + 1]]
+            g._plans["degree_factors"] = (rowf[lo:hi].clone(), pad, table)
         return g.to(self.device)
 
     def row_slice(self, r0: int, r1: int) -> "CsrGraph":
@@ -353,9 +370,12 @@ class CsrGraph:
         so per-view plans (heavy rows) are computed once."""
         key = ("slice", r0, r1)
         if key not in self._plans:
-            self._plans[key] = CsrGraph(self.row_ptr[r0:r1 + 1], self.col, self.val,
-                                        (r1 - r0, self.shape[1]), self.n_users, self.n_items,
-                                        False, self.shard_info)
+            v = CsrGraph(self.row_ptr[r0:r1 + 1], self.col, self.val,
+                         (r1 - r0, self.shape[1]), self.n_users, self.n_items,
+                         False, self.shard_info)
+            f = self.degree_factors()
+            v._plans["degree_factors"] = None if f is None else (f[0][r0:r1], f[1], f[2])
+            self._plans[key] = v
         return self._plans[key]
 
     def heavy_rows(self, threshold: int) -> Optional[torch.Tensor]:
@@ -405,8 +425,63 @@ class CsrGraph:
                         n_slots=plan["n_chunks"] * _lib.TILED_CHUNK,
                         sync=torch.zeros(_lib.TILED_SYNC_WORDS, dtype=torch.int32,
                                          device=self.device))
+            if (TILED_FACTOR and self.device.type == "cuda"
+                    and int(rows_per_block) <= _lib.TILED_MAX_ROWS_FACTORED):
+                self._factor_plan(plan)
             self._plans[key] = plan
         return self._plans[key]
+
+    def degree_factors(self):
+        """(row_factor [n_rows], col_class uint8 [n_cols], class_table [n_classes]) on this
+        device, or None (cached): the symmetric normalisation's dis = float32(deg)^-0.5 exactly
+        as inv_sqrt_degrees (graph_builder.py:111-131) with deg = the row's stored-entry
+        count (a binary interaction graph), when the operand is square and dis takes at most
+        TILED_MAX_CLASSES distinct values. A guess: gnnrec_tiled_plan_factor checks every
+        value against it bit for bit before a plan drops its values."""
+        if "degree_factors" not in self._plans:
+            out = None
+            n, m = self.shape
+            info = self.shard_info
+            # node-indexed columns: a square operand, or the identity layout of one shard
+            # (columns padded to a multiple of 4); shards of several ranks get theirs from
+            # their full graph (shard())
+            node_cols = (n == m and info is None) or (info is not None and info.world == 1
+                                                      and m >= n)
+            if node_cols and self.row_ptr.numel() == n + 1 and self.nnz > 0:
+                deg = (self.row_ptr[1:] - self.row_ptr[:-1]).cpu().numpy().astype(np.float32)
+                dis = inv_sqrt_degrees(deg, "symmetric")
+                table = np.unique(dis)
+                if table.size <= _lib.TILED_MAX_CLASSES:
+                    cls = np.zeros(m, np.uint8)
+                    cls[:n] = np.searchsorted(table, dis)
+                    dev = self.device
+                    out = (torch.from_numpy(dis).to(dev), torch.from_numpy(cls).to(dev),
+                           torch.from_numpy(table).to(dev))
+            self._plans["degree_factors"] = out
+        return self._plans["degree_factors"]
+
+    def _factor_plan(self, plan: dict) -> bool:
+        """Replace the plan's fp32 values by 1-byte column classes when every real slot's value
+        is fl(row_factor[r] * class_table[class]) bit for bit (gnnrec_tiled_plan_factor);
+        otherwise the plan keeps its values. Returns whether it was factored."""
+        f = self.degree_factors()
+        if f is None:
+            return False
+        rowf, col_class, table = f
+        L = _lib.lib()
+        dev = self.device
+        cls = torch.zeros(plan["slot"].numel(), dtype=torch.uint8, device=dev)
+        bad = torch.zeros(1, dtype=torch.int32, device=dev)
+        _lib.check(L.gnnrec_tiled_plan_factor(
+            _lib.ptr(plan["slot"]), _lib.ptr(plan["val"]), _lib.ptr(plan["hdr"]),
+            _lib.ptr(plan["wave_ptr"]), plan["n_blocks"], plan["rows_per_block"], self.n_rows,
+            self.shape[1], _lib.ptr(rowf), _lib.ptr(col_class), _lib.ptr(table), table.numel(),
+            _lib.ptr(cls), _lib.ptr(bad), _lib.stream_of(dev)), "gnnrec_tiled_plan_factor")
+        if int(bad):
+            return False
+        del plan["val"]
+        plan.update(cls=cls, row_factor=rowf, class_table=table, n_classes=int(table.numel()))
+        return True
 
     def _tiled_plan_host(self, R: int, panel: int, sub_panel: int) -> dict:
         import ctypes as C

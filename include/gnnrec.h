@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GNNREC_ABI_VERSION 7
+#define GNNREC_ABI_VERSION 8
 
 typedef struct ihipStream_t* gnnrec_stream_t;
 
@@ -174,6 +174,8 @@ int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col, const
 #define GNNREC_TILED_SYNC_WORDS 256
 #define GNNREC_TILED_HDR_WORDS 4
 #define GNNREC_TILED_MAX_LDX 1024
+#define GNNREC_TILED_MAX_CLASSES 256
+#define GNNREC_TILED_MAX_ROWS_FACTORED 1232
 
 int gnnrec_tiled_plan_build(const int64_t* row_ptr, const int32_t* col, const float* val,
                             int64_t n_rows, int32_t rows_per_block, int32_t panel,
@@ -207,7 +209,27 @@ int gnnrec_tiled_plan_device(const int64_t* row_ptr, const int32_t* col, const f
  * then keeps the row-parallel hop (gnnrec_spmm_csr_masked_f32). */
 int gnnrec_spmm_tiled_supported(int32_t device, int32_t rows_per_block);
 
-int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val, const uint32_t* hdr,
+/* Factored plans (ABI 8): when every value of the operand is fl(row_factor[r] *
+ * class_table[k]) for a class k of its column (the symmetric normalisation fl(dis_r * dis_c)
+ * of graph_builder.py:119-126 when the column degrees take at most GNNREC_TILED_MAX_CLASSES
+ * distinct values), a slot carries the 1-byte class instead of its 4-byte value: 5.25 instead
+ * of 8.25 plan bytes per slot, the value formed in the kernel as the same fp32 product (same
+ * bits). gnnrec_tiled_plan_factor derives slot_class [(n_chunks + TAIL) * CHUNK, zeroed by the
+ * caller] from a plan and col_class [n_cols] and counts into *mismatches (a device uint32,
+ * zeroed by the caller) every real slot whose value is not that product; with zero
+ * mismatches gnnrec_spmm_tiled_f32 may take slot_class, row_factor [n_rows], class_table
+ * [n_classes] and val = NULL (rows_per_block <= GNNREC_TILED_MAX_ROWS_FACTORED: the factors
+ * share the LDS). slot_class = NULL: explicit values, the other three are ignored. */
+int gnnrec_tiled_plan_factor(const uint32_t* slot, const float* val, const uint32_t* hdr,
+                             const int64_t* wave_ptr, int64_t n_blocks, int32_t rows_per_block,
+                             int64_t n_rows, int64_t n_cols, const float* row_factor,
+                             const uint8_t* col_class, const float* class_table,
+                             int32_t n_classes, uint8_t* slot_class, uint32_t* mismatches,
+                             gnnrec_stream_t stream);
+
+int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val, const uint8_t* slot_class,
+                          const float* row_factor, const float* class_table, int32_t n_classes,
+                          const uint32_t* hdr,
                           const int64_t* wave_ptr, const int32_t* n_steps, int64_t n_blocks,
                           int32_t rows_per_block, const float* x, int64_t x_rows, int64_t ldx,
                           float* y, int64_t ldy, int64_t n_rows, int32_t d, int32_t epi,

@@ -101,7 +101,7 @@ def test_partition_covers_rows_and_remaps_columns(world):
 def _walk_tiled_plan(plan, n_rows, R):
     """Replay gnnrec_spmm_tiled_f32's schedule on the host: per row, the (col, val) sequence
     its accumulator receives, in kernel order; checks the plan's structural rules on the way
-    (include/gnnrec.h, ABI 7: chunks of 8 steps x 8 slot streams, entry 8 g + t = slot t of
+    (include/gnnrec.h, ABI 8 (7): chunks of 8 steps x 8 slot streams, entry 8 g + t = slot t of
     stream g; per-chunk {barriers, chain mask lo, hi, panel base}; slot word = (col - base) <<
     11 | row; a row at most one run per group of 4 slots of a stream; every slot of a chunk
     inside its panel)."""

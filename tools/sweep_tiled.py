@@ -15,6 +15,10 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(ROOT / "gnn-recommendations_amd"), str(ROOT)]
 import bench  # noqa: E402
 from src.ops import functional as F  # noqa: E402
+from src.ops import graph as G  # noqa: E402
+
+if __import__("os").environ.get("TILED_FACTOR") == "0":   # explicit-value plans (A/B)
+    G.TILED_FACTOR = False
 
 args = sys.argv[1:]
 D, LDX, FOLD = 64, None, 0
@@ -61,7 +65,7 @@ for spec in args:
     exact = bool(torch.equal(y.view(torch.int32), ref.view(torch.int32)))
     times.sort()
     print(json.dumps({"d": D, "ldx": LDX, "fold": FOLD, "R": R, "panel": panel, "sub_panel": sub, "meet_us": meet,
-                      "n_blocks": plan["n_blocks"],
+                      "n_blocks": plan["n_blocks"], "factored": "cls" in plan,
                       "pad": plan["n_slots"] / g.nnz - 1, "ms_median": times[len(times) // 2],
                       "ms_min": times[0], "bit_exact": exact, "plan_s": round(t_plan, 1)}),
           flush=True)

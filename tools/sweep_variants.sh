@@ -9,6 +9,8 @@ if [ "${1:-}" = "--fold" ]; then EXTRA="--fold $2"; shift 2; fi
 : > "$OUT"
 for spec in "$@"; do
   name=${spec%%=*}; lib=${spec#*=}
+  # name suffix "_explicit": the same library with explicit-value plans
+  case "$name" in *_explicit) export TILED_FACTOR=0 ;; *) unset TILED_FACTOR ;; esac
   GNNREC_LIB=$lib timeout -k 10 200 python -u tools/sweep_tiled.py $EXTRA $SHAPE 2>&1 \
     | grep "^{" | sed "s/^{/{\"variant\": \"$name\", /" >> "$OUT" || { echo "variant $name failed"; exit 1; }
 done
