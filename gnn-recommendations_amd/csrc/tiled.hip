@@ -402,13 +402,6 @@ __device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, 
   }
 }
 
-#ifndef GNNREC_TILED_MIDMEET
-#define GNNREC_TILED_MIDMEET 0   // experiment: the XCD group also meets every N step barriers
-#endif
-#ifndef GNNREC_TILED_MIDMEET_US
-#define GNNREC_TILED_MIDMEET_US 20
-#endif
-
 // the main loop unrolled over one turn of the pipeline rings (compile-time ring indices)
 template <class F, int... I>
 __device__ __forceinline__ void run_ring(std::integer_sequence<int, I...>, F&& stage) {
@@ -441,23 +434,6 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   unsigned* ctr = sync + (blockIdx.x % 8) * 32;   // the group's counter, own 128-B line
   const int G = gridDim.x / 8 + ((blockIdx.x % 8) < (gridDim.x % 8) ? 1 : 0);
-  unsigned mid_meets = 0;
-  // step barrier number b of the pass (1-based); experiment builds also meet the XCD group
-  auto step_barrier = [&](int b, int ns) {
-    __syncthreads();
-    if (GNNREC_TILED_MIDMEET > 0 && meet_ticks > 0 && b % (GNNREC_TILED_MIDMEET > 0 ? GNNREC_TILED_MIDMEET : 1) == 0 && b < ns) {
-      ++mid_meets;
-      if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long t0 = wall_clock64();
-        while (__hip_atomic_load(ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                   (unsigned)G * mid_meets &&
-               wall_clock64() - t0 < (unsigned long long)GNNREC_TILED_MIDMEET_US * 100)
-          __builtin_amdgcn_s_sleep(1);
-      }
-      __syncthreads();
-    }
-  };
   int pass = 0;
 #ifdef GNNREC_TILED_TRACE
   int ev = 0;
@@ -490,7 +466,6 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     const uint64_t xs_bytes = (uint64_t)x_rows32 * row_bytes - soff;
     const int64_t s = (int64_t)blk * kTiledWaves + w;
     const int64_t b = wptr[s], e = (GNNREC_TILED_EXP & 32) ? b : wptr[s + 1];
-    const int ns = nsteps[blk];
     int cur = 0;
     f4 sink = {0.f, 0.f, 0.f, 0.f};   // diagnostic builds only (GNNREC_TILED_EXP & 1)
     if (b < e) {
@@ -520,7 +495,7 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
         const TiledSlots& ma = M[I % kMRing];
         const int bar = (int)hdr_word<0>(ma);
         for (int i = 0; i < bar; ++i) {
-          if (!(GNNREC_TILED_EXP & 4)) step_barrier(cur + i + 1, ns);
+          if (!(GNNREC_TILED_EXP & 4)) __syncthreads();
           GNNREC_TILED_STAMP(ev);
         }
         cur += bar;
@@ -535,9 +510,10 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
       run_ring(std::make_integer_sequence<int, kRingUnroll>{}, stage);
     }
     if (GNNREC_TILED_EXP & 1) *reinterpret_cast<f4*>(reinterpret_cast<char*>(acc) + R * kRowBytes + q16) = sink;
+    const int ns = nsteps[blk];
     auto wait = [&]() {
       for (int i = cur; i < ns; ++i) {  // this wave's remaining steps + the last
-        step_barrier(i + 1, ns);
+        __syncthreads();
         GNNREC_TILED_STAMP(ev);
       }
     };
