@@ -297,6 +297,10 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
   __shared__ __attribute__((aligned(16))) float b_lds[KD * LDB];
   __shared__ __attribute__((aligned(16))) float g_lds[MODE == 0 ? D * LDB : 4];
   __shared__ __attribute__((aligned(16))) float t_lds[NW][TSZ];
+  // GAS with 8x8 blocks on the VALU (below): the blocks [b][c][e] and the inverse permutation
+  constexpr int kVbs = 8;
+  __shared__ __attribute__((aligned(16))) float wv_lds[MODE == 0 ? D * kVbs : 4];
+  __shared__ int inv_lds[MODE == 0 ? D : 1];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -310,7 +314,15 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
     b_lds[k * LDB + j] = v;
   }
   const bool gas = MODE == 0 && p.gas_blocks != nullptr;
-  if (gas) {   // G[k][j] = blockdiag(blocks)[k][perm[j]]
+  // 8x8 blocks: the GAS product runs on the VALU, 8 fmaf per output in the oracle's order
+  // (oracle_gas: c ascending from +0), instead of as a dense 64x64 MFMA product that spends 7/8
+  // of its work on zeros — a third of the kernel's matrix-core time (profiles/r02/
+  // config3_transform_mfma_pmc.json: 24M MFMA per launch, 8M of them GAS)
+  const bool gas_valu = gas && p.gas_bs == kVbs;
+  if (gas_valu) {
+    for (int e = threadIdx.x; e < D * kVbs; e += 64 * NW) wv_lds[e] = p.gas_blocks[e];
+    for (int j = threadIdx.x; j < D; j += 64 * NW) inv_lds[p.gas_perm[j]] = j;
+  } else if (gas) {   // G[k][j] = blockdiag(blocks)[k][perm[j]]
     const int bs = p.gas_bs;
     for (int e = threadIdx.x; e < D * D; e += 64 * NW) {
       const int k = e / D, j = e % D;
@@ -401,7 +413,36 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
         }
         ot[(4 * k4 + q) * LDO + 16 * nt + i16] = v;
       }
-    if (gas) {   // out = o @ G on the matrix cores, k ascending (== gas_row_v's chain)
+    if (gas_valu) {
+      // lane (i16, k4): z = GAS of row i16's columns 16 k4 .. 16 k4 + 15 (two 8-blocks), then
+      // z[t] to column inv[16 k4 + t] of the same row; the wave's LDS operations run in order,
+      // so every lane's reads of the row precede the scattered writes
+      float ov[16], z[16];
+      const float* orow = ot + i16 * LDO + 16 * k4;
+#pragma unroll
+      for (int t4 = 0; t4 < 4; ++t4) {
+        const float4 v = *reinterpret_cast<const float4*>(orow + 4 * t4);
+        ov[4 * t4] = v.x; ov[4 * t4 + 1] = v.y; ov[4 * t4 + 2] = v.z; ov[4 * t4 + 3] = v.w;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float* W = wv_lds + (16 * k4 + kVbs * h) * kVbs;   // block 2 k4 + h
+#pragma unroll
+        for (int e = 0; e < kVbs; ++e) z[kVbs * h + e] = 0.f;
+#pragma unroll
+        for (int c = 0; c < kVbs; ++c) {
+          const float4 w0 = *reinterpret_cast<const float4*>(W + c * kVbs);
+          const float4 w1 = *reinterpret_cast<const float4*>(W + c * kVbs + 4);
+          const float wc[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+          const float x = ov[kVbs * h + c];
+#pragma unroll
+          for (int e = 0; e < kVbs; ++e) z[kVbs * h + e] = __builtin_fmaf(x, wc[e], z[kVbs * h + e]);
+        }
+      }
+      float* wrow = ot + i16 * LDO;
+#pragma unroll
+      for (int t = 0; t < 16; ++t) wrow[inv_lds[16 * k4 + t]] = z[t];
+    } else if (gas) {   // out = o @ G on the matrix cores, k ascending (== gas_row_v's chain)
       floatx4 cg[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) cg[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
