@@ -285,7 +285,7 @@ __global__ __launch_bounds__(64 * NW) void spmm_mfma_kernel(DenseParams p) {
 // GAS product on the matrix cores, and stores whole rows (float4). The next tile's rows are in
 // flight in registers meanwhile. Same MFMA instructions, fragment maps and k order as
 // spmm_mfma_kernel<64, MODE, 8, false>, so the same bits.
-template <int MODE, int NW>
+template <int MODE, int NW, bool GASV>
 __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
   constexpr int D = 64;
   constexpr int KD = MODE == 0 ? 2 * D : D;
@@ -295,12 +295,12 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
   constexpr int STEPS = KD / 4;
   constexpr int TSZ = 16 * (LDA > LDO ? LDA : LDO);   // the o tile aliases the A tile
   __shared__ __attribute__((aligned(16))) float b_lds[KD * LDB];
-  __shared__ __attribute__((aligned(16))) float g_lds[MODE == 0 ? D * LDB : 4];
+  __shared__ __attribute__((aligned(16))) float g_lds[MODE == 0 && !GASV ? D * LDB : 4];
   __shared__ __attribute__((aligned(16))) float t_lds[NW][TSZ];
   // GAS with 8x8 blocks on the VALU (below): the blocks [b][c][e] and the inverse permutation
   constexpr int kVbs = 8;
-  __shared__ __attribute__((aligned(16))) float wv_lds[MODE == 0 ? D * kVbs : 4];
-  __shared__ int inv_lds[MODE == 0 ? D : 1];
+  __shared__ __attribute__((aligned(16))) float wv_lds[MODE == 0 && GASV ? D * kVbs : 4];
+  __shared__ int inv_lds[MODE == 0 && GASV ? D : 1];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -318,11 +318,13 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
   // (oracle_gas: c ascending from +0), instead of as a dense 64x64 MFMA product that spends 7/8
   // of its work on zeros — a third of the kernel's matrix-core time (profiles/r02/
   // config3_transform_mfma_pmc.json: 24M MFMA per launch, 8M of them GAS)
-  const bool gas_valu = gas && p.gas_bs == kVbs;
+  // (GASV instances are launched for 8x8 blocks only; they hold no dense G in LDS, which
+  // leaves room for 12 waves per workgroup)
+  constexpr bool gas_valu = GASV;
   if (gas_valu) {
     for (int e = threadIdx.x; e < D * kVbs; e += 64 * NW) wv_lds[e] = p.gas_blocks[e];
     for (int j = threadIdx.x; j < D; j += 64 * NW) inv_lds[p.gas_perm[j]] = j;
-  } else if (gas) {   // G[k][j] = blockdiag(blocks)[k][perm[j]]
+  } else if (gas && !GASV) {   // G[k][j] = blockdiag(blocks)[k][perm[j]]
     const int bs = p.gas_bs;
     for (int e = threadIdx.x; e < D * D; e += 64 * NW) {
       const int k = e / D, j = e % D;
@@ -442,7 +444,7 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
       float* wrow = ot + i16 * LDO;
 #pragma unroll
       for (int t = 0; t < 16; ++t) wrow[inv_lds[16 * k4 + t]] = z[t];
-    } else if (gas) {   // out = o @ G on the matrix cores, k ascending (== gas_row_v's chain)
+    } else if (gas && !GASV) {   // out = o @ G on the matrix cores, k ascending (== gas_row_v's chain)
       floatx4 cg[4];
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) cg[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -628,17 +630,26 @@ namespace {
 //    occupancy;
 //  * fused (no workspace): gather + MFMA in one kernel.
 // Waves per workgroup: 8 for d <= 64 (weights in LDS), 4 for d = 128 (weights in VGPRs).
+#ifndef GNNREC_TRANSFORM_GASV_WAVES
+#define GNNREC_TRANSFORM_GASV_WAVES 12
+#endif
 template <int MODE, bool GATHER>
 int launch_dense(const DenseParams& p, int d, hipStream_t s) {
   if (!GATHER && d == 64) {
-    constexpr int NW = 8;
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
-    const int64_t tiles = ceil_div(p.A.n_rows, 16 * NW);
-    const unsigned grid = (unsigned)std::min<int64_t>(tiles, (int64_t)cus);
-    hipLaunchKernelGGL((transform64_kernel<MODE, NW>), dim3(grid), dim3(64 * NW), 0, s, p);
+    auto go64 = [&](auto kern, int nw) {
+      const int64_t tiles = ceil_div(p.A.n_rows, 16 * nw);
+      const unsigned grid = (unsigned)std::min<int64_t>(tiles, (int64_t)cus);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * nw), 0, s, p);
+    };
+    if (MODE == 0 && p.gas_blocks && p.gas_bs == 8)
+      go64(transform64_kernel<MODE, GNNREC_TRANSFORM_GASV_WAVES, true>,
+           GNNREC_TRANSFORM_GASV_WAVES);
+    else
+      go64(transform64_kernel<MODE, 8, false>, 8);
     return check_launch(MODE == 0 ? "ngcf_transform" : "dense_transform");
   }
   auto go = [&](auto kern, int nw) {
