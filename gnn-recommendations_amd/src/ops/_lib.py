@@ -70,6 +70,8 @@ _SIGNATURES = {
                               _p, _i64,
                               _i64, _i32, _i32, _p, _i64, _p, _i64, _f32, _p, _i64, _p, _i32, _p],
     "gnnrec_row_nonzero_f32": [_p, _i64, _i64, _i32, _p, _p],
+    "gnnrec_spmm_sparse_src_f32": [_p, _p, _p, _i64, _i64, _p, _i64, _i64, _p, _i64, _p, _i64,
+                                   _i32, _p, _p, _p],
     "gnnrec_lightgcn_split_f32": [_p, _p, _p, _i64, _p, _i32, _i32, _p, _p, _p, _p, _i64, _p,
                                   _i64, _i64, _p],
     "gnnrec_gas_f32": [_p, _i64, _i64, _i32, _i32, _p, _p, _p, _i64, _p],

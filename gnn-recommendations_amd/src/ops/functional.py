@@ -206,6 +206,51 @@ def row_nonzero(x: torch.Tensor) -> torch.Tensor:
     return m
 
 
+# Row-sparse input hop (gnnrec_spmm_sparse_src_f32): used for the training backward's first
+# hop when its sources' stored entries are at most this fraction of the operand's
+SPARSE_SRC_MAX_FRAC = 0.05
+
+
+class SparseSrc:
+    """A hop input that is zero outside `rows` (int64, ascending) whose rows of the forward
+    operand hold `pairs` entries: the hop runs as gnnrec_spmm_sparse_src_f32."""
+
+    def __init__(self, fwd: CsrGraph, rows: torch.Tensor, pairs: int):
+        self.fwd, self.rows, self.pairs = fwd, rows, int(pairs)
+
+
+def sparse_sources(fwd: CsrGraph, x: torch.Tensor, max_frac: float = SPARSE_SRC_MAX_FRAC):
+    """SparseSrc for a hop over fwd^T of x when x's non-zero rows (NaN included) hold at most
+    `max_frac` of fwd's entries, else None (two small device reads)."""
+    rows = torch.nonzero(row_nonzero(x)).flatten()
+    if rows.numel() == 0:
+        return SparseSrc(fwd, rows, 0)
+    rp = fwd.row_ptr
+    pairs = int((rp[rows + 1] - rp[rows]).sum())
+    return SparseSrc(fwd, rows, pairs) if pairs <= max_frac * max(fwd.nnz, 1) else None
+
+
+def spmm_sparse_src_into(src: SparseSrc, x: torch.Tensor, y: torch.Tensor) -> None:
+    """y = fwd^T x for an x that is zero outside src.rows: every output row a source reaches
+    gets the dense hop's bits, the others are zeroed here."""
+    fwd = src.fwd
+    _require_device(fwd, x, y)
+    y.zero_()
+    if src.pairs == 0:
+        return
+    L = _lib.lib()
+    nbytes = _lib.C.c_size_t(0)
+    args = (ptr(fwd.row_ptr), ptr(fwd.col), ptr(fwd.val), fwd.n_rows, fwd.shape[1],
+            ptr(src.rows), src.rows.numel(), src.pairs, ptr(x), x.stride(0), ptr(y), y.stride(0),
+            x.shape[1])
+    stream = _lib.stream_of(fwd.device)
+    check(L.gnnrec_spmm_sparse_src_f32(*args, None, _lib.C.addressof(nbytes), stream),
+          "gnnrec_spmm_sparse_src_f32 (size)")
+    work = torch.empty(max(int(nbytes.value), 1), dtype=torch.uint8, device=x.device)
+    check(L.gnnrec_spmm_sparse_src_f32(*args, ptr(work), _lib.C.addressof(nbytes), stream),
+          "gnnrec_spmm_sparse_src_f32")
+
+
 def mark_rows(row_ptr: torch.Tensor, col: torch.Tensor, marked: torch.Tensor,
               n_out: int) -> torch.Tensor:
     """uint8 [n_out]: 1 at every column listed in a marked row of (row_ptr, col)
@@ -274,6 +319,11 @@ def _lightgcn_hops(op: CsrGraph, x0: torch.Tensor, K: int, masks,
             if name not in bufs:
                 bufs[name] = torch.empty_like(x0)
         xm, ya = masks(k, bufs[xn])
+        if isinstance(xm, SparseSrc) and epi == 0:
+            spmm_sparse_src_into(xm, bufs[xn], bufs[yn])
+            continue
+        if isinstance(xm, SparseSrc):
+            xm = None
         spmm_into(op, bufs[xn], bufs[yn], epi=epi, self_rows=x0, acc=out,
                   acc_div=float(K + 1), x_mask=xm, y_active=ya)
     return out
@@ -306,6 +356,12 @@ def lightgcn_backward(adj: CsrGraph, g: torch.Tensor, n_layers: int,
     def masks(k, x_in):
         if k > masked_hops:
             return None, None
+        if k == 1 and deferred and SPARSE_SRC_MAX_FRAC > 0:
+            # hop 1 of the deferred schedule stores y only: the row-sparse input hop when the
+            # gradient's rows are few (same bits)
+            src = sparse_sources(adj, x_in)
+            if src is not None:
+                return src, None
         xm = row_nonzero(x_in)
         # rows of A^T that reach a non-zero row: listed by (A^T)^T = A's rows
         ya = mark_rows(adj.row_ptr, adj.col, xm, at.n_rows) if k <= active_hops else None

@@ -237,6 +237,22 @@ int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val, const uint8_t*
                           float acc_div, const float* prev, int64_t ld_prev, uint32_t* sync,
                           int32_t meet_us, gnnrec_stream_t stream);
 
+/* Hop with a row-sparse input (ABI 8): y = A^T x where x is zero outside the n_src rows
+ * src_rows (ascending int64) — the training backward's first hop, whose input (the BPR
+ * gradient, trainer.py:199-281 through lightgcn.py:88) touches the 3B rows of a batch. The
+ * sources' rows of A (row_ptr/col/val: n_rows x n_cols, the forward operand) are scattered as
+ * (output row, source) pairs, sorted, and every reached output row of y ([n_cols, ldy]) is one
+ * fmaf chain from +0 over its sources in ascending order: the bits of the dense hop over A^T
+ * (a left-out term is fmaf(v, 0, acc) = acc). Rows no source reaches are not written (zero y
+ * first). max_pairs >= the sources' stored entries (exact count or a bound; a short bound
+ * fails with GNNREC_EINVAL). Two calls: workspace == NULL returns its size in
+ * *workspace_bytes; the second call synchronises `stream` once (the bound check). */
+int gnnrec_spmm_sparse_src_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
+                               int64_t n_rows, int64_t n_cols, const int64_t* src_rows,
+                               int64_t n_src, int64_t max_pairs, const float* x, int64_t ldx,
+                               float* y, int64_t ldy, int32_t d, void* workspace,
+                               size_t* workspace_bytes, gnnrec_stream_t stream);
+
 int gnnrec_row_nonzero_f32(const float* x, int64_t ldx, int64_t n_rows, int32_t d,
                            uint8_t* mask, gnnrec_stream_t stream);
 
