@@ -71,10 +71,12 @@ __global__ __launch_bounds__(256) void scatter_pairs_kernel(
 __global__ __launch_bounds__(256) void source_chain_kernel(
     const uint64_t* __restrict__ keys, const float* __restrict__ vals, int64_t n_pairs,
     const int64_t* __restrict__ src, const float* __restrict__ x, int64_t ldx,
-    float* __restrict__ y, int64_t ldy, int d) {
+    float* __restrict__ y, int64_t ldy, int d, const int* __restrict__ overflow) {
   const int64_t e = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int q = threadIdx.x & 15;
-  if (e >= n_pairs) return;
+  // a short bound left some key slots unwritten (scatter_pairs_kernel, same stream, already
+  // finished): their garbage would index x and y, so nothing is computed and y stays as it was
+  if (e >= n_pairs || *overflow) return;
   const uint64_t key = keys[e];
   if (key == kPadKey) return;
   const uint32_t r = (uint32_t)(key >> 32);
@@ -183,7 +185,7 @@ extern "C" int gnnrec_spmm_sparse_src_f32(const int64_t* row_ptr, const int32_t*
                                          end_bit, s) != hipSuccess)
     return check_launch("sparse_src: sort");
   hipLaunchKernelGGL(source_chain_kernel, dim3((unsigned)ceil_div(max_pairs, 16)), dim3(256), 0,
-                     s, keys_out, vals_out, max_pairs, src_rows, x, ldx, y, ldy, (int)d);
+                     s, keys_out, vals_out, max_pairs, src_rows, x, ldx, y, ldy, (int)d, flag);
   if (int rc = check_launch("sparse_src: chain")) return rc;
   int h_flag = 0;
   hipMemcpyAsync(&h_flag, flag, sizeof(int), hipMemcpyDeviceToHost, s);

@@ -11,6 +11,7 @@ and creation order. Semantics difference, documented: an isolated node yields a 
 for that node only (softmax over an empty set); the reference's dense matmul spreads that
 NaN to every node.
 """
+import warnings
 from typing import Optional, Tuple
 
 import torch
@@ -21,6 +22,27 @@ from ..base import BaseRecommender
 from ... import ops
 from ...ops._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT, EPI_NO_Y
 from ...ops.graph import CsrGraph
+
+# The reference's dense path (gat.py:99-141) holds an [N, N] mask plus, per head, [N, N]
+# scores and attention: ~16 N^2 bytes at once (N = 20 000: 6.4 GB). The native kernel has no
+# backward, so a native operand with autograd on (GAT training) or with dropout in training
+# mode falls back to that path only up to this many nodes and raises above it — never a
+# silent O(N^2) allocation on a large graph.
+GAT_DENSE_MAX_NODES = 20_000
+
+
+def check_dense_fallback(n_nodes: int, why: str) -> None:
+    """Refuse (RuntimeError) the dense masked-softmax path for a native operand of more than
+    GAT_DENSE_MAX_NODES nodes; warn below it. `why` says what ruled the native kernel out."""
+    if n_nodes > GAT_DENSE_MAX_NODES:
+        raise RuntimeError(
+            f"GATLayer: the native sparse kernel does not apply ({why}) and the reference's "
+            f"dense [N, N] softmax path would allocate O(N^2) memory for N = {n_nodes} "
+            f"(> GAT_DENSE_MAX_NODES = {GAT_DENSE_MAX_NODES}). GAT on the native path is "
+            f"inference-only: run the forward under torch.no_grad() / eval(), or train on a "
+            f"graph of at most {GAT_DENSE_MAX_NODES} nodes.")
+    warnings.warn(f"GATLayer: dense O(N^2) reference path on a native operand "
+                  f"(N = {n_nodes}; {why})", RuntimeWarning, stacklevel=3)
 
 
 class GATLayer(nn.Module):
@@ -37,11 +59,21 @@ class GATLayer(nn.Module):
         self.leakyrelu = nn.LeakyReLU(alpha)
         self.dropout_layer = nn.Dropout(dropout)
 
-    def native_ok(self, a, x) -> bool:
+    def native_block(self, a) -> Optional[str]:
+        """Why the native kernel cannot run this layer on operand `a` (None: it can)."""
+        if not isinstance(a, CsrGraph):
+            return "not a native operand"
         width = self.n_heads * self.out_dim
-        return (isinstance(a, CsrGraph) and width in (16, 32, 64, 128, 256)
-                and self.out_dim % 4 == 0 and (not self.training or self.dropout == 0.0)
-                and not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())))
+        if width not in (16, 32, 64, 128, 256) or self.out_dim % 4:
+            return f"heads*out_dim = {width} has no kernel instance"
+        if self.training and self.dropout != 0.0:
+            return "attention dropout in training mode"
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            return "autograd is enabled and the native kernel has no backward"
+        return None
+
+    def native_ok(self, a, x) -> bool:
+        return self.native_block(a) is None
 
     def fused_weight(self) -> torch.Tensor:
         """[H*o + 2H, in]: the stacked head projections W_h, then a_self_h^T W_h and
@@ -121,9 +153,12 @@ class GATLayer(nn.Module):
     def forward(self, x: torch.Tensor, adj_matrix, *, apply_elu: bool = False, epi: int = 0,
                 self_rows=None, acc=None, acc_div: float = 1.0) -> torch.Tensor:
         a = ops.as_operand(adj_matrix)
-        if self.native_ok(a, x):
+        why = self.native_block(a)
+        if why is None:
             return self.native_forward(a, *self.native_inputs(x), apply_elu=apply_elu, epi=epi,
                                        self_rows=self_rows, acc=acc, acc_div=acc_div)
+        if isinstance(a, CsrGraph):
+            check_dense_fallback(a.shape[0], why)
         out = self._dense_forward(x, a)
         return F.elu(out) if apply_elu else out
 

@@ -397,7 +397,10 @@ def _propagate_deferred(dg, x0_pad, K, hop, mkw, work, self_rows, chunked, overl
         gath = dict(piece)
     else:
         acc_piece = torch.zeros((dg.rows_pad, d), dtype=torch.float32, device=dev)
-        piece = {"acc": acc_piece, "a": Y, "b": Y}
+        # K >= 4: hop 3 reads its own input rows ("b", EPI_ACC_X's prev) while it writes "a";
+        # the kernel takes prev and y as __restrict__, so the two get separate pieces
+        piece = {"acc": acc_piece, "a": Y,
+                 "b": Y if K <= 3 else torch.zeros_like(Y)}
         gath = {}
     acc = acc_piece[:n]
     sched = lightgcn_hop_schedule(K, deferred=True)

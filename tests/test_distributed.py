@@ -23,9 +23,24 @@ from src.ops.distributed import (DistributedGraph, RankGrid, feature_groups_for,
                                  lightgcn_propagate_dist, lightgcn_propagate_grid)
 
 
+def _overlap(a, b) -> bool:
+    """Do two row-major tables share any byte of storage?"""
+    if a is None or b is None or a.numel() == 0 or b.numel() == 0:
+        return False
+    def span(t):
+        lo = t.data_ptr()
+        return lo, lo + ((t.shape[0] - 1) * t.stride(0) + t.shape[-1]) * t.element_size()
+    (a0, a1), (b0, b1) = span(a), span(b)
+    return a0 < b1 and b0 < a1
+
+
 def cpu_hop(adj, x, y, *, epi, self_rows, acc, acc_div, prev=None):
     """CPU stand-in for gnnrec_spmm_tiled_f32 (oracle SpMM + the same epilogue order:
-    acc = (((self | acc) [+ acc on INIT|ADD]) [+ prev on ACC_X]) + y [/ div])."""
+    acc = (((self | acc) [+ acc on INIT|ADD]) [+ prev on ACC_X]) + y [/ div]). It computes
+    before it writes, so it also asserts the kernel's __restrict__ contract: y shares no rows
+    with the gathered table x nor with the ACC_X rows prev."""
+    assert not _overlap(y, x), "a hop writes rows it gathers"
+    assert not (epi & EPI_ACC_X and _overlap(y, prev)), "a hop writes its ACC_X rows"
     yy = oracle.spmm(adj.row_ptr.numpy(), adj.col.numpy(), adj.val.numpy(), x.numpy())
     if epi & (EPI_ACC_INIT | EPI_ACC_ADD):
         b = (self_rows if epi & EPI_ACC_INIT else acc).numpy().copy()
@@ -80,7 +95,8 @@ def _worker(rank, world, port, K, balance, q, exchange="auto", chunks=1, deferre
     # from the rank's own exchange piece): 2/3/4 ranks, both exchanges, chunked, K = 2, 3, 4
     (2, 3, "nnz", "auto", 1, True), (4, 3, "nnz", "p2p", 3, True),
     (3, 3, "rows", "allgather", 1, True), (4, 2, "nnz", "auto", 2, True),
-    (3, 4, "nnz", "p2p", 1, True), (1, 3, "nnz", "auto", 1, True)])
+    (3, 4, "nnz", "p2p", 1, True), (1, 3, "nnz", "auto", 1, True),
+    (2, 4, "nnz", "p2p", 1, True), (4, 5, "nnz", "allgather", 1, True)])
 def test_sharded_propagation_matches_single_device(world, K, balance, exchange, chunks,
                                                    deferred):
     ctx = mp.get_context("spawn")
@@ -131,7 +147,13 @@ def _grid_worker(rank, world, port, K, d, F, exchange, deferred, q):
     (4, 2, 64, 2, "allgather", False),
     (4, 3, 128, None, "auto", True),       # F = 4
     (4, 3, 64, 1, "auto", True),           # plain row shards through the grid
-    (3, 3, 96, 3, "auto", False)])
+    (3, 3, 96, 3, "auto", False),
+    # the driver's 8-GPU layouts (bench.py): headline d = 64 -> 2 feature groups x 4 row
+    # shards, config 4 d = 128 -> 4 x 2, and the north star's 1-D row shards (F = 1), with
+    # both exchanges and the deferred layer mean
+    (8, 3, 64, None, "p2p", True), (8, 3, 64, None, "allgather", True),
+    (8, 3, 128, None, "p2p", True), (8, 3, 128, None, "allgather", True),
+    (8, 3, 64, 1, "p2p", True), (8, 3, 64, 1, "allgather", True)])
 def test_rank_grid_matches_single_device(world, K, d, F, exchange, deferred):
     """Feature groups x row shards: every rank's column block of its rows, and the gathered
     [N, d] table, bit-identical to the single-device oracle propagation."""

@@ -39,6 +39,8 @@ def _model(kind, nu, ni, dev):
         m = LightGCN(nu, ni, 64, 3, 0.1)
     elif kind == "lightgcn_d128_tiled":
         m = LightGCN(nu, ni, 128, 3, 0.1)
+    elif kind == "lightgcn_k4_tiled":
+        m = LightGCN(nu, ni, 64, 4, 0.1)
     elif kind == "ngcf_gs":
         m = NGCFGroupShuffle(nu, ni, 64, [64, 64, 64], 0.1, 0.1, 8, 0.3)
     else:
@@ -109,6 +111,12 @@ def _work(rank, world, port, kind, exchange, q):
                 return
             if kind == "lightgcn":
                 mine = lightgcn_propagate_dist(dg, x0p, 3, overlap_chunks=3)
+            elif kind == "lightgcn_k4_tiled":
+                # deferred layer mean at K = 4: hop 3 reads its input rows (prev) from one
+                # exchange piece and writes its output into another (no aliasing)
+                from src.ops import functional as F
+                assert F.tiled_plan_for(dg.shard, x0p) is not None
+                mine = lightgcn_propagate_dist(dg, x0p, 4)
             elif kind.endswith("_tiled"):
                 from src.ops import functional as F
                 for c0, c1 in dg.chunk_bounds(3):   # every overlap chunk runs the tiled kernel
@@ -138,6 +146,7 @@ def _work(rank, world, port, kind, exchange, q):
                                            ("lightgcn_tiled", "p2p"),
                                            ("lightgcn_grid_tiled", "auto"),
                                            ("lightgcn_d128_tiled", "p2p"),
+                                           ("lightgcn_k4_tiled", "p2p"),
                                            ("ngcf_gs", "auto"), ("gat", "auto"),
                                            ("train", "auto")])
 def test_two_ranks_native_match_single_device(cuda, kind, exchange):

@@ -285,3 +285,25 @@ def test_rows_gemm_guards_on_host():
     # last (head-mean) layer of a 128-wide GAT: H * in = 512 has no instance -> not shared
     assert not GATLayer(128, 128, 4, concat_heads=False).shares_input()
     assert GATLayer(64, 64, 4, concat_heads=False).shares_input()
+
+
+def test_gat_dense_fallback_guard():
+    """GAT training is outside the native path (the sparse kernel has no backward): a native
+    operand that cannot take it falls back to the reference's dense [N, N] softmax only up to
+    GAT_DENSE_MAX_NODES nodes (with a warning) and raises above it; the reason is reported."""
+    from src.models.baselines.gat import (GAT_DENSE_MAX_NODES, GATLayer,
+                                          check_dense_fallback)
+    with pytest.raises(RuntimeError, match="inference-only"):
+        check_dense_fallback(GAT_DENSE_MAX_NODES + 1, "autograd")
+    with pytest.warns(RuntimeWarning):
+        check_dense_fallback(GAT_DENSE_MAX_NODES, "autograd")
+    layer = GATLayer(64, 16, 4)
+    g = CsrGraph(torch.tensor([0, 1, 2]), torch.tensor([1, 0], dtype=torch.int32),
+                 torch.ones(2), (2, 2), 1, 1, True)
+    assert "autograd" in layer.native_block(g)
+    with torch.no_grad():
+        assert layer.native_block(g) is None
+        layer.train()
+        layer.dropout = 0.1
+        assert "dropout" in layer.native_block(g)
+    assert layer.native_block(torch.zeros(2, 2)) == "not a native operand"

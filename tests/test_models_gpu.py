@@ -149,6 +149,33 @@ def test_gat_model_sparse(cuda):
     np.testing.assert_allclose(i.cpu().numpy(), f["item_out"], rtol=0, atol=2e-5)
 
 
+def test_gat_refuses_dense_fallback_on_large_graph(cuda):
+    """A native operand with autograd on cannot take the native kernel (no backward); above
+    GAT_DENSE_MAX_NODES the layer raises instead of allocating the reference's [N, N] mask
+    (gat.py:124-137 of the reference), and below it warns. Under no_grad it runs natively."""
+    from src.models.baselines.gat import GAT_DENSE_MAX_NODES
+    nu = ni = GAT_DENSE_MAX_NODES // 2 + 10
+    rng = np.random.default_rng(0)
+    u = np.concatenate([np.arange(nu), rng.integers(0, nu, 4 * nu)])
+    i = np.concatenate([rng.integers(0, ni, nu), rng.integers(0, ni, 4 * nu)])
+    g = CsrGraph.from_interactions(u, i, nu, ni).to(cuda)
+    torch.manual_seed(0)
+    m = GAT(nu, ni, embedding_dim=64, n_layers=3, n_heads=4, dropout=0.0).to(cuda).eval()
+    with pytest.raises(RuntimeError, match="GAT_DENSE_MAX_NODES"):
+        m(g)                                       # grad enabled, parameters require grad
+    before = torch.cuda.max_memory_allocated(cuda)
+    with torch.no_grad():
+        uo, io = m(g)
+    assert uo.shape == (nu, 64) and torch.isfinite(uo).all() and torch.isfinite(io).all()
+    assert torch.cuda.max_memory_allocated(cuda) - before < (nu + ni) ** 2  # no [N, N] buffer
+    small = CsrGraph.from_interactions([0, 1, 2, 0], [0, 1, 2, 1], 3, 3).to(cuda)
+    ms = GAT(3, 3, embedding_dim=16, n_layers=2, n_heads=4, dropout=0.0).to(cuda)
+    with pytest.warns(RuntimeWarning, match="dense O\\(N\\^2\\)"):
+        us, _ = ms(small)
+    us.sum().backward()                            # the dense path is differentiable
+    assert ms.layers[0].W[0].weight.grad is not None
+
+
 def test_gat_isolated_node_row_is_nan_only_locally(cuda):
     torch.manual_seed(0)
     m = GAT(4, 3, embedding_dim=16, n_layers=2, n_heads=4, dropout=0.0).to(cuda).eval()

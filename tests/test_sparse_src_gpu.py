@@ -85,6 +85,35 @@ def test_sparse_src_edge_cases(cuda):
     assert F.sparse_sources(gd, torch.ones(n, 64, device=cuda)) is None
 
 
+@pytest.mark.parametrize("short", [1, 2, 10**9])
+def test_sparse_src_short_bound_leaves_y_untouched(cuda, short):
+    """Through the C ABI with a max_pairs below the sources' entries: the call fails with
+    EINVAL and y is not written (the chain kernel sees the scatter's overflow flag and never
+    reads the key slots the scatter skipped)."""
+    gd, _ = _graph(cuda, seed=5, nu=3000, ni=2000, n=40000)
+    n = gd.shape[0]
+    rows = np.sort(np.random.default_rng(5).choice(n, 200, replace=False))
+    x = _sparse_x(n, 64, rows, cuda)
+    src = F.sparse_sources(gd, x)
+    max_pairs = 0 if short == 10**9 else src.pairs // (2 * short) + 1   # 0: nothing to do
+    y = torch.full((n, 64), 7.0, device=cuda)
+    L = _lib.lib()
+    nbytes = _lib.C.c_size_t(0)
+    args = (_lib.ptr(gd.row_ptr), _lib.ptr(gd.col), _lib.ptr(gd.val), gd.n_rows, gd.shape[1],
+            _lib.ptr(src.rows), src.rows.numel(), max_pairs, _lib.ptr(x), x.stride(0),
+            _lib.ptr(y), y.stride(0), 64)
+    stream = _lib.stream_of(gd.device)
+    assert L.gnnrec_spmm_sparse_src_f32(*args, None, _lib.C.addressof(nbytes), stream) == 0
+    work = torch.full((max(int(nbytes.value), 1),), 0xAB, dtype=torch.uint8, device=cuda)
+    rc = L.gnnrec_spmm_sparse_src_f32(*args, _lib.ptr(work), _lib.C.addressof(nbytes), stream)
+    torch.cuda.synchronize()
+    if max_pairs:
+        assert rc != 0 and b"max_pairs" in L.gnnrec_last_error()
+    else:
+        assert rc == 0
+    assert torch.all(y == 7.0)
+
+
 def test_backward_through_sparse_src_equals_dense_backward(cuda, monkeypatch):
     """lightgcn_backward's first hop on the row-sparse path (deferred schedule, tiled hops 2-3)
     gives the dense backward's bits."""
