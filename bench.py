@@ -48,8 +48,8 @@ sys.path.insert(0, str(ROOT))
 from src.ops import CsrGraph  # noqa: E402
 from src.ops import functional as F  # noqa: E402
 from src.ops._lib import EPI_ACC_ADD, EPI_ACC_INIT, EPI_ACC_X, EPI_NO_Y  # noqa: E402
-from src.ops.distributed import (RankGrid, lightgcn_propagate_dist,  # noqa: E402
-                                 make_work, _native_hop)
+from src.ops.distributed import (RankGrid, feature_groups_for,  # noqa: E402
+                                 lightgcn_propagate_dist, make_work, _native_hop)
 
 METRIC = "edges/s + achieved HBM GB/s, LightGCN K=3 dim=64, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
@@ -100,6 +100,9 @@ class HopTimer:
 
     hop.native_hop = True   # lightgcn_propagate_dist passes the chunk options through it
 
+    def reset(self, active: bool):
+        self.pairs, self.active = [], active
+
     def durations_ms(self):
         return [s.elapsed_time(e) for s, e in self.pairs]
 
@@ -130,8 +133,42 @@ class ExchangeTimer:
             return r
         return timed
 
+    def reset(self, active: bool):
+        self.pairs, self.active = [], active
+
     def durations_ms(self):
         return [s.elapsed_time(e) for s, e in self.pairs]
+
+
+class Layout:
+    """One rank layout of the N-GPU propagation: the RankGrid (F feature groups x R row
+    shards), this rank's padded x0 columns, hop buffers, column-ordered plan and timers."""
+
+    def __init__(self, full: CsrGraph, rank: int, world: int, device, d: int, fg, exchange: str):
+        self.grid = RankGrid(full, rank, world, device, d, fg,
+                             exchange="p2p" if exchange == "auto" else exchange)
+        self.dg = self.grid.dg
+        self.src = distinct_cols(self.dg.shard, self.dg.shard.shape[1])
+        self.x0_pad = None
+        self.work = None
+        self.plan_s = 0.0
+        self.tiled = False
+        self.timer = HopTimer()
+        self.xtimer = ExchangeTimer(self.dg) if self.dg.world > 1 else None
+
+    def prepare(self, x0: torch.Tensor, device) -> "Layout":
+        self.x0_pad = self.grid.x0_table(x0)
+        self.work = make_work(self.dg, self.x0_pad.shape[1], device)
+        # operand re-layout for the column-ordered hop (built once, outside the timed region)
+        t1 = time.perf_counter()
+        self.tiled = F.tiled_plan_for(self.dg.shard, self.x0_pad) is not None
+        torch.cuda.synchronize()
+        self.plan_s = time.perf_counter() - t1
+        return self
+
+    def release(self):
+        self.x0_pad = self.work = None
+        self.dg.shard._plans.clear()
 
 
 def hop_bytes_alg(nnz: int, rows: int, src: int, d: int) -> int:
@@ -300,6 +337,67 @@ def cpu_baseline(g: CsrGraph, x0: torch.Tensor, K: int, n_users: int, gpu_hop1: 
                               "output_max_abs_diff": max_abs}}
 
 
+def vendor_baseline(g: CsrGraph, x0: torch.Tensor, K: int, hip_out: torch.Tensor, hip_ms: float,
+                    device, reps: int = 5) -> dict:
+    """The vendor comparator (SURVEY.md §8 d3 / BASELINE.md): the reference's own propagation
+    call, `torch.sparse.mm(adj, x)` K times + `torch.stack(layers).mean(0)` (lightgcn.py:76-95),
+    on THIS device — ATen's ROCm sparse path (hipSPARSE SpMM) — over the same operand and x0,
+    outside the timed region. Two operand forms: the CSR tensor (the vendor library's best
+    case) and the reference's own uncoalesced int64 COO moved to the device
+    (graph_builder.py:163-172, trainer.py:233-234), which torch coalesces on every call.
+    HIP events on torch's stream; 1 untimed rep, then `reps` (median). Compared with the HIP
+    path's output (max |diff| and bit-exactness)."""
+    N = g.shape[0]
+    res = {"what": f"K={K} x torch.sparse.mm(A, x) + stack().mean(0) on {torch.cuda.get_device_name(device)}"
+                   f" (torch {torch.__version__}, ATen ROCm sparse / hipSPARSE)",
+           "reps": reps, "statistic": "median"}
+    xd = x0.to(device)
+    for form in ("csr", "coo_reference"):
+        A = None
+        try:
+            rp = g.row_ptr.to(device)
+            col = g.col.to(device).to(torch.int64)
+            val = g.val.to(device)
+            if form == "csr":
+                A = torch.sparse_csr_tensor(rp, col, val, (N, N))
+            else:
+                rows = torch.repeat_interleave(torch.arange(N, device=device), rp[1:] - rp[:-1])
+                A = torch.sparse_coo_tensor(torch.stack([rows, col]), val, (N, N))
+                del rows
+            del rp, col, val
+
+            def prop():
+                layers, x = [xd], xd
+                for _ in range(K):
+                    x = torch.sparse.mm(A, x)
+                    layers.append(x)
+                return torch.stack(layers, dim=0).mean(dim=0)
+            out = prop()
+            torch.cuda.synchronize()
+            ms = []
+            for _ in range(reps):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                o2 = prop()
+                e.record()
+                torch.cuda.synchronize()
+                ms.append(s.elapsed_time(e))
+                del o2
+            t = float(np.median(ms))
+            res[form] = {"ms_per_step": t, "ms_samples": ms, "edges_per_s": K * g.nnz / (t * 1e-3),
+                         "max_abs_diff_vs_hip": float((out - hip_out).abs().max()),
+                         "bit_exact_vs_hip": bool(torch.equal(out.view(torch.int32),
+                                                              hip_out.view(torch.int32))),
+                         "hip_speedup": t / hip_ms}
+            del out
+        except Exception as ex:  # noqa: BLE001 — recorded, not fatal to the bench line
+            res[form] = {"error": f"{type(ex).__name__}: {ex}"[:400]}
+        del A
+        torch.cuda.empty_cache()
+        log(f"vendor {form}: {res[form]}")
+    return res
+
+
 def verify(dg, full: CsrGraph, x0, x0_pad, K, out, device, rank, cols) -> dict:
     """Full-size parity: this rank's rows of the timed (possibly sharded) propagation must equal,
     bit for bit, a single-device propagation of the whole graph (the oracle itself is checked
@@ -326,6 +424,8 @@ def main(argv=None) -> int:
     ap.add_argument("--pairs", type=int, default=100_000_000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-vendor", action="store_true",
+                    help="skip the vendor comparator (torch.sparse.mm on the device, N = 1)")
     ap.add_argument("--cpu-reps", type=int, default=2,
                     help="timed reps of the reference CPU path (median reported)")
     ap.add_argument("--verify", action="store_true",
@@ -373,74 +473,116 @@ def main(argv=None) -> int:
     torch.manual_seed(0)
     x0 = torch.randn(N, d, dtype=torch.float32) * 0.1  # nn.init.normal_(std=init_scale=0.1)
 
-    t0 = time.perf_counter()
-    grid = RankGrid(full, rank, world, device, d, a.feature_groups or None,
-                    exchange="p2p" if a.exchange == "auto" else a.exchange)
-    dg = grid.dg
-    src = distinct_cols(dg.shard, dg.shard.shape[1])
-    x0_pad = grid.x0_table(x0)
-    d_loc = x0_pad.shape[1]          # this rank's feature columns (d / F)
-    work = make_work(dg, d_loc, device)
-    # operand re-layout for the column-ordered hop (built once, outside the timed region)
-    t1 = time.perf_counter()
-    tiled = F.tiled_plan_for(dg.shard, x0_pad) is not None
-    plan_s = time.perf_counter() - t1
+    # Rank layouts timed at N > 1: the default grid (F = gcd(N, d/32) feature groups x N/F
+    # row shards) and, when it differs, the north star's own 1-D destination-row shards with a
+    # per-hop exchange over all N ranks (F = 1). --feature-groups F > 0 pins one layout.
+    if world > 1 and not a.feature_groups:
+        f_default = feature_groups_for(world, d)
+        layout_fs = [f_default] + ([1] if f_default != 1 else [])
+    else:
+        layout_fs = [a.feature_groups or None]
+    layouts = []
+    for fg in layout_fs:
+        t0 = time.perf_counter()
+        lay = Layout(full, rank, world, device, d, fg, a.exchange).prepare(x0, device)
+        layouts.append(lay)
+        log(f"rank {rank}: F={lay.grid.F} x R={lay.grid.R}: rows [{lay.dg.row_begin},"
+            f"{lay.dg.row_end}) cols [{lay.grid.cols[0]},{lay.grid.cols[1]}) "
+            f"nnz={lay.dg.shard.nnz} src={lay.src} uploaded in {time.perf_counter() - t0:.1f}s "
+            f"(tiled plan {lay.plan_s:.1f}s)")
     torch.cuda.synchronize()
-    log(f"rank {rank}: rows [{dg.row_begin},{dg.row_end}) cols [{grid.cols[0]},{grid.cols[1]}) "
-        f"nnz={dg.shard.nnz} src={src} "
-        f"uploaded in {time.perf_counter() - t0:.1f}s (tiled plan {plan_s:.1f}s)")
     cpu_graph = full if (rank == 0 and world == 1 and not a.no_cpu_baseline) else None
+    vendor_graph = full if (rank == 0 and world == 1 and not a.no_vendor) else None
     verify_graph = full if a.verify else None
     del full
 
-    timer = HopTimer()
-    xtimer = ExchangeTimer(dg) if dg.world > 1 else None
-    chunks, reserve = 1, 0
+    cur = {"lay": layouts[0], "chunks": 1, "reserve": 0}
 
     def step():
-        return lightgcn_propagate_dist(dg, x0_pad, K, hop_fn=timer.hop, work=work,
-                                       overlap_chunks=chunks, reserve_cus=reserve)
+        lay = cur["lay"]
+        return lightgcn_propagate_dist(lay.dg, lay.x0_pad, K, hop_fn=lay.timer.hop, work=lay.work,
+                                       overlap_chunks=cur["chunks"], reserve_cus=cur["reserve"])
 
-    # Exchange form (N > 1): time whole steps of each candidate before the timed region and
-    # keep the fastest (same decision on every rank: max over ranks).
-    exchange_info = {"mode": dg.exchange_mode if dg.world > 1 else "none", "overlap_chunks": 1}
-    if dg.world > 1:
-        # (mode, overlap chunks, CUs a chunk kernel leaves to the concurrent RCCL kernels)
-        cands = [("allgather", 1, 0)]
-        if not bool(dg.needs.all()) and a.exchange in ("auto", "p2p"):
-            cands = ([] if a.exchange == "p2p" else cands) + [
-                ("p2p", 1, 0), ("p2p", 4, 0), ("p2p", 8, 0), ("p2p", 4, 16), ("p2p", 8, 16)]
-        elif a.exchange == "p2p":
-            cands = [("p2p", 1, 0)]
+    # Exchange form (N > 1): time whole steps of each candidate (layout, exchange, overlap
+    # chunks, CUs left to RCCL) before the timed region and keep the fastest (same decision on
+    # every rank: max over ranks). Every candidate's ms per step, kernel ms per hop and the
+    # ms per exchanged hop that the exchange holds the hop chain are reported.
+    exchange_info = {"mode": "none", "overlap_chunks": 1}
+    if world > 1:
+        cands = []
+        for li, lay in enumerate(layouts):
+            dg = lay.dg
+            if dg.world == 1:              # F = N: one row shard, nothing to exchange
+                cands.append((li, "allgather", 1, 0))
+                continue
+            cc = [] if a.exchange == "p2p" else [(li, "allgather", 1, 0)]
+            if not bool(dg.needs.all()) and a.exchange in ("auto", "p2p"):
+                cc += [(li, "p2p", 1, 0), (li, "p2p", 4, 0), (li, "p2p", 8, 0),
+                       (li, "p2p", 4, 16), (li, "p2p", 8, 16)]
+            elif a.exchange == "p2p":
+                cc += [(li, "p2p", 1, 0)]
+            cands += cc
 
         def cname(c):
-            return f"{c[0]}_x{c[1]}" + (f"_r{c[2]}" if c[2] else "") + "_ms"
+            lay = layouts[c[0]]
+            return (f"F{lay.grid.F}xR{lay.grid.R}_" + (f"{c[1]}_x{c[2]}" if lay.dg.world > 1
+                                                       else "no_exchange")
+                    + (f"_r{c[3]}" if c[3] else ""))
         tried = {}
         for cand in cands:
-            dg.exchange_mode, chunks, reserve = cand
+            lay = layouts[cand[0]]
+            cur.update(lay=lay, chunks=cand[2], reserve=cand[3])
+            lay.dg.exchange_mode = cand[1]
             step()
             torch.cuda.synchronize()
             dist.barrier()
+            lay.timer.reset(True)
+            if lay.xtimer is not None:
+                lay.xtimer.reset(True)
             t0 = time.perf_counter()
             for _ in range(3):
                 step()
             torch.cuda.synchronize()
-            tt = torch.tensor([(time.perf_counter() - t0) / 3 * 1e3], dtype=torch.float64, device=device)
+            dist.barrier()
+            tt = torch.tensor([(time.perf_counter() - t0) / 3 * 1e3,
+                               float(np.sum(lay.timer.durations_ms())) / (3 * K),
+                               (float(np.sum(lay.xtimer.durations_ms())) / (3 * max(1, K - 1))
+                                if lay.xtimer is not None else 0.0)],
+                              dtype=torch.float64, device=device)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            tried[cname(cand)] = float(tt.item())
-        best = min(cands, key=lambda c: tried[cname(c)])
-        dg.exchange_mode, chunks, reserve = best
-        exchange_info = {"mode": best[0], "overlap_chunks": best[1], "reserved_cus": best[2],
-                         "candidates_ms_per_step": tried}
+            lay.timer.reset(False)
+            if lay.xtimer is not None:
+                lay.xtimer.reset(False)
+            tried[cname(cand)] = {"ms_per_step": float(tt[0]), "compute_ms_per_hop": float(tt[1]),
+                                  "exchange_ms_per_hop": float(tt[2]),
+                                  "recv_bytes_per_hop_per_rank":
+                                      lay.dg.recv_rows() * lay.x0_pad.shape[1] * 4}
+            log(f"candidate {cname(cand)}: {tried[cname(cand)]}")
+        best = min(cands, key=lambda c: tried[cname(c)]["ms_per_step"])
+        lay = layouts[best[0]]
+        cur.update(lay=lay, chunks=best[2], reserve=best[3])
+        lay.dg.exchange_mode = best[1]
+        exchange_info = {"mode": best[1] if lay.dg.world > 1 else "none",
+                         "overlap_chunks": best[2], "reserved_cus": best[3],
+                         "chosen": cname(best), "candidates": tried}
+    lay = cur["lay"]
+    grid, dg, x0_pad, work, src, tiled, plan_s = (lay.grid, lay.dg, lay.x0_pad, lay.work, lay.src,
+                                                  lay.tiled, lay.plan_s)
+    d_loc = x0_pad.shape[1]          # this rank's feature columns (d / F)
+    chunks = cur["chunks"]
+    timer, xtimer = lay.timer, lay.xtimer
+    for other in layouts:
+        if other is not lay:
+            other.release()
 
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    timer.active = True
+    timer.reset(True)
     if xtimer is not None:
-        xtimer.active = True
+        xtimer.reset(True)
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for _ in range(a.steps):
@@ -492,6 +634,12 @@ def main(argv=None) -> int:
     workload_key = f"g100m_lightgcn_k{K}_d{d}_n{world}" + ("_tiled" if tiled else "")
     kkey = kernel_key(tiled_plan_info(dg.shard, x0_pad))
     traffic, traffic_src = load_traffic(workload_key, kkey) if world == 1 else (None, "N > 1")
+
+    vendor = None
+    if vendor_graph is not None:
+        log("timing the vendor comparator (torch.sparse.mm on the device) ...")
+        vendor = vendor_baseline(vendor_graph, x0, K, out, ms_per_step, device)
+        del vendor_graph
 
     cpu = None
     if cpu_graph is not None:
@@ -566,6 +714,7 @@ def main(argv=None) -> int:
                 if traffic else None,
             },
             "cpu_baseline": cpu,
+            "vendor": vendor,
             "operand_prep_s": {"tiled_plan_build": plan_s if tiled else None},
             "edges_per_s_per_interaction": value / 2.0,
             "hbm_gbps_algorithmic_step": K * launch_bytes * world / (ms_per_step * 1e-3) / 1e9,

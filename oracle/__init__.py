@@ -142,6 +142,8 @@ def score_topk(u, v, k, seen_ptr=None, seen_col=None):
 def gat_head(rp, col, h, ss, sn, slope=0.2):
     """One head of the GAT aggregation; h: [N, o], ss/sn: [N]. float64 accumulation."""
     h = _f32(h)
+    if h.shape[1] > 1024:
+        raise ValueError("oracle.gat_head: o_dim <= 1024")
     ss, sn = _f32(ss).reshape(-1), _f32(sn).reshape(-1)
     n = rp.size - 1
     out = np.zeros((n, h.shape[1]), np.float32)

@@ -86,6 +86,92 @@ def powerlaw_graph(n_users, n_items, n_pairs, a, seed, threads=16, device=None):
     return CsrGraph.from_interactions(u, i, n_users, n_items, binary=True, n_threads=threads)
 
 
+def config3_model(device):
+    """Config 3's model: NGCF K=3 d=64 + GAS (8x8 blocks) after every layer, seed 0, eval."""
+    torch.manual_seed(0)
+    return NGCFGroupShuffle(1_000_000, 1_000_000, 64, [64, 64, 64], 0.1, 0.01, 8, 0.3).to(device).eval()
+
+
+def config5_model(shape, device):
+    """Config 5's model: GAT d=64, 4 heads, K=3 (concat layers, head-averaged last), seed 0."""
+    torch.manual_seed(0)
+    return GAT(shape[0], shape[1], 64, 3, 4, 0.1, 0.2, 0.1).to(device).eval()
+
+
+def _close(got, ref, rtol=1e-4, atol=1e-6) -> dict:
+    err = (got - ref).abs()
+    return {"max_abs_diff": float(err.max()), "max_abs_ref": float(ref.abs().max()),
+            "within_rtol_1e-4": bool((err <= atol + rtol * ref.abs()).all())}
+
+
+def torch_csr(g, device):
+    """The operand as a torch CSR tensor on the device (ATen's ROCm sparse path)."""
+    return torch.sparse_csr_tensor(g.row_ptr.to(device), g.col.to(device).long(),
+                                   g.val.to(device), g.shape)
+
+
+def verify_config3(g, m, table, device) -> dict:
+    """Every layer of the native NGCF + GAS forward ([N, 4d] = cat(x0..x3)) against the
+    reference's own composition in plain PyTorch fp32 on the same device and layer input:
+    torch.sparse.mm (hipSPARSE), the two nn.Linear, LeakyReLU (ngcf.py:69-84), then
+    (x @ blockdiag(expm))[:, perm] (group_shuffle_layer.py:88-94)."""
+    A = torch_csr(g, device)
+    d = m.embedding_dim
+    res = {"reference": "torch fp32 on the device: torch.sparse.mm + nn.Linear + LeakyReLU + "
+                        "dense block-diagonal GAS, per layer on the native layer input"}
+    for k, (layer, gs) in enumerate(zip(m.layers, m.gs_layers)):
+        x = table[:, k * d:(k + 1) * d].contiguous()
+        n = torch.sparse.mm(A, x)
+        o = layer.activation(layer.W1(n) + layer.W2(x * n))
+        ref = (o @ gs._build_orthogonal_matrix())[:, gs.perm]
+        res[f"layer{k + 1}"] = _close(table[:, (k + 1) * d:(k + 2) * d], ref)
+        del x, n, o, ref
+    del A
+    res["all_within_rtol_1e-4"] = all(v["within_rtol_1e-4"] for k, v in res.items()
+                                      if k.startswith("layer"))
+    return res
+
+
+def _edge_softmax_layer(rows, col, x, layer, n, chunk_heads=1):
+    """One GATLayer forward as a sparse restatement of the reference's dense masked softmax
+    (gat.py:99-149) in plain PyTorch: per head h = W_h x, e = LeakyReLU(h a_self [row] +
+    h a_neigh [col]), softmax over each row's edges (scatter amax / exp / index_add), the
+    weighted sum of h[col]; concat or head mean, then ELU."""
+    outs = []
+    for i in range(layer.n_heads):
+        h = x @ layer.W[i].weight.t()
+        ss = (h @ layer.a_self[i])[:, 0]
+        sn = (h @ layer.a_neigh[i])[:, 0]
+        e = torch.nn.functional.leaky_relu(ss[rows] + sn[col], layer.alpha)
+        mx = torch.full((n,), float("-inf"), device=x.device).scatter_reduce(0, rows, e, "amax")
+        p = torch.exp(e - mx[rows])
+        s = torch.zeros(n, device=x.device).index_add_(0, rows, p)
+        agg = torch.zeros(n, h.shape[1], device=x.device).index_add_(0, rows, p[:, None] * h[col])
+        outs.append(agg / s[:, None])
+        del h, e, p, agg
+    out = torch.cat(outs, dim=1) if layer.concat_heads else torch.stack(outs).mean(0)
+    return torch.nn.functional.elu(out)
+
+
+def verify_config5(g, m, mine, device) -> dict:
+    """The native GAT forward's layer mean against the reference composition (sparse
+    restatement of gat.py:99-149 + gat.py:258-297) in plain PyTorch fp32 on the device."""
+    rp = g.row_ptr.to(device)
+    n = g.shape[0]
+    rows = torch.repeat_interleave(torch.arange(n, device=device), rp[1:] - rp[:-1])
+    col = g.col.to(device).long()
+    x = m._initial_table()
+    acc = x.clone()
+    for layer in m.layers:
+        x = _edge_softmax_layer(rows, col, x, layer, n)
+        acc += x
+    ref = acc / float(len(m.layers) + 1)
+    res = {"reference": "torch fp32 on the device: per-head edge softmax (scatter amax/exp/"
+                        "index_add) over the CSR pattern, ELU, layer mean"}
+    res.update(_close(mine, ref))
+    return res
+
+
 def timed(fn, steps, warmup, world, device):
     for _ in range(warmup):
         fn()
@@ -130,6 +216,9 @@ def main(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--g1b", action="store_true", help="config 5 at full size (10M x 10M, 1B pairs)")
     ap.add_argument("--verify", action="store_true")
+    ap.add_argument("--no-ref-check", action="store_true",
+                    help="N = 1: skip the per-config check against the reference's composition "
+                         "in plain PyTorch on the device (configs 3 and 5-slice)")
     ap.add_argument("--topk-splits", type=int, nargs="*", default=[],
                     help="config 8: item-range splits timed besides 1 and the default")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"])
@@ -166,8 +255,7 @@ def main(argv=None):
         if 3 in a.configs or 4 in a.configs or 9 in a.configs or (6 in a.configs and world == 1):
             g100 = bench.build_graph(1_000_000, 1_000_000, 100_000_000, 0, threads)
         if 3 in a.configs:
-            torch.manual_seed(0)
-            m = NGCFGroupShuffle(1_000_000, 1_000_000, 64, [64, 64, 64], 0.1, 0.01, 8, 0.3).to(device).eval()
+            m = config3_model(device)
             dg = DistributedGraph(g100, rank, world, device)
             x0p = dg.pad_table(m._initial_table())
             t, mine = timed(lambda: ngcf_forward_dist(dg, m, x0p), a.steps, a.warmup, world, device)
@@ -182,6 +270,8 @@ def main(argv=None):
                 rec["verify"] = check(mine, torch.cat([u, i])[dg.row_begin:dg.row_end], True,
                                       world, device)
                 del g1, u, i
+            if world == 1 and not a.no_ref_check:
+                rec["verify_vs_torch_reference"] = verify_config3(g100, m, mine, device)
             emit(rec)
             del m, dg, x0p, mine
         if 4 in a.configs:
@@ -310,8 +400,7 @@ def main(argv=None):
             print(f"[bench_configs] operand built: {g.nnz} nnz in {build_s:.1f} s",
                   file=sys.stderr, flush=True)
             deg = (g.row_ptr[1:] - g.row_ptr[:-1]).cpu().numpy()
-            torch.manual_seed(0)
-            m = GAT(shape[0], shape[1], 64, 3, 4, 0.1, 0.2, 0.1).to(device).eval()
+            m = config5_model(shape, device)
             dg = DistributedGraph(g, rank, world, device)
             x0p = dg.pad_table(m._initial_table())
             t, mine = timed(lambda: gat_forward_dist(dg, m, x0p), a.steps, a.warmup, world, device)
@@ -328,6 +417,8 @@ def main(argv=None):
                 rec["verify"] = check(mine, torch.cat([u, i])[dg.row_begin:dg.row_end], False,
                                       world, device)
                 del g1, u, i
+            if world == 1 and not a.g1b and not a.no_ref_check:
+                rec["verify_vs_torch_reference"] = verify_config5(g, m, mine, device)
             emit(rec)
     if world > 1:
         dist.destroy_process_group()
