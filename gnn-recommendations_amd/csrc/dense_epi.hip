@@ -55,6 +55,14 @@ struct DenseParams {
   float w_out, w_res;
 };
 
+// MFMA contraction order of the dense transforms: step s of a chain (s < K/4) contracts
+// k = 16 (s / 4) + 4 g + (s % 4) in lane group g = lane >> 4. With that order a lane's A
+// operands for steps 4t .. 4t+3 are the row's columns 16t + 4g .. +3 — ONE float4 — so the
+// streaming transform feeds the matrix cores from registers (the rows_gemm form), and its B
+// fragments for those four steps are one ds_read_b128. spmm_mfma_kernel (the fused form)
+// contracts in the same order, so the split and the fused layers keep equal bits.
+__device__ __forceinline__ constexpr int mfma_k(int s, int g) { return 16 * (s >> 2) + 4 * g + (s & 3); }
+
 // GATHER = true: the A rows are gathered here (fused hop). GATHER = false: p.x already holds
 // the hop output n = A x (rows read straight, float4 per lane) and only the transform runs.
 template <int D, int MODE, int NW, bool GATHER>
@@ -98,7 +106,7 @@ __global__ __launch_bounds__(64 * NW) void spmm_mfma_kernel(DenseParams p) {
       const int t = wave + NW * i;
       const int j = 16 * ((t < TILES ? t : 0) % NT) + i16;
 #pragma unroll
-      for (int s = 0; s < STEPS; ++s) bf[i][s] = bval(4 * s + k4, j);
+      for (int s = 0; s < STEPS; ++s) bf[i][s] = bval(mfma_k(s, k4), j);
     }
   }
   float bias1[TPW], bias2[TPW];
@@ -196,13 +204,13 @@ __global__ __launch_bounds__(64 * NW) void spmm_mfma_kernel(DenseParams p) {
       if (t < TILES) {
         const int mt = t / NT, nt = t % NT;
         floatx4 c1 = {0.f, 0.f, 0.f, 0.f}, c2 = {0.f, 0.f, 0.f, 0.f};
-        const float* arow = &a_lds[(16 * mt + i16) * LDA + k4];
-        const float* bcol = &b_lds[k4 * LDB + 16 * nt + i16];
+        const float* arow = &a_lds[(16 * mt + i16) * LDA];
+        const float* bcol = &b_lds[16 * nt + i16];
 #pragma unroll
         for (int s = 0; s < STEPS; ++s) {
-          const float a = arow[4 * s];
+          const float a = arow[mfma_k(s, k4)];   // the streaming transform's k order
           float b;
-          if constexpr (B_LDS) b = bcol[4 * s * LDB]; else b = bf[i][s];
+          if constexpr (B_LDS) b = bcol[mfma_k(s, k4) * LDB]; else b = bf[i][s];
           if (MODE == 0 && s >= STEPS / 2)
             c2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c2, 0, 0, 0);
           else
@@ -279,25 +287,23 @@ __global__ __launch_bounds__(64 * NW) void spmm_mfma_kernel(DenseParams p) {
 }
 
 // Streaming transform for d = 64 (the split form's second kernel; n = A x is already in HBM):
-// every wave owns 16-row tiles on its own — no workgroup barrier inside the loop. Per tile it
-// stages [n | x (.) n] (MODE 0) or n (MODE 1) in its private LDS rows, runs the 16x16x4 f32
-// MFMA chains of all four 16-column output tiles (8 independent accumulators in MODE 0), the
-// GAS product on the matrix cores, and stores whole rows (float4). The next tile's rows are in
-// flight in registers meanwhile. Same MFMA instructions, fragment maps and k order as
-// spmm_mfma_kernel<64, MODE, 8, false>, so the same bits.
+// every wave owns 16-row tiles on its own — no workgroup barrier inside the loop. Lane
+// (i16, g) holds row i16's columns 16t + 4g .. +3 (t < 4) of n and x in registers, forms
+// x (.) n there, and runs the 16x16x4 f32 MFMA chains of all four 16-column output tiles
+// (c1: n @ W1^T, c2: (x (.) n) @ W2^T — the reference's two Linear layers, kept apart for
+// (c1 + b1) + (c2 + b2)) with B read from LDS as one float4 per 4 steps; bias, LeakyReLU and
+// the GAS product (VALU for 8x8 blocks, else on the matrix cores) run from a private o tile,
+// and whole rows are stored (float4). The next tile's rows are in flight in registers.
 template <int MODE, int NW, bool GASV>
 __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
   constexpr int D = 64;
-  constexpr int KD = MODE == 0 ? 2 * D : D;
-  constexpr int LDA = KD + 2;        // == 2 mod 32: conflict-free A-fragment reads
+  constexpr int NP = MODE == 0 ? 2 : 1;   // contraction parts: n (W1) [, x (.) n (W2)]
   constexpr int LDO = D + 4;
-  constexpr int LDB = D + 16;        // == 16 mod 32: conflict-free B-fragment reads
-  constexpr int STEPS = KD / 4;
-  constexpr int TSZ = 16 * (LDA > LDO ? LDA : LDO);   // the o tile aliases the A tile
-  __shared__ __attribute__((aligned(16))) float b_lds[KD * LDB];
+  constexpr int LDB = D + 16;             // dense GAS matrix (non-8x8 blocks), as before
+  // B fragments: [part][t][nt][lane][q] = B_part[k = 16t + 4(lane>>4) + q][j = 16nt + (lane&15)]
+  __shared__ __attribute__((aligned(16))) float b_lds[NP * 4 * 4 * 64 * 4];
   __shared__ __attribute__((aligned(16))) float g_lds[MODE == 0 && !GASV ? D * LDB : 4];
-  __shared__ __attribute__((aligned(16))) float t_lds[NW][TSZ];
-  // GAS with 8x8 blocks on the VALU (below): the blocks [b][c][e] and the inverse permutation
+  __shared__ __attribute__((aligned(16))) float t_lds[NW][16 * LDO];
   constexpr int kVbs = 8;
   __shared__ __attribute__((aligned(16))) float wv_lds[MODE == 0 && GASV ? D * kVbs : 4];
   __shared__ int inv_lds[MODE == 0 && GASV ? D : 1];
@@ -305,21 +311,20 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int i16 = lane & 15, k4 = lane >> 4;
-  float* at = t_lds[wave];
-  for (int e = threadIdx.x; e < KD * D; e += 64 * NW) {
-    const int k = e / D, j = e % D;
+  float* ot = t_lds[wave];
+  for (int e = threadIdx.x; e < NP * 4096; e += 64 * NW) {
+    const int q = e & 3, l = (e >> 2) & 63, nt = (e >> 8) & 3, t = (e >> 10) & 3, part = e >> 12;
+    const int k = 16 * t + 4 * (l >> 4) + q, j = 16 * nt + (l & 15);
     float v;
-    if (MODE == 0) v = k < D ? p.W1[j * D + k] : p.W2[j * D + (k - D)];
+    if (MODE == 0) v = part == 0 ? p.W1[j * D + k] : p.W2[j * D + k];
     else v = p.M[k * D + j];
-    b_lds[k * LDB + j] = v;
+    b_lds[e] = v;
   }
   const bool gas = MODE == 0 && p.gas_blocks != nullptr;
   // 8x8 blocks: the GAS product runs on the VALU, 8 fmaf per output in the oracle's order
   // (oracle_gas: c ascending from +0), instead of as a dense 64x64 MFMA product that spends 7/8
-  // of its work on zeros — a third of the kernel's matrix-core time (profiles/r02/
-  // config3_transform_mfma_pmc.json: 24M MFMA per launch, 8M of them GAS)
-  // (GASV instances are launched for 8x8 blocks only; they hold no dense G in LDS, which
-  // leaves room for 12 waves per workgroup)
+  // of its work on zeros (profiles/r02/config3_transform_mfma_pmc.json: 24M MFMA per launch,
+  // 8M of them GAS). GASV instances are launched for 8x8 blocks only.
   constexpr bool gas_valu = GASV;
   if (gas_valu) {
     for (int e = threadIdx.x; e < D * kVbs; e += 64 * NW) wv_lds[e] = p.gas_blocks[e];
@@ -342,35 +347,34 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
   }
   __syncthreads();
 
-  // row loads: lane covers rows 4 it + (lane >> 4), columns 4 (lane & 15) .. +3, it = 0..3
-  const int lr = lane >> 4, lc = 4 * (lane & 15);
   const int64_t n_tiles = ceil_div(p.A.n_rows, 16);
   const int64_t stride = (int64_t)gridDim.x * NW;
+  // A operands: lane (i16, k4) loads row i16's float4 at columns 16t + 4 k4 (t < 4)
   float4 pn[4], px[4];
   auto load = [&](int64_t tile) {
+    const int64_t r = tile * 16 + i16;
+    const bool ok = tile < n_tiles && r < p.A.n_rows;
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int64_t r = tile * 16 + 4 * it + lr;
-      pn[it] = px[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (tile < n_tiles && r < p.A.n_rows) {
-        pn[it] = *reinterpret_cast<const float4*>(p.x + r * p.ldx + lc);
-        if (MODE == 0) px[it] = *reinterpret_cast<const float4*>(p.x_self + r * p.ld_self + lc);
+    for (int t = 0; t < 4; ++t) {
+      pn[t] = px[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ok) {
+        pn[t] = *reinterpret_cast<const float4*>(p.x + r * p.ldx + 16 * t + 4 * k4);
+        if (MODE == 0) px[t] = *reinterpret_cast<const float4*>(p.x_self + r * p.ld_self + 16 * t + 4 * k4);
       }
     }
   };
+  // output rows: lane covers rows 4 it + (lane >> 4), columns 4 (lane & 15) .. +3, it = 0..3
+  const int lr = lane >> 4, lc = 4 * (lane & 15);
   int64_t tile = (int64_t)blockIdx.x * NW + wave;
   load(tile);
   for (; tile < n_tiles; tile += stride) {
-    // stage this tile, then start the next one's loads
+    float an[4][4], ax[4][4];
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      float* ar = at + (4 * it + lr) * LDA + lc;
-      const float nv[4] = {pn[it].x, pn[it].y, pn[it].z, pn[it].w};
-      const float xv[4] = {px[it].x, px[it].y, px[it].z, px[it].w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        ar[q] = nv[q];
-        if (MODE == 0) ar[D + q] = xv[q] * nv[q];
+    for (int t = 0; t < 4; ++t) {
+      an[t][0] = pn[t].x; an[t][1] = pn[t].y; an[t][2] = pn[t].z; an[t][3] = pn[t].w;
+      if (MODE == 0) {
+        ax[t][0] = px[t].x * pn[t].x; ax[t][1] = px[t].y * pn[t].y;
+        ax[t][2] = px[t].z * pn[t].z; ax[t][3] = px[t].w * pn[t].w;
       }
     }
     float4 rs[4];   // MODE 1 residual rows (loaded with the tile, used at the store)
@@ -383,25 +387,33 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
       }
     }
     load(tile + stride);
-    // MFMA: c1 over k < D, c2 over k >= D (MODE 0: the reference's two Linear layers)
     floatx4 c1[4], c2[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) c1[nt] = c2[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
-    const float* arow = at + i16 * LDA + k4;
+    const float4* bl = reinterpret_cast<const float4*>(b_lds) + lane;
 #pragma unroll
-    for (int s = 0; s < STEPS; ++s) {
-      const float a = arow[4 * s];
+    for (int t = 0; t < 4; ++t) {
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) {
-        const float b = b_lds[(4 * s + k4) * LDB + 16 * nt + i16];
-        if (MODE == 0 && s >= STEPS / 2)
-          c2[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c2[nt], 0, 0, 0);
-        else
-          c1[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c1[nt], 0, 0, 0);
+        const float4 b = bl[(t * 4 + nt) * 64];
+        const float bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c1[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(an[t][q], bv[q], c1[nt], 0, 0, 0);
       }
+      if (MODE == 0) {
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          const float4 b = bl[((4 + t) * 4 + nt) * 64];
+          const float bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) c2[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ax[t][q], bv[q], c2[nt], 0, 0, 0);
+        }
+      }
+      // keep the B reads of step group t next to their MFMAs (hoisting all 32 float4 ahead
+      // costs 128 VGPRs and spills)
+      __builtin_amdgcn_sched_barrier(0);
     }
-    // o tile (rows 4 k4 + q, column 16 nt + i16) over the A tile (all its reads are done)
-    float* ot = at;
+    // o tile (rows 4 k4 + q, column 16 nt + i16)
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll

@@ -156,8 +156,9 @@ def test_gat_refuses_dense_fallback_on_large_graph(cuda):
     from src.models.baselines.gat import GAT_DENSE_MAX_NODES
     nu = ni = GAT_DENSE_MAX_NODES // 2 + 10
     rng = np.random.default_rng(0)
-    u = np.concatenate([np.arange(nu), rng.integers(0, nu, 4 * nu)])
-    i = np.concatenate([rng.integers(0, ni, nu), rng.integers(0, ni, 4 * nu)])
+    # every node has a neighbour (an isolated node is a NaN row by design)
+    u = np.concatenate([np.arange(nu), rng.integers(0, nu, ni), rng.integers(0, nu, 4 * nu)])
+    i = np.concatenate([rng.integers(0, ni, nu), np.arange(ni), rng.integers(0, ni, 4 * nu)])
     g = CsrGraph.from_interactions(u, i, nu, ni).to(cuda)
     torch.manual_seed(0)
     m = GAT(nu, ni, embedding_dim=64, n_layers=3, n_heads=4, dropout=0.0).to(cuda).eval()

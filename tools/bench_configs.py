@@ -56,6 +56,19 @@ from src.ops.distributed import (DistributedGraph, gat_forward_dist,  # noqa: E4
                                  lightgcn_propagate_dist, make_work, ngcf_forward_dist)
 
 
+def progress(msg: str) -> None:
+    """Phase line with host RSS and device memory (stderr, line-buffered): a run that dies
+    leaves the phase it died in."""
+    try:
+        import psutil
+        rss = psutil.Process().memory_info().rss / 2**30
+    except Exception:  # noqa: BLE001
+        rss = float("nan")
+    dev = torch.cuda.memory_allocated() / 2**30 if torch.cuda.is_available() else 0.0
+    print(f"[bench_configs {time.strftime('%H:%M:%S')}] {msg} | host RSS {rss:.1f} GiB, "
+          f"device {dev:.1f} GiB", file=sys.stderr, flush=True)
+
+
 def zipf_ids(rng, n: int, count: int, a: float, chunk: int = 1 << 26) -> np.ndarray:
     """`count` ids in [0, n) with P(k) ~ (k+1)^-a (inverse CDF of the continuous power law on
     [1, n+1), vectorised in chunks; rng.choice over 10M categories would take minutes)."""
@@ -79,7 +92,7 @@ def powerlaw_graph(n_users, n_items, n_pairs, a, seed, threads=16, device=None):
     # min degree >= 1 (the reference's dense GAT turns an isolated node into all-NaN)
     u = np.concatenate([u, np.arange(n_users), rng.integers(0, n_users, n_items)])
     i = np.concatenate([i, rng.integers(0, n_items, n_users), np.arange(n_items)])
-    print(f"[bench_configs] {u.size} pairs sampled", file=sys.stderr, flush=True)
+    progress(f"{u.size} pairs sampled")
     if device is not None:
         return CsrGraph.from_interactions_device(u, i, n_users, n_items, binary=True,
                                                  device=device)
@@ -215,6 +228,11 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--g1b", action="store_true", help="config 5 at full size (10M x 10M, 1B pairs)")
+    ap.add_argument("--c5-shape", type=int, nargs=3, default=None, metavar=("USERS", "ITEMS", "PAIRS"),
+                    help="config 5 at another size (operand built on the device)")
+    ap.add_argument("--host-build", action="store_true",
+                    help="config 5 --g1b / --c5-shape: build the operand on the host (the form "
+                         "round 2's G1B run completed with; profiles/r03/g1b_box_loss_record.md)")
     ap.add_argument("--verify", action="store_true")
     ap.add_argument("--no-ref-check", action="store_true",
                     help="N = 1: skip the per-config check against the reference's composition "
@@ -394,16 +412,24 @@ def main(argv=None):
         torch.cuda.empty_cache()
         if 5 in a.configs:
             t0 = time.time()
-            shape = (10_000_000, 10_000_000, 1_000_000_000) if a.g1b else (2_000_000, 2_000_000, 50_000_000)
-            g = powerlaw_graph(*shape, 0.9, 0, threads, device=device if a.g1b else None)
+            big = a.g1b or a.c5_shape is not None
+            shape = (tuple(a.c5_shape) if a.c5_shape else
+                     (10_000_000, 10_000_000, 1_000_000_000) if a.g1b else (2_000_000, 2_000_000, 50_000_000))
+            progress(f"config 5: sampling {shape}")
+            g = powerlaw_graph(*shape, 0.9, 0, threads,
+                               device=device if big and not a.host_build else None)
             build_s = time.time() - t0
-            print(f"[bench_configs] operand built: {g.nnz} nnz in {build_s:.1f} s",
-                  file=sys.stderr, flush=True)
+            progress(f"operand built: {g.nnz} nnz in {build_s:.1f} s")
             deg = (g.row_ptr[1:] - g.row_ptr[:-1]).cpu().numpy()
             m = config5_model(shape, device)
             dg = DistributedGraph(g, rank, world, device)
             x0p = dg.pad_table(m._initial_table())
+            progress("shard + x0 ready; first forward")
+            gat_forward_dist(dg, m, x0p)
+            torch.cuda.synchronize()
+            progress("first forward done; timing")
             t, mine = timed(lambda: gat_forward_dist(dg, m, x0p), a.steps, a.warmup, world, device)
+            progress(f"timed: {t:.2f} ms per forward")
             rec = {"config": 5, "workload": f"power-law {shape[0]}x{shape[1]} ({shape[2]} pairs, "
                    f"Zipf 0.9, seed 0) GAT d=64 4 heads K=3 forward", "nnz": g.nnz,
                    "max_degree": int(deg.max()), "median_degree": float(np.median(deg)),
@@ -417,7 +443,7 @@ def main(argv=None):
                 rec["verify"] = check(mine, torch.cat([u, i])[dg.row_begin:dg.row_end], False,
                                       world, device)
                 del g1, u, i
-            if world == 1 and not a.g1b and not a.no_ref_check:
+            if world == 1 and not big and not a.no_ref_check:
                 rec["verify_vs_torch_reference"] = verify_config5(g, m, mine, device)
             emit(rec)
     if world > 1:
