@@ -390,27 +390,45 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
     floatx4 c1[4], c2[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) c1[nt] = c2[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // B of step group t (4 MFMA steps) for every (part, nt): 8 float4, double-buffered so the
+    // next group's LDS reads fly under this group's 32 MFMAs; the MFMAs cycle over the 8
+    // independent accumulators (no dependent back-to-back issue), each chain in (t, q) order
     const float4* bl = reinterpret_cast<const float4*>(b_lds) + lane;
+    float4 bc[NP][4], bn[NP][4];
+    auto load_b = [&](int t, float4 (&b)[NP][4]) {
+#pragma unroll
+      for (int part = 0; part < NP; ++part)
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) b[part][nt] = bl[((part * 4 + t) * 4 + nt) * 64];
+    };
+    load_b(0, bc);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
+      if (t < 3) load_b(t + 1, bn);
+      __builtin_amdgcn_sched_barrier(0);   // the next group's reads issue before these MFMAs
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        const float4 b = bl[(t * 4 + nt) * 64];
-        const float bv[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) c1[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(an[t][q], bv[q], c1[nt], 0, 0, 0);
-      }
-      if (MODE == 0) {
+      for (int q = 0; q < 4; ++q) {
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
-          const float4 b = bl[((4 + t) * 4 + nt) * 64];
-          const float bv[4] = {b.x, b.y, b.z, b.w};
+          const float b = q == 0 ? bc[0][nt].x : q == 1 ? bc[0][nt].y : q == 2 ? bc[0][nt].z : bc[0][nt].w;
+          c1[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(an[t][q], b, c1[nt], 0, 0, 0);
+        }
+        if (MODE == 0) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) c2[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ax[t][q], bv[q], c2[nt], 0, 0, 0);
+          for (int nt = 0; nt < 4; ++nt) {
+            const float b = q == 0 ? bc[NP - 1][nt].x : q == 1 ? bc[NP - 1][nt].y
+                          : q == 2 ? bc[NP - 1][nt].z : bc[NP - 1][nt].w;
+            c2[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ax[t][q], b, c2[nt], 0, 0, 0);
+          }
         }
       }
-      // keep the B reads of step group t next to their MFMAs (hoisting all 32 float4 ahead
-      // costs 128 VGPRs and spills)
+      if (t < 3) {
+#pragma unroll
+        for (int part = 0; part < NP; ++part)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt) bc[part][nt] = bn[part][nt];
+      }
+      // keep each group's B reads next to its MFMAs (hoisting all 32 float4 costs 128 VGPRs)
       __builtin_amdgcn_sched_barrier(0);
     }
     // o tile (rows 4 k4 + q, column 16 nt + i16)
@@ -643,7 +661,7 @@ namespace {
 //  * fused (no workspace): gather + MFMA in one kernel.
 // Waves per workgroup: 8 for d <= 64 (weights in LDS), 4 for d = 128 (weights in VGPRs).
 #ifndef GNNREC_TRANSFORM_GASV_WAVES
-#define GNNREC_TRANSFORM_GASV_WAVES 12
+#define GNNREC_TRANSFORM_GASV_WAVES 8
 #endif
 template <int MODE, bool GATHER>
 int launch_dense(const DenseParams& p, int d, hipStream_t s) {

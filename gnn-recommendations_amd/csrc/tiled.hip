@@ -50,8 +50,17 @@ constexpr int kGroups = GNNREC_TILED_GROUPS;      // slot streams per wave (8 la
 constexpr int kSteps = GNNREC_TILED_STEPS;        // steps per chunk
 constexpr int kTiledChunk = GNNREC_TILED_CHUNK;   // slots per chunk (one per lane)
 constexpr int kTiledTail = GNNREC_TILED_TAIL;
-constexpr int kSlice = 32;                        // features per pass
-constexpr int kRowBytes = kSlice * 4;             // one LDS accumulator row, one gathered line
+constexpr int kSlice = 32;                        // features per gathered line
+constexpr int kRowBytes = kSlice * 4;             // one gathered line
+#ifndef GNNREC_TILED_SPW
+#define GNNREC_TILED_SPW 1
+#endif
+// Slices per plan walk (experiment builds, DESIGN.md §3.1c "one plan walk"): SPW = 2 walks the
+// plan once for two adjacent 32-feature slices — every slot gathers two 128-B lines and the
+// LDS accumulator rows are 256 B, so a block holds half the rows.
+constexpr int kSPW = GNNREC_TILED_SPW;
+constexpr int kAccBytes = kRowBytes * kSPW;       // one LDS accumulator row
+static_assert(kSPW == 1 || kSPW == 2, "1 or 2 slices per plan walk");
 constexpr int kRowBits = 11;
 constexpr int kRowMask = (1 << kRowBits) - 1;
 constexpr int kMaxPanel = 1 << 20;                // columns per panel (slot word: 21 bits)
@@ -98,7 +107,7 @@ static_assert(kTiledChunk == kGroups * kSteps && kTiledChunk == 64, "one slot pe
 static_assert(kGroups == 8 && kSteps == 8, "a stream is 8 lanes: half a 16-lane DPP row");
 static_assert(kSteps == 2 * kApply || kSteps == kApply, "a chunk is one or two apply groups");
 static_assert(GNNREC_TILED_MAX_ROWS < kRowMask, "row field is 11 bits (row R = scratch)");
-static_assert((GNNREC_TILED_MAX_ROWS + 1) * kRowBytes <= 160 * 1024, "LDS");
+static_assert(kSPW > 1 || (GNNREC_TILED_MAX_ROWS + 1) * kRowBytes <= 160 * 1024, "LDS");
 static_assert((int64_t)kMaxPanel * kMaxRowBytes <= ((int64_t)1 << 32), "32-bit lane offsets");
 
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -142,7 +151,7 @@ struct TiledSlots {   // this lane's slot of the chunk: stream lane / 8, step la
 // accumulator rows; the value is formed once per chunk per lane — the same fp32 product the
 // operand's builder stored, so the same bits.
 constexpr int kMaxClasses = GNNREC_TILED_MAX_CLASSES;
-static_assert(GNNREC_TILED_MAX_ROWS_FACTORED * (kRowBytes + 4) + kRowBytes + 4 +
+static_assert(kSPW > 1 || GNNREC_TILED_MAX_ROWS_FACTORED * (kRowBytes + 4) + kRowBytes + 4 +
                       kMaxClasses * 4 <= 160 * 1024, "LDS of a factored plan");
 
 // Slot t of every stream to the stream's 8 lanes: within a 16-lane DPP row, lanes 0-7 (stream
@@ -209,8 +218,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const char* xs, uin
 // range ends right after the last row's slice, so offsets of later rows are out of range.
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* p, int64_t r0,
                                                             int64_t ld, int slice, int rows) {
-  const float* b = p ? p + r0 * ld + (int64_t)slice * kSlice : p;
-  const uint32_t n = p ? (uint32_t)(rows - 1) * (uint32_t)ld * 4u + kRowBytes : 0u;
+  const float* b = p ? p + r0 * ld + (int64_t)slice * kSlice * kSPW : p;
+  const uint32_t n = p ? (uint32_t)(rows - 1) * (uint32_t)ld * 4u + kAccBytes : 0u;
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(b), 0, (int)n, 0x00020000);
 }
 
@@ -236,12 +245,17 @@ template <int... T>
 __device__ __forceinline__ void tiled_gather(std::integer_sequence<int, T...>,
                                              __amdgpu_buffer_rsrc_t xr, uint32_t q16,
                                              uint32_t row_bytes, const TiledSlots& m,
-                                             f4 (&x)[kSteps]) {
+                                             f4 (&x)[kSteps][kSPW]) {
   const uint32_t o = __umul24(m.w >> kRowBits, row_bytes);   // this lane's slot's source row
   if constexpr (GNNREC_TILED_EXP & 2) {
-    ((x[T] = f4{__builtin_bit_cast(float, gbcast<T>(o)), 1.f, 1.f, 1.f}), ...);
+    ((x[T][0] = f4{__builtin_bit_cast(float, gbcast<T>(o)), 1.f, 1.f, 1.f}), ...);
+    if constexpr (kSPW > 1) ((x[T][kSPW - 1] = x[T][0]), ...);
+  } else if constexpr (kSPW == 1) {
+    ((x[T][0] = load4(xr, gbcast<T>(o) + q16)), ...);
   } else {
-    ((x[T] = load4(xr, gbcast<T>(o) + q16)), ...);
+    uint32_t ot[sizeof...(T)];
+    ((ot[T] = gbcast<T>(o) + q16), ...);
+    ((x[T][0] = load4(xr, ot[T]), x[T][1] = load4(xr, ot[T] + kRowBytes)), ...);
   }
 }
 
@@ -283,12 +297,12 @@ __device__ __forceinline__ f4 fma4(float v, f4 x, f4 a) {
 // of a row each). A chunk is applied as two such groups, so a row may appear in both groups
 // of a stream: the second group's reads follow the first group's writes in the wave's LDS
 // order (and a slot at step 4 chaining on step 3 selects the value step 3 just wrote).
-template <bool CHAIN, int G, int... T>
+template <bool CHAIN, int G, int S, int... T>
 __device__ __forceinline__ void tiled_apply4(std::integer_sequence<int, T...>, char* base,
                                              uint32_t q16, uint32_t r, const TiledSlots& m,
-                                             const f4 (&x)[kSteps], uint64_t cm, f4& prev) {
+                                             const f4 (&x)[kSteps][kSPW], uint64_t cm, f4& prev) {
   uint32_t a[sizeof...(T)];
-  ((a[T] = gbcast<G + T>(r) + q16), ...);
+  ((a[T] = gbcast<G + T>(r) + q16 + S * kRowBytes), ...);
   f4 av[sizeof...(T)];
   if constexpr (GNNREC_TILED_EXP & 1)
     ((av[T] = f4{__builtin_bit_cast(float, a[T]), 0.f, 0.f, 0.f}), ...);
@@ -296,13 +310,13 @@ __device__ __forceinline__ void tiled_apply4(std::integer_sequence<int, T...>, c
     ((av[T] = *reinterpret_cast<const f4*>(base + a[T])), ...);
   if constexpr (CHAIN) {
     // slot t continuing slot t-1's row (same stream) chains on its register value
-    ((av[T] = fma4(gbcastf<G + T>(m.v), x[G + T],
+    ((av[T] = fma4(gbcastf<G + T>(m.v), x[G + T][S],
                    G + T > 0 ? select4(av[T], T > 0 ? av[T > 0 ? T - 1 : 0] : prev,
                                        chain_lanes<G + T>(cm))
                              : av[T])),
      ...);
   } else {
-    ((av[T] = fma4(gbcastf<G + T>(m.v), x[G + T], av[T])), ...);
+    ((av[T] = fma4(gbcastf<G + T>(m.v), x[G + T][S], av[T])), ...);
   }
   if constexpr (GNNREC_TILED_EXP & 1)
     prev = prev + ((av[T]) + ...);
@@ -313,14 +327,22 @@ __device__ __forceinline__ void tiled_apply4(std::integer_sequence<int, T...>, c
 
 template <bool CHAIN>
 __device__ __forceinline__ void tiled_apply(float* acc, uint32_t q16, const TiledSlots& m,
-                                            const f4 (&x)[kSteps], uint64_t cm, f4& sink) {
+                                            const f4 (&x)[kSteps][kSPW], uint64_t cm, f4& sink) {
   constexpr auto k4 = std::make_integer_sequence<int, kApply>{};
   char* base = reinterpret_cast<char*>(acc);
-  f4 prev = (GNNREC_TILED_EXP & 1) ? sink : f4{0.f, 0.f, 0.f, 0.f};
-  const uint32_t r = (m.w & kRowMask) * kRowBytes;   // this lane's slot's accumulator row
-  tiled_apply4<CHAIN, 0>(k4, base, q16, r, m, x, cm, prev);
-  if constexpr (kApply < kSteps) tiled_apply4<CHAIN, kApply>(k4, base, q16, r, m, x, cm, prev);
-  if (GNNREC_TILED_EXP & 1) sink = prev;
+  const uint32_t r = (m.w & kRowMask) * kAccBytes;   // this lane's slot's accumulator row
+  // the slices of a walk are independent chains over the same slots
+  {
+    f4 prev = (GNNREC_TILED_EXP & 1) ? sink : f4{0.f, 0.f, 0.f, 0.f};
+    tiled_apply4<CHAIN, 0, 0>(k4, base, q16, r, m, x, cm, prev);
+    if constexpr (kApply < kSteps) tiled_apply4<CHAIN, kApply, 0>(k4, base, q16, r, m, x, cm, prev);
+    if (GNNREC_TILED_EXP & 1) sink = prev;
+  }
+  if constexpr (kSPW > 1) {
+    f4 prev = {0.f, 0.f, 0.f, 0.f};
+    tiled_apply4<CHAIN, 0, 1>(k4, base, q16, r, m, x, cm, prev);
+    if constexpr (kApply < kSteps) tiled_apply4<CHAIN, kApply, 1>(k4, base, q16, r, m, x, cm, prev);
+  }
 }
 
 // Pass-end epilogue of one 8-lane group: its rows i = rl + 128 j of the block (rl = 8 * wave
@@ -344,7 +366,7 @@ __device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, 
   constexpr int kStride = kGroups * kTiledWaves;
   const __amdgpu_buffer_rsrc_t rb[3] = {rb0, rb1, rb2};
   const uint32_t lb[3] = {lb0, lb1, lb2};
-  f4 base[NB > 0 ? NB : 1][B];
+  f4 base[NB > 0 ? NB : 1][B][kSPW];
   // the base rows of batch i0 (global, independent of the pass: the first batch is loaded
   // before the pass-end barriers, so its latency hides behind the block's slowest wave)
   auto load_base = [&](int i0) {
@@ -360,7 +382,8 @@ __device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, 
     for (int q = 0; q < B; ++q)
 #pragma unroll
       for (int j = 0; j < NB; ++j) {
-        base[j][q] = load4_base(rb[j], ob[j]);
+#pragma unroll
+        for (int sl = 0; sl < kSPW; ++sl) base[j][q][sl] = load4_base(rb[j], ob[j] + sl * kRowBytes);
         ob[j] += kStride * lb[j];
       }
   };
@@ -374,27 +397,33 @@ __device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, 
     if (!GNNREC_TILED_EPI_PRELOAD) load_base(i0);
     uint32_t ol = (uint32_t)i0;
     asm volatile("" : "+v"(ol));
-    f4 a[B];
+    f4 a[B][kSPW];
 #pragma unroll
     for (int q = 0; q < B; ++q) {
-      a[q] = *reinterpret_cast<const f4*>(lds + min(ol, (uint32_t)R) * kRowBytes + q16);
+#pragma unroll
+      for (int sl = 0; sl < kSPW; ++sl)
+        a[q][sl] = *reinterpret_cast<const f4*>(lds + min(ol, (uint32_t)R) * kAccBytes +
+                                                sl * kRowBytes + q16);
       ol += kStride;
     }
     uint32_t oy = (uint32_t)i0 * ly + q16, oa = (uint32_t)i0 * la + q16;
     asm volatile("" : "+v"(oy), "+v"(oa));
 #pragma unroll
     for (int q = 0; q < B; ++q) {
-      store4(a[q], ry, oy);
-      oy += kStride * ly;
-      if (NB > 0) {
-        f4 bsum = base[0][q];
 #pragma unroll
-        for (int j = 1; j < NB; ++j) bsum = bsum + base[j][q];
-        bsum = bsum + a[q];
-        if (div) bsum = bsum / acc_div;
-        store4(bsum, ra, oa);
-        oa += kStride * la;
+      for (int sl = 0; sl < kSPW; ++sl) {
+        store4(a[q][sl], ry, oy + sl * kRowBytes);
+        if (NB > 0) {
+          f4 bsum = base[0][q][sl];
+#pragma unroll
+          for (int j = 1; j < NB; ++j) bsum = bsum + base[j][q][sl];
+          bsum = bsum + a[q][sl];
+          if (div) bsum = bsum / acc_div;
+          store4(bsum, ra, oa + sl * kRowBytes);
+        }
       }
+      oy += kStride * ly;
+      if (NB > 0) oa += kStride * la;
     }
     i0 += kStride * B;
     if (i0 - (rl & (kGroups - 1)) >= R) break;   // wave-uniform: the wave's first row
@@ -423,7 +452,7 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
   extern __shared__ f4 acc4[];   // [(R+1)][32] floats: row R is the padding slots' scratch row
   float* acc = reinterpret_cast<float*>(acc4);
   // factored plans: the block's row factors [R+1] (row R: 0) and the class table [kMaxClasses]
-  float* rfl = acc + (R + 1) * kSlice;
+  float* rfl = acc + (R + 1) * kSlice * kSPW;
   float* ctl = rfl + (R + 1);
   if constexpr (FACT)
     for (int i = threadIdx.x; i < kMaxClasses; i += kTiledWaves * 64)
@@ -452,7 +481,7 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     if (blk >= n_blocks) continue;   // padding item (uniform over the workgroup)
     {
       const f4 z = {0.f, 0.f, 0.f, 0.f};
-      for (int i = threadIdx.x; i < (R + 1) * (kSlice / 4); i += kTiledWaves * 64) acc4[i] = z;
+      for (int i = threadIdx.x; i < (R + 1) * (kSlice * kSPW / 4); i += kTiledWaves * 64) acc4[i] = z;
       if constexpr (FACT) {
         const int r0 = blk * R;
         for (int i = threadIdx.x; i <= R; i += kTiledWaves * 64)
@@ -461,7 +490,7 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     }
     __syncthreads();
     GNNREC_TILED_STAMP(ev);
-    const uint32_t soff = (uint32_t)slice * kRowBytes;
+    const uint32_t soff = (uint32_t)slice * kAccBytes;
     const char* xs = reinterpret_cast<const char*>(x) + soff;
     const uint64_t xs_bytes = (uint64_t)x_rows32 * row_bytes - soff;
     const int64_t s = (int64_t)blk * kTiledWaves + w;
@@ -472,7 +501,7 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
       // a ring of kPlanAhead + 1 slot sets and kGatherAhead + 1 gathered chunks: stage c loads
       // chunk c + kPlanAhead's slots, gathers chunk c + kGatherAhead and applies chunk c
       TiledSlots M[kMRing];
-      f4 X[kXRing][kSteps];
+      f4 X[kXRing][kSteps][kSPW];
       const int nc = (int)(e - b);   // this wave's chunks of the pass
       int c = 0;
 #pragma unroll
@@ -509,7 +538,7 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
       };
       run_ring(std::make_integer_sequence<int, kRingUnroll>{}, stage);
     }
-    if (GNNREC_TILED_EXP & 1) *reinterpret_cast<f4*>(reinterpret_cast<char*>(acc) + R * kRowBytes + q16) = sink;
+    if (GNNREC_TILED_EXP & 1) *reinterpret_cast<f4*>(reinterpret_cast<char*>(acc) + R * kAccBytes + q16) = sink;
     const int ns = nsteps[blk];
     auto wait = [&]() {
       for (int i = cur; i < ns; ++i) {  // this wave's remaining steps + the last
@@ -841,8 +870,8 @@ extern "C" int gnnrec_spmm_tiled_supported(int32_t device, int32_t rows_per_bloc
   int cur = 0;
   if (hipGetDevice(&cur) != hipSuccess) return 0;
   if (device != cur && hipSetDevice(device) != hipSuccess) return 0;
-  const size_t lds = (size_t)(rows_per_block + 1) * kRowBytes;
-  const int ok = lds <= 64 * 1024 || tiled_lds_attribute(device) > 0;
+  const size_t lds = (size_t)(rows_per_block + 1) * kAccBytes;
+  const int ok = lds <= 160 * 1024 && (lds <= 64 * 1024 || tiled_lds_attribute(device) > 0);
   if (device != cur) (void)hipSetDevice(cur);
   return ok;
 }
@@ -858,8 +887,8 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
                                      int64_t ld_acc, float acc_div, const float* prev,
                                      int64_t ld_prev, uint32_t* sync, int32_t meet_us,
                                      gnnrec_stream_t stream) {
-  GNNREC_REQUIRE(d > 0 && d % kSlice == 0, "spmm_tiled: d must be a multiple of 32 (got %d)",
-                 (int)d);
+  GNNREC_REQUIRE(d > 0 && d % (kSlice * kSPW) == 0,
+                 "spmm_tiled: d must be a multiple of %d (got %d)", kSlice * kSPW, (int)d);
   GNNREC_REQUIRE(rows_per_block >= 1 && rows_per_block <= GNNREC_TILED_MAX_ROWS,
                  "spmm_tiled: bad rows_per_block");
   GNNREC_REQUIRE(n_rows >= 0 && n_blocks == (n_rows + rows_per_block - 1) / rows_per_block,
@@ -909,15 +938,17 @@ extern "C" int gnnrec_spmm_tiled_f32(const uint32_t* slot, const float* val,
   if (hipGetDevice(&dev) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     cus = 256;
-  const size_t lds = (size_t)(rows_per_block + 1) * kRowBytes +
+  const size_t lds = (size_t)(rows_per_block + 1) * kAccBytes +
                      (fact ? (size_t)(rows_per_block + 1) * 4 + kMaxClasses * 4 : 0);
+  GNNREC_REQUIRE(lds <= 160 * 1024, "spmm_tiled: %d rows per block need %zu B of LDS (> 160 KB)",
+                 (int)rows_per_block, lds);
   if (lds > 64 * 1024 && tiled_lds_attribute(dev) < 0) {
     set_error("spmm_tiled: the device refused %zu bytes of dynamic LDS", lds);
     return GNNREC_EHIP;
   }
   const int64_t grid = std::min<int64_t>(cus, n_blocks);
   const int64_t nb_pad = ceil_div(n_blocks, grid) * grid;   // every slice starts a pass
-  const int64_t n_items = (int64_t)(d / kSlice) * nb_pad;
+  const int64_t n_items = (int64_t)(d / (kSlice * kSPW)) * nb_pad;
   GNNREC_REQUIRE(n_items < INT32_MAX && n_rows < INT32_MAX && x_rows < INT32_MAX,
                  "spmm_tiled: too many blocks / rows");
   if (hipMemsetAsync(sync, 0, GNNREC_TILED_SYNC_WORDS * sizeof(uint32_t), s) != hipSuccess)
