@@ -152,6 +152,7 @@ class Layout:
         self.x0_pad = None
         self.work = None
         self.plan_s = 0.0
+        self.plan_phases = None
         self.tiled = False
         self.timer = HopTimer()
         self.xtimer = ExchangeTimer(self.dg) if self.dg.world > 1 else None
@@ -161,9 +162,13 @@ class Layout:
         self.work = make_work(self.dg, self.x0_pad.shape[1], device)
         # operand re-layout for the column-ordered hop (built once, outside the timed region)
         t1 = time.perf_counter()
-        self.tiled = F.tiled_plan_for(self.dg.shard, self.x0_pad) is not None
+        plan = F.tiled_plan_for(self.dg.shard, self.x0_pad)
+        self.tiled = plan is not None
         torch.cuda.synchronize()
         self.plan_s = time.perf_counter() - t1
+        # phase times inside it (CsrGraph.tiled_plan: device planner, degree factors, factor
+        # check), each synchronised; the rest of plan_s is the first call's setup
+        self.plan_phases = plan.get("build_s") if plan is not None else None
         return self
 
     def release(self):
@@ -715,7 +720,8 @@ def main(argv=None) -> int:
             },
             "cpu_baseline": cpu,
             "vendor": vendor,
-            "operand_prep_s": {"tiled_plan_build": plan_s if tiled else None},
+            "operand_prep_s": {"tiled_plan_build": plan_s if tiled else None,
+                               "phases": lay.plan_phases},
             "edges_per_s_per_interaction": value / 2.0,
             "hbm_gbps_algorithmic_step": K * launch_bytes * world / (ms_per_step * 1e-3) / 1e9,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,

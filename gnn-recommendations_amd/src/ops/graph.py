@@ -412,8 +412,16 @@ class CsrGraph:
         order)."""
         key = ("tiled", int(rows_per_block), int(panel), int(sub_panel))
         if key not in self._plans:
+            import time
+            cuda = self.device.type == "cuda"
+
+            def now():
+                if cuda:
+                    torch.cuda.synchronize(self.device)
+                return time.perf_counter()
             if planner is None:
-                planner = TILED_PLANNER if self.device.type == "cuda" else "host"
+                planner = TILED_PLANNER if cuda else "host"
+            t0 = now()
             if planner == "device":
                 plan = self._tiled_plan_device(int(rows_per_block), int(panel), int(sub_panel))
             elif planner == "host":
@@ -425,9 +433,18 @@ class CsrGraph:
                         n_slots=plan["n_chunks"] * _lib.TILED_CHUNK,
                         sync=torch.zeros(_lib.TILED_SYNC_WORDS, dtype=torch.int32,
                                          device=self.device))
-            if (TILED_FACTOR and self.device.type == "cuda"
+            t1 = now()
+            build_s = {"planner": planner, "plan_s": t1 - t0}
+            if (TILED_FACTOR and cuda
                     and int(rows_per_block) <= _lib.TILED_MAX_ROWS_FACTORED):
-                self._factor_plan(plan)
+                self.degree_factors()
+                t2 = now()
+                factored = self._factor_plan(plan)
+                t3 = now()
+                build_s.update(degree_factors_s=t2 - t1, factor_check_s=t3 - t2,
+                               factored=bool(factored))
+            # phase times of this build (each phase synchronised): bench.py reports them
+            plan["build_s"] = build_s
             self._plans[key] = plan
         return self._plans[key]
 
