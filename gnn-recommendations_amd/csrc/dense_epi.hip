@@ -294,6 +294,27 @@ __global__ __launch_bounds__(64 * NW) void spmm_mfma_kernel(DenseParams p) {
 // (c1 + b1) + (c2 + b2)) with B read from LDS as one float4 per 4 steps; bias, LeakyReLU and
 // the GAS product (VALU for 8x8 blocks, else on the matrix cores) run from a private o tile,
 // and whole rows are stored (float4). The next tile's rows are in flight in registers.
+#ifndef GNNREC_TRANSFORM_GAS_DPP
+#define GNNREC_TRANSFORM_GAS_DPP 1
+#endif
+// Lanes 0-7 of each 16-lane DPP row take row lane T, lanes 8-15 row lane 8 + T (two DPP
+// row_newbcast moves under bank masks): one 8-column GAS block's value c to its 8 lanes.
+template <int T>
+__device__ __forceinline__ float half_bcast(float v) {
+  const int a = __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x150 + T, 0xF, 0x3, false);
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(a, __builtin_bit_cast(int, v), 0x158 + T, 0xF, 0xC, false));
+}
+// z = sum_c o[c] W[c][e] of one 8x8 GAS block in the MFMA output layout (lane i16 = 8 h + e
+// holds column 8 b + e of the block's row): fmaf over c ascending from +0, oracle_gas's order
+template <int... C>
+__device__ __forceinline__ float gas_dpp8(std::integer_sequence<int, C...>, float v,
+                                          const float (&w)[8]) {
+  float z = 0.f;
+  ((z = __builtin_fmaf(half_bcast<C>(v), w[C], z)), ...);
+  return z;
+}
+
 template <int MODE, int NW, bool GASV>
 __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
   constexpr int D = 64;
@@ -345,7 +366,24 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
     bias1[nt] = MODE == 0 ? p.b1[16 * nt + i16] : 0.f;
     bias2[nt] = MODE == 0 ? p.b2[16 * nt + i16] : 0.f;
   }
+  // GAS in registers (GNNREC_TRANSFORM_GAS_DPP): lane i16 = 8 h + e of output tile nt holds
+  // column 8 (2 nt + h) + e, so it needs W_{2nt+h}[c][e] for c < 8 (32 weights, constant)
+  // and the output column of its block column, inv[16 nt + i16]
+  constexpr bool gas_dpp = MODE == 0 && GASV && GNNREC_TRANSFORM_GAS_DPP;
+  float wg[gas_dpp ? 4 : 1][8];
+  int invc[4];
+  if (gas_dpp) {
+    const int h = i16 >> 3, e = i16 & 7;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) wg[nt][c] = p.gas_blocks[((2 * nt + h) * kVbs + c) * kVbs + e];
+  }
   __syncthreads();
+  if (gas_dpp) {
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) invc[nt] = inv_lds[16 * nt + i16];
+  }
 
   const int64_t n_tiles = ceil_div(p.A.n_rows, 16);
   const int64_t stride = (int64_t)gridDim.x * NW;
@@ -431,7 +469,8 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
       // keep each group's B reads next to its MFMAs (hoisting all 32 float4 costs 128 VGPRs)
       __builtin_amdgcn_sched_barrier(0);
     }
-    // o tile (rows 4 k4 + q, column 16 nt + i16)
+    // o tile (rows 4 k4 + q, column 16 nt + i16); with gas_dpp the GAS outputs go straight
+    // to their permuted columns
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt)
 #pragma unroll
@@ -443,9 +482,12 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
         } else {
           v = c1[nt][q];
         }
-        ot[(4 * k4 + q) * LDO + 16 * nt + i16] = v;
+        if (gas_dpp)
+          ot[(4 * k4 + q) * LDO + invc[nt]] = gas_dpp8(std::make_integer_sequence<int, 8>{}, v, wg[nt]);
+        else
+          ot[(4 * k4 + q) * LDO + 16 * nt + i16] = v;
       }
-    if (gas_valu) {
+    if (gas_valu && !gas_dpp) {
       // lane (i16, k4): z = GAS of row i16's columns 16 k4 .. 16 k4 + 15 (two 8-blocks), then
       // z[t] to column inv[16 k4 + t] of the same row; the wave's LDS operations run in order,
       // so every lane's reads of the row precede the scattered writes

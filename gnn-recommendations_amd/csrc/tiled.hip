@@ -116,7 +116,9 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 // accumulator reads and writes (registers instead), bit 1 replaces the gathers by a constant,
 // bit 2 skips the step barriers, bit 3 reads every chunk's slot words and values from the
 // plan's first 64 chunks (cache-resident plan stream; headers unchanged), bit 4 replaces the
-// DPP broadcasts by the lane's own value, bit 5 skips the main loop (passes and epilogues).
+// DPP broadcasts by the lane's own value, bit 5 skips the main loop (passes and epilogues),
+// bit 6 drops a factored plan's class load (every slot class 0: the cost of one plan-load
+// instruction per chunk).
 #ifndef GNNREC_TILED_EXP
 #define GNNREC_TILED_EXP 0
 #endif
@@ -184,7 +186,7 @@ __device__ __forceinline__ void tiled_slots(const uint32_t* __restrict__ ss,
   const int64_t i = c * kTiledChunk + lane;
   m.w = ss[i];   // default policy: nt plan loads measured 1 % slower (exp_plan_nt.jsonl)
   if constexpr (FACT)
-    m.c = sc[i];
+    m.c = (GNNREC_TILED_EXP & 64) ? 0u : sc[i];
   else
     m.v = sv[i];
   m.h = hdr[4 * c + (lane & 3)];
