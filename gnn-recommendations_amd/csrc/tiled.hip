@@ -142,8 +142,25 @@ __device__ unsigned long long* g_tiled_trace;
 struct TiledSlots {   // this lane's slot of the chunk: stream lane / 8, step lane % 8
   uint32_t w;         // slot word: (column - panel base) << kRowBits | local row
   float v;            // the slot's value (a factored plan: formed at the gather stage)
-  uint32_t h;         // word (lane % 4) of the chunk header
+  uint32_t h;         // word (lane % 4) of the chunk header (quad layout: lane % 16 of the quad's)
   uint32_t c;         // a factored plan: the slot's column class
+  int hl = 0;         // quad layout: the chunk's first header lane (4 k)
+};
+
+#ifndef GNNREC_TILED_QUAD
+#define GNNREC_TILED_QUAD 0
+#endif
+// Quad plan layout (experiment builds, DESIGN.md §3.1c "plan-load instructions"): the plan
+// streams are interleaved per 4 chunks — lane l's slot words of chunks 4q .. 4q+3 are one
+// 16-B load, their class bytes one dword (values one 16-B load), the 4 chunk headers one dword
+// per lane (lane % 16) — so a wave issues 3 plan loads per 4 chunks instead of 12. Every wave's
+// chunk range starts on a quad (the planner pads ranges to multiples of 4 with empty chunks).
+constexpr bool kQuad = GNNREC_TILED_QUAD != 0;
+struct TiledQuad {
+  uint4 w;
+  uint32_t c;   // factored: 4 class bytes (byte k: chunk 4q + k)
+  float4 v;     // explicit values
+  uint32_t h;   // header word lane % 16 of the quad (chunk k: lanes 4k .. 4k+3)
 };
 
 // Factored plans (ABI 8, DESIGN.md §3.1c "plan values"): every value of the operand is
@@ -202,7 +219,35 @@ __device__ __forceinline__ void slot_value(TiledSlots& m, const float* rfl, cons
 
 template <int W>
 __device__ __forceinline__ uint32_t hdr_word(const TiledSlots& m) {
-  return (uint32_t)__builtin_amdgcn_readlane((int)m.h, W);
+  return (uint32_t)__builtin_amdgcn_readlane((int)m.h, W + m.hl);
+}
+
+template <bool FACT>
+__device__ __forceinline__ void tiled_quad(const uint32_t* __restrict__ ss,
+                                           const float* __restrict__ sv,
+                                           const uint8_t* __restrict__ sc,
+                                           const uint32_t* __restrict__ hdr, int64_t q, int lane,
+                                           TiledQuad& Q) {
+  const int64_t i = q * kTiledChunk + lane;
+  Q.w = reinterpret_cast<const uint4*>(ss)[i];
+  if constexpr (FACT)
+    Q.c = reinterpret_cast<const uint32_t*>(sc)[i];
+  else
+    Q.v = reinterpret_cast<const float4*>(sv)[i];
+  Q.h = hdr[16 * q + (lane & 15)];
+}
+
+template <int K, bool FACT>
+__device__ __forceinline__ TiledSlots quad_chunk(const TiledQuad& Q) {
+  TiledSlots m;
+  m.w = K == 0 ? Q.w.x : K == 1 ? Q.w.y : K == 2 ? Q.w.z : Q.w.w;
+  if constexpr (FACT)
+    m.c = (Q.c >> (8 * K)) & 255u;
+  else
+    m.v = K == 0 ? Q.v.x : K == 1 ? Q.v.y : K == 2 ? Q.v.z : Q.v.w;
+  m.h = Q.h;
+  m.hl = 4 * K;
+  return m;
 }
 
 // The gathers of a chunk read through a buffer whose base is its panel's first source row, so
@@ -433,6 +478,11 @@ __device__ __forceinline__ void tiled_epilogue(const float* acc, int R, int rl, 
   }
 }
 
+template <class F, int... J>
+__device__ __forceinline__ void for_seq(std::integer_sequence<int, J...>, F&& f) {
+  (f(std::integral_constant<int, J>{}), ...);
+}
+
 // the main loop unrolled over one turn of the pipeline rings (compile-time ring indices)
 template <class F, int... I>
 __device__ __forceinline__ void run_ring(std::integer_sequence<int, I...>, F&& stage) {
@@ -499,7 +549,51 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     const int64_t b = wptr[s], e = (GNNREC_TILED_EXP & 32) ? b : wptr[s + 1];
     int cur = 0;
     f4 sink = {0.f, 0.f, 0.f, 0.f};   // diagnostic builds only (GNNREC_TILED_EXP & 1)
-    if (b < e) {
+    if (kQuad && b < e) {
+      // quad layout: a ring of 3 quads (12 chunks) and kGatherAhead + 1 gathered chunks; stage
+      // c (c % 4 == 0) loads quad c / 4 + 2, every stage gathers chunk c + kGatherAhead and
+      // applies chunk c (wave ranges start on a quad, so c % 4 is the unrolled stage's)
+      TiledQuad QR[3];
+      f4 X[kXRing][kSteps][kSPW];
+      float V[kXRing];
+      const int nc = (int)(e - b);
+      const int64_t q0 = b / 4;
+      int c = 0;
+      tiled_quad<FACT>(ss, sv, sc, hdr, q0, lane, QR[0]);
+      tiled_quad<FACT>(ss, sv, sc, hdr, q0 + 1, lane, QR[1]);
+      auto gather_j = [&](auto jc) {
+        constexpr int J = decltype(jc)::value;
+        TiledSlots mg = quad_chunk<J % 4, FACT>(QR[(J / 4) % 3]);
+        tiled_gather(kSeq, chunk_rsrc(xs, xs_bytes, hdr_word<3>(mg), row_bytes), q16,
+                     row_bytes, mg, X[J % kXRing]);
+        slot_value<FACT>(mg, rfl, ctl, (uint32_t)R);
+        V[J % kXRing] = mg.v;
+      };
+      for_seq(std::make_integer_sequence<int, kGatherAhead>{}, gather_j);
+      auto stage = [&](auto ic) -> bool {
+        constexpr int I = decltype(ic)::value;
+        if constexpr (I % 4 == 0)
+          tiled_quad<FACT>(ss, sv, sc, hdr, q0 + c / 4 + 2, lane, QR[(I / 4 + 2) % 3]);
+        gather_j(std::integral_constant<int, I + kGatherAhead>{});
+        TiledSlots ma = quad_chunk<I % 4, FACT>(QR[(I / 4) % 3]);
+        ma.v = V[I % kXRing];
+        const int bar = (int)hdr_word<0>(ma);
+        for (int i = 0; i < bar; ++i) {
+          if (!(GNNREC_TILED_EXP & 4)) __syncthreads();
+          GNNREC_TILED_STAMP(ev);
+        }
+        cur += bar;
+        const uint64_t cm =
+            kNoChain ? 0 : (uint64_t)hdr_word<1>(ma) | ((uint64_t)hdr_word<2>(ma) << 32);
+        if (!kNoChain && cm)
+          tiled_apply<true>(acc, q16, ma, X[I % kXRing], cm, sink);
+        else
+          tiled_apply<false>(acc, q16, ma, X[I % kXRing], 0, sink);
+        return ++c >= nc;
+      };
+      static_assert(12 % kXRing == 0, "quad ring: 12 stages cover the gather ring");
+      run_ring(std::make_integer_sequence<int, 12>{}, stage);
+    } else if (b < e) {
       // a ring of kPlanAhead + 1 slot sets and kGatherAhead + 1 gathered chunks: stage c loads
       // chunk c + kPlanAhead's slots, gathers chunk c + kGatherAhead and applies chunk c
       TiledSlots M[kMRing];
@@ -866,6 +960,8 @@ int tiled_lds_attribute(int dev) {
   return done[dev];
 }
 }  // namespace
+
+extern "C" int gnnrec_tiled_plan_quad(void) { return kQuad ? 1 : 0; }
 
 extern "C" int gnnrec_spmm_tiled_supported(int32_t device, int32_t rows_per_block) {
   if (rows_per_block < 1 || rows_per_block > GNNREC_TILED_MAX_ROWS) return 0;

@@ -64,6 +64,7 @@ _SIGNATURES = {
     "gnnrec_tiled_plan_device": [_p, _p, _p, _i64, _i32, _i32, _i32, _i64, _p, _i32, _p, _p, _p,
                                  _p, _p, _p, _p, _p],
     "gnnrec_spmm_tiled_supported": [_i32, _i32],
+    "gnnrec_tiled_plan_quad": [],
     "gnnrec_tiled_plan_factor": [_p, _p, _p, _p, _i64, _i32, _i64, _i64, _p, _p, _p, _i32, _p,
                                  _p, _p],
     "gnnrec_spmm_tiled_f32": [_p, _p, _p, _p, _p, _i32, _p, _p, _p, _i64, _i32, _p, _i64, _i64,

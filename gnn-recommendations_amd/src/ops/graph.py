@@ -443,6 +443,10 @@ class CsrGraph:
                 t3 = now()
                 build_s.update(degree_factors_s=t2 - t1, factor_check_s=t3 - t2,
                                factored=bool(factored))
+            if cuda and _lib.lib().gnnrec_tiled_plan_quad():
+                t4 = now()
+                self._quad_plan(plan)
+                build_s["quad_layout_s"] = now() - t4
             # phase times of this build (each phase synchronised): bench.py reports them
             plan["build_s"] = build_s
             self._plans[key] = plan
@@ -499,6 +503,43 @@ class CsrGraph:
         del plan["val"]
         plan.update(cls=cls, row_factor=rowf, class_table=table, n_classes=int(table.numel()))
         return True
+
+    @staticmethod
+    def _quad_plan(plan: dict) -> None:
+        """The quad-interleaved layout a GNNREC_TILED_QUAD build of the kernel reads
+        (gnnrec_tiled_plan_quad): every wave's chunk range padded to a multiple of 4 with
+        empty chunks (column offset 0, the scratch row, header 0), then per 4 chunks the slot
+        words / class bytes / values as [lane][4], and 16 tail chunks. Headers stay
+        chunk-major (a quad's 16 words are contiguous)."""
+        W, CH = _lib.TILED_WAVES, _lib.TILED_CHUNK
+        wp = plan["wave_ptr"]
+        dev = wp.device
+        n = int(plan["n_chunks"])
+        counts = wp[1:] - wp[:-1]
+        new_counts = (counts + 3) // 4 * 4
+        new_wp = torch.zeros_like(wp)
+        torch.cumsum(new_counts, 0, out=new_wp[1:])
+        total = int(new_wp[-1])
+        waves = torch.repeat_interleave(torch.arange(counts.numel(), device=dev), counts)
+        idx = new_wp[waves] + torch.arange(n, device=dev) - wp[waves]   # old chunk -> new
+        alloc = total + 16
+        R = int(plan["rows_per_block"])
+
+        def moved(a, fill, width):
+            out = torch.full((alloc, width), fill, dtype=a.dtype, device=dev)
+            out[idx] = a.view(-1, width)[:n]
+            return out
+        slot = moved(plan["slot"], R, CH)
+        plan["slot"] = slot.view(-1, 4, CH).transpose(1, 2).contiguous().view(-1)
+        if "cls" in plan:
+            cls = moved(plan["cls"], 0, CH)
+            plan["cls"] = cls.view(-1, 4, CH).transpose(1, 2).contiguous().view(-1)
+        if plan.get("val") is not None:
+            val = moved(plan["val"], 0.0, CH)
+            plan["val"] = val.view(-1, 4, CH).transpose(1, 2).contiguous().view(-1)
+        plan["hdr"] = moved(plan["hdr"], 0, _lib.TILED_HDR_WORDS).view(-1)
+        plan["wave_ptr"] = new_wp
+        plan.update(n_chunks=total, n_slots=total * CH, layout="quad")
 
     def _tiled_plan_host(self, R: int, panel: int, sub_panel: int) -> dict:
         import ctypes as C

@@ -209,6 +209,13 @@ int gnnrec_tiled_plan_device(const int64_t* row_ptr, const int32_t* col, const f
  * then keeps the row-parallel hop (gnnrec_spmm_csr_masked_f32). */
 int gnnrec_spmm_tiled_supported(int32_t device, int32_t rows_per_block);
 
+/* The plan layout gnnrec_spmm_tiled_f32 of this build reads: 0 = chunk-major (the arrays
+ * gnnrec_tiled_plan_emit / gnnrec_tiled_plan_device write); 1 = quad-interleaved (experiment
+ * builds, GNNREC_TILED_QUAD): every wave's chunk range padded to a multiple of 4 chunks with
+ * empty chunks (all slots: column offset 0, row = rows_per_block; header 0), then per 4 chunks
+ * [lane][4] slot words, class bytes / values, and >= 12 tail chunks. */
+int gnnrec_tiled_plan_quad(void);
+
 /* Factored plans (ABI 8): when every value of the operand is fl(row_factor[r] *
  * class_table[k]) for a class k of its column (the symmetric normalisation fl(dis_r * dis_c)
  * of graph_builder.py:119-126 when the column degrees take at most GNNREC_TILED_MAX_CLASSES
