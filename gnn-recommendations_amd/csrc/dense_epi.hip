@@ -294,8 +294,14 @@ __global__ __launch_bounds__(64 * NW) void spmm_mfma_kernel(DenseParams p) {
 // (c1 + b1) + (c2 + b2)) with B read from LDS as one float4 per 4 steps; bias, LeakyReLU and
 // the GAS product (VALU for 8x8 blocks, else on the matrix cores) run from a private o tile,
 // and whole rows are stored (float4). The next tile's rows are in flight in registers.
+// Diagnostic builds only (results wrong, timing only): bit 0 skips the MFMAs (accumulators stay
+// 0), bit 1 skips the GAS product (the o tile is stored as is), bit 2 replaces the row loads by
+// register constants (no HBM reads).
+#ifndef GNNREC_TRANSFORM_EXP
+#define GNNREC_TRANSFORM_EXP 0
+#endif
 #ifndef GNNREC_TRANSFORM_GAS_DPP
-#define GNNREC_TRANSFORM_GAS_DPP 1
+#define GNNREC_TRANSFORM_GAS_DPP 0
 #endif
 // Lanes 0-7 of each 16-lane DPP row take row lane T, lanes 8-15 row lane 8 + T (two DPP
 // row_newbcast moves under bank masks): one 8-column GAS block's value c to its 8 lanes.
@@ -395,7 +401,10 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       pn[t] = px[t] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ok) {
+      if (GNNREC_TRANSFORM_EXP & 4) {
+        pn[t] = make_float4((float)r, 1.f, 2.f, (float)t);
+        px[t] = pn[t];
+      } else if (ok) {
         pn[t] = *reinterpret_cast<const float4*>(p.x + r * p.ldx + 16 * t + 4 * k4);
         if (MODE == 0) px[t] = *reinterpret_cast<const float4*>(p.x_self + r * p.ld_self + 16 * t + 4 * k4);
       }
@@ -428,45 +437,42 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
     floatx4 c1[4], c2[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) c1[nt] = c2[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
-    // B of step group t (4 MFMA steps) for every (part, nt): 8 float4, double-buffered so the
-    // next group's LDS reads fly under this group's 32 MFMAs; the MFMAs cycle over the 8
-    // independent accumulators (no dependent back-to-back issue), each chain in (t, q) order
+    // B in half-groups h = (t, part): the 4 float4 (one per nt) of 4 MFMA steps of one
+    // contraction part, double-buffered so half-group h + 1's LDS reads fly under h's 16
+    // MFMAs; inside h the MFMAs cycle over the 4 output tiles (independent accumulators, no
+    // dependent back-to-back issue); every chain keeps its (t, q) order
     const float4* bl = reinterpret_cast<const float4*>(b_lds) + lane;
-    float4 bc[NP][4], bn[NP][4];
-    auto load_b = [&](int t, float4 (&b)[NP][4]) {
+    constexpr int NH = 4 * NP;   // half-groups: h = t * NP + part
+    float4 bc[4], bn[4];
+    auto load_b = [&](int h, float4 (&bb)[4]) {
+      const int t = h / NP, part = h % NP;
 #pragma unroll
-      for (int part = 0; part < NP; ++part)
-#pragma unroll
-        for (int nt = 0; nt < 4; ++nt) b[part][nt] = bl[((part * 4 + t) * 4 + nt) * 64];
+      for (int nt = 0; nt < 4; ++nt) bb[nt] = bl[((part * 4 + t) * 4 + nt) * 64];
     };
     load_b(0, bc);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (t < 3) load_b(t + 1, bn);
-      __builtin_amdgcn_sched_barrier(0);   // the next group's reads issue before these MFMAs
+    for (int h = 0; h < NH; ++h) {
+      const int t = h / NP, part = h % NP;
+      if (h + 1 < NH) load_b(h + 1, bn);
+      __builtin_amdgcn_sched_barrier(0);   // the next half-group's reads issue first
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        const float a = part == 0 ? an[t][q] : ax[t][q];
 #pragma unroll
         for (int nt = 0; nt < 4; ++nt) {
-          const float b = q == 0 ? bc[0][nt].x : q == 1 ? bc[0][nt].y : q == 2 ? bc[0][nt].z : bc[0][nt].w;
-          c1[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(an[t][q], b, c1[nt], 0, 0, 0);
-        }
-        if (MODE == 0) {
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) {
-            const float b = q == 0 ? bc[NP - 1][nt].x : q == 1 ? bc[NP - 1][nt].y
-                          : q == 2 ? bc[NP - 1][nt].z : bc[NP - 1][nt].w;
-            c2[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(ax[t][q], b, c2[nt], 0, 0, 0);
-          }
+          const float bq = q == 0 ? bc[nt].x : q == 1 ? bc[nt].y : q == 2 ? bc[nt].z : bc[nt].w;
+          if (GNNREC_TRANSFORM_EXP & 1)
+            c1[nt][q] += a * bq;   // keeps the operands live without the matrix cores
+          else if (part == 0)
+            c1[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bq, c1[nt], 0, 0, 0);
+          else
+            c2[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bq, c2[nt], 0, 0, 0);
         }
       }
-      if (t < 3) {
+      if (h + 1 < NH) {
 #pragma unroll
-        for (int part = 0; part < NP; ++part)
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) bc[part][nt] = bn[part][nt];
+        for (int nt = 0; nt < 4; ++nt) bc[nt] = bn[nt];
       }
-      // keep each group's B reads next to its MFMAs (hoisting all 32 float4 costs 128 VGPRs)
       __builtin_amdgcn_sched_barrier(0);
     }
     // o tile (rows 4 k4 + q, column 16 nt + i16); with gas_dpp the GAS outputs go straight
@@ -487,7 +493,7 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
         else
           ot[(4 * k4 + q) * LDO + 16 * nt + i16] = v;
       }
-    if (gas_valu && !gas_dpp) {
+    if (gas_valu && !gas_dpp && !(GNNREC_TRANSFORM_EXP & 2)) {
       // lane (i16, k4): z = GAS of row i16's columns 16 k4 .. 16 k4 + 15 (two 8-blocks), then
       // z[t] to column inv[16 k4 + t] of the same row; the wave's LDS operations run in order,
       // so every lane's reads of the row precede the scattered writes
@@ -703,7 +709,7 @@ namespace {
 //  * fused (no workspace): gather + MFMA in one kernel.
 // Waves per workgroup: 8 for d <= 64 (weights in LDS), 4 for d = 128 (weights in VGPRs).
 #ifndef GNNREC_TRANSFORM_GASV_WAVES
-#define GNNREC_TRANSFORM_GASV_WAVES 8
+#define GNNREC_TRANSFORM_GASV_WAVES 12
 #endif
 template <int MODE, bool GATHER>
 int launch_dense(const DenseParams& p, int d, hipStream_t s) {

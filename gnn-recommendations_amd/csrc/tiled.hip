@@ -148,13 +148,15 @@ struct TiledSlots {   // this lane's slot of the chunk: stream lane / 8, step la
 };
 
 #ifndef GNNREC_TILED_QUAD
-#define GNNREC_TILED_QUAD 0
+#define GNNREC_TILED_QUAD 1
 #endif
-// Quad plan layout (experiment builds, DESIGN.md §3.1c "plan-load instructions"): the plan
-// streams are interleaved per 4 chunks — lane l's slot words of chunks 4q .. 4q+3 are one
-// 16-B load, their class bytes one dword (values one 16-B load), the 4 chunk headers one dword
-// per lane (lane % 16) — so a wave issues 3 plan loads per 4 chunks instead of 12. Every wave's
-// chunk range starts on a quad (the planner pads ranges to multiples of 4 with empty chunks).
+// Quad plan layout (ABI 9, DESIGN.md §3.1c "plan-load instructions"): the plan streams are
+// interleaved per 4 chunks — lane l's slot words of chunks 4q .. 4q+3 are one 16-B load, their
+// class bytes one dword (values one 16-B load), the 4 chunk headers one dword per lane
+// (lane % 16) — so a wave issues 3 plan loads per 4 chunks instead of 12 (G100M hop 3.54 ->
+// 3.41 ms, profiles/r04/ab_quad_plan.jsonl). Every wave's chunk range starts on a quad: the
+// layout step (gnnrec_tiled_plan_quad_layout) pads ranges to multiples of 4 with empty chunks.
+// GNNREC_TILED_QUAD=0 builds read the planners' chunk-major arrays directly.
 constexpr bool kQuad = GNNREC_TILED_QUAD != 0;
 struct TiledQuad {
   uint4 w;
@@ -962,6 +964,106 @@ int tiled_lds_attribute(int dev) {
 }  // namespace
 
 extern "C" int gnnrec_tiled_plan_quad(void) { return kQuad ? 1 : 0; }
+
+namespace gnnrec {
+namespace {
+// wave_ptr_out = exclusive scan of each wave's chunk count rounded up to a multiple of 4: one
+// workgroup, each thread a contiguous run of waves
+__global__ __launch_bounds__(1024) void quad_offsets_kernel(const int64_t* __restrict__ wp,
+                                                            int64_t n_waves,
+                                                            int64_t* __restrict__ out) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (n_waves + 1023) / 1024;
+  const int64_t s0 = min(n_waves, t * per), s1 = min(n_waves, s0 + per);
+  int64_t sum = 0;
+  for (int64_t s = s0; s < s1; ++s) sum += (wp[s + 1] - wp[s] + 3) / 4 * 4;
+  part[t] = sum;
+  __syncthreads();
+  if (t == 0) {
+    int64_t run = 0;
+    for (int i = 0; i < 1024; ++i) {
+      const int64_t v = part[i];
+      part[i] = run;
+      run += v;
+    }
+    out[0] = 0;
+  }
+  __syncthreads();
+  int64_t run = part[t];
+  for (int64_t s = s0; s < s1; ++s) {
+    run += (wp[s + 1] - wp[s] + 3) / 4 * 4;
+    out[s + 1] = run;
+  }
+}
+
+// one 64-lane workgroup per output chunk j: the chunk-major plan's chunk at the same position
+// of its wave's range, or an empty chunk (padding to the quad, or one of the 16 tail chunks)
+template <bool FACT>
+__global__ __launch_bounds__(64) void quad_layout_kernel(
+    const int64_t* __restrict__ wp, const int64_t* __restrict__ wq, int64_t n_waves,
+    int64_t total, uint32_t pad_word, const uint32_t* __restrict__ slot,
+    const float* __restrict__ val, const uint8_t* __restrict__ cls,
+    const uint32_t* __restrict__ hdr, uint32_t* __restrict__ slot_out,
+    float* __restrict__ val_out, uint8_t* __restrict__ cls_out, uint32_t* __restrict__ hdr_out) {
+  const int64_t j = blockIdx.x;
+  const int l = threadIdx.x;
+  int64_t src = -1;
+  if (j < total) {
+    int64_t lo = 0, hi = n_waves;   // the wave s with wq[s] <= j < wq[s + 1]
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) / 2;
+      if (wq[mid] <= j) lo = mid; else hi = mid;
+    }
+    const int64_t off = j - wq[lo];
+    if (off < wp[lo + 1] - wp[lo]) src = wp[lo] + off;
+  }
+  const int64_t o = (j / 4) * (4 * kTiledChunk) + 4 * l + (j % 4);
+  slot_out[o] = src >= 0 ? slot[src * kTiledChunk + l] : pad_word;
+  if constexpr (FACT)
+    cls_out[o] = src >= 0 ? cls[src * kTiledChunk + l] : (uint8_t)0;
+  else
+    val_out[o] = src >= 0 ? val[src * kTiledChunk + l] : 0.f;
+  if (l < 4) hdr_out[4 * j + l] = src >= 0 ? hdr[4 * src + l] : 0u;
+}
+}  // namespace
+}  // namespace gnnrec
+
+extern "C" int gnnrec_tiled_plan_quad_offsets(const int64_t* wave_ptr, int64_t n_waves,
+                                              int64_t* wave_ptr_out, gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(wave_ptr && wave_ptr_out && n_waves >= 0, "tiled_quad_offsets: bad args");
+  hipLaunchKernelGGL(quad_offsets_kernel, dim3(1), dim3(1024), 0, as_hip(stream), wave_ptr,
+                     n_waves, wave_ptr_out);
+  return check_launch("tiled_quad_offsets");
+}
+
+extern "C" int gnnrec_tiled_plan_quad_layout(const int64_t* wave_ptr, const int64_t* wave_ptr_out,
+                                             int64_t n_waves, int64_t total_chunks,
+                                             int32_t rows_per_block, const uint32_t* slot,
+                                             const float* val, const uint8_t* slot_class,
+                                             const uint32_t* hdr, uint32_t* slot_out,
+                                             float* val_out, uint8_t* class_out,
+                                             uint32_t* hdr_out, gnnrec_stream_t stream) {
+  const bool fact = slot_class != nullptr;
+  GNNREC_REQUIRE(wave_ptr && wave_ptr_out && slot && hdr && slot_out && hdr_out &&
+                     (fact ? class_out != nullptr : (val && val_out)) && n_waves >= 0 &&
+                     total_chunks >= 0 && total_chunks % 4 == 0 && rows_per_block >= 1 &&
+                     rows_per_block <= GNNREC_TILED_MAX_ROWS,
+                 "tiled_quad_layout: bad args (total_chunks = wave_ptr_out[n_waves], a multiple "
+                 "of 4)");
+  const int64_t chunks = total_chunks + GNNREC_TILED_QUAD_TAIL;
+  GNNREC_REQUIRE(chunks < INT32_MAX, "tiled_quad_layout: too many chunks");
+  hipStream_t s = as_hip(stream);
+  if (fact)
+    hipLaunchKernelGGL(quad_layout_kernel<true>, dim3((unsigned)chunks), dim3(64), 0, s, wave_ptr,
+                       wave_ptr_out, n_waves, total_chunks, (uint32_t)rows_per_block, slot, val,
+                       slot_class, hdr, slot_out, val_out, class_out, hdr_out);
+  else
+    hipLaunchKernelGGL(quad_layout_kernel<false>, dim3((unsigned)chunks), dim3(64), 0, s,
+                       wave_ptr, wave_ptr_out, n_waves, total_chunks, (uint32_t)rows_per_block,
+                       slot, val, slot_class, hdr, slot_out, val_out, class_out, hdr_out);
+  return check_launch("tiled_quad_layout");
+}
 
 extern "C" int gnnrec_spmm_tiled_supported(int32_t device, int32_t rows_per_block) {
   if (rows_per_block < 1 || rows_per_block > GNNREC_TILED_MAX_ROWS) return 0;

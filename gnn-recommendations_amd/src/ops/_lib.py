@@ -17,7 +17,7 @@ import torch  # noqa: F401  (load order: torch's HIP runtime first)
 
 _PKG_ROOT = Path(__file__).resolve().parents[2]
 LIB_PATH = Path(os.environ.get("GNNREC_LIB", _PKG_ROOT / "lib" / "libgnnrec.so"))
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # gnnrec.h epilogue flags
 EPI_ACC_INIT = 1
@@ -31,6 +31,7 @@ TILED_GROUPS = 8
 TILED_STEPS = 8
 TILED_CHUNK = 64
 TILED_TAIL = 8
+TILED_QUAD_TAIL = 16
 TILED_MAX_ROWS = 1279
 TILED_SYNC_WORDS = 256
 TILED_HDR_WORDS = 4
@@ -65,6 +66,9 @@ _SIGNATURES = {
                                  _p, _p, _p, _p, _p],
     "gnnrec_spmm_tiled_supported": [_i32, _i32],
     "gnnrec_tiled_plan_quad": [],
+    "gnnrec_tiled_plan_quad_offsets": [_p, _i64, _p, _p],
+    "gnnrec_tiled_plan_quad_layout": [_p, _p, _i64, _i64, _i32, _p, _p, _p, _p, _p, _p, _p, _p,
+                                      _p],
     "gnnrec_tiled_plan_factor": [_p, _p, _p, _p, _i64, _i32, _i64, _i64, _p, _p, _p, _i32, _p,
                                  _p, _p],
     "gnnrec_spmm_tiled_f32": [_p, _p, _p, _p, _p, _i32, _p, _p, _p, _i64, _i32, _p, _i64, _i64,

@@ -506,40 +506,38 @@ class CsrGraph:
 
     @staticmethod
     def _quad_plan(plan: dict) -> None:
-        """The quad-interleaved layout a GNNREC_TILED_QUAD build of the kernel reads
-        (gnnrec_tiled_plan_quad): every wave's chunk range padded to a multiple of 4 with
-        empty chunks (column offset 0, the scratch row, header 0), then per 4 chunks the slot
-        words / class bytes / values as [lane][4], and 16 tail chunks. Headers stay
-        chunk-major (a quad's 16 words are contiguous)."""
-        W, CH = _lib.TILED_WAVES, _lib.TILED_CHUNK
+        """The quad-interleaved layout the kernel reads (ABI 9, gnnrec_tiled_plan_quad):
+        gnnrec_tiled_plan_quad_offsets pads every wave's chunk range to a multiple of 4,
+        gnnrec_tiled_plan_quad_layout moves the chunks there (empty chunks after them and in
+        TILED_QUAD_TAIL tail chunks) and interleaves the slot words and class bytes / values
+        of 4 chunks per lane. Headers stay chunk-major."""
+        L = _lib.lib()
+        ptr = _lib.ptr
+        CH = _lib.TILED_CHUNK
         wp = plan["wave_ptr"]
         dev = wp.device
-        n = int(plan["n_chunks"])
-        counts = wp[1:] - wp[:-1]
-        new_counts = (counts + 3) // 4 * 4
-        new_wp = torch.zeros_like(wp)
-        torch.cumsum(new_counts, 0, out=new_wp[1:])
-        total = int(new_wp[-1])
-        waves = torch.repeat_interleave(torch.arange(counts.numel(), device=dev), counts)
-        idx = new_wp[waves] + torch.arange(n, device=dev) - wp[waves]   # old chunk -> new
-        alloc = total + 16
-        R = int(plan["rows_per_block"])
-
-        def moved(a, fill, width):
-            out = torch.full((alloc, width), fill, dtype=a.dtype, device=dev)
-            out[idx] = a.view(-1, width)[:n]
-            return out
-        slot = moved(plan["slot"], R, CH)
-        plan["slot"] = slot.view(-1, 4, CH).transpose(1, 2).contiguous().view(-1)
-        if "cls" in plan:
-            cls = moved(plan["cls"], 0, CH)
-            plan["cls"] = cls.view(-1, 4, CH).transpose(1, 2).contiguous().view(-1)
-        if plan.get("val") is not None:
-            val = moved(plan["val"], 0.0, CH)
-            plan["val"] = val.view(-1, 4, CH).transpose(1, 2).contiguous().view(-1)
-        plan["hdr"] = moved(plan["hdr"], 0, _lib.TILED_HDR_WORDS).view(-1)
-        plan["wave_ptr"] = new_wp
-        plan.update(n_chunks=total, n_slots=total * CH, layout="quad")
+        stream = _lib.stream_of(dev)
+        n_waves = wp.numel() - 1
+        wq = torch.empty_like(wp)
+        _lib.check(L.gnnrec_tiled_plan_quad_offsets(ptr(wp), n_waves, ptr(wq), stream),
+                   "gnnrec_tiled_plan_quad_offsets")
+        total = int(wq[-1])
+        alloc = total + _lib.TILED_QUAD_TAIL
+        fact = "cls" in plan
+        slot = torch.empty(alloc * CH, dtype=torch.int32, device=dev)
+        hdr = torch.empty(alloc * _lib.TILED_HDR_WORDS, dtype=torch.int32, device=dev)
+        cls = torch.empty(alloc * CH, dtype=torch.uint8, device=dev) if fact else None
+        val = None if fact else torch.empty(alloc * CH, dtype=torch.float32, device=dev)
+        _lib.check(L.gnnrec_tiled_plan_quad_layout(
+            ptr(wp), ptr(wq), n_waves, total, int(plan["rows_per_block"]), ptr(plan["slot"]),
+            ptr(plan.get("val")), ptr(plan["cls"]) if fact else 0, ptr(plan["hdr"]),
+            ptr(slot), ptr(val), ptr(cls), ptr(hdr), stream), "gnnrec_tiled_plan_quad_layout")
+        plan.update(slot=slot, hdr=hdr, wave_ptr=wq, n_chunks=total, n_slots=total * CH,
+                    layout="quad")
+        if fact:
+            plan["cls"] = cls
+        else:
+            plan["val"] = val
 
     def _tiled_plan_host(self, R: int, panel: int, sub_panel: int) -> dict:
         import ctypes as C

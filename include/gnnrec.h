@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GNNREC_ABI_VERSION 8
+#define GNNREC_ABI_VERSION 9
 
 typedef struct ihipStream_t* gnnrec_stream_t;
 
@@ -170,6 +170,7 @@ int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col, const
 #define GNNREC_TILED_STEPS 8
 #define GNNREC_TILED_CHUNK 64
 #define GNNREC_TILED_TAIL 8
+#define GNNREC_TILED_QUAD_TAIL 16   /* tail chunks of the quad layout (prefetch 11 chunks ahead) */
 #define GNNREC_TILED_MAX_ROWS 1279
 #define GNNREC_TILED_SYNC_WORDS 256
 #define GNNREC_TILED_HDR_WORDS 4
@@ -209,12 +210,31 @@ int gnnrec_tiled_plan_device(const int64_t* row_ptr, const int32_t* col, const f
  * then keeps the row-parallel hop (gnnrec_spmm_csr_masked_f32). */
 int gnnrec_spmm_tiled_supported(int32_t device, int32_t rows_per_block);
 
-/* The plan layout gnnrec_spmm_tiled_f32 of this build reads: 0 = chunk-major (the arrays
- * gnnrec_tiled_plan_emit / gnnrec_tiled_plan_device write); 1 = quad-interleaved (experiment
- * builds, GNNREC_TILED_QUAD): every wave's chunk range padded to a multiple of 4 chunks with
- * empty chunks (all slots: column offset 0, row = rows_per_block; header 0), then per 4 chunks
- * [lane][4] slot words, class bytes / values, and >= 12 tail chunks. */
+/* The plan layout gnnrec_spmm_tiled_f32 of this build reads (ABI 9): 1 = quad-interleaved
+ * (the default): the planners' chunk-major arrays (gnnrec_tiled_plan_emit /
+ * gnnrec_tiled_plan_device, factored by gnnrec_tiled_plan_factor) go through
+ * gnnrec_tiled_plan_quad_offsets + gnnrec_tiled_plan_quad_layout first; 0 = chunk-major
+ * (GNNREC_TILED_QUAD=0 builds read the planner arrays directly). */
 int gnnrec_tiled_plan_quad(void);
+
+/* Quad layout, step 1 (device, async): wave_ptr_out[n_waves + 1] = the exclusive scan of each
+ * wave's chunk count (wave_ptr[s+1] - wave_ptr[s]) rounded up to a multiple of 4. The caller
+ * reads total_chunks = wave_ptr_out[n_waves] and allocates the step-2 outputs for
+ * total_chunks + GNNREC_TILED_QUAD_TAIL chunks. */
+int gnnrec_tiled_plan_quad_offsets(const int64_t* wave_ptr, int64_t n_waves, int64_t* wave_ptr_out,
+                                   gnnrec_stream_t stream);
+
+/* Quad layout, step 2 (device, async): every wave's chunks at the start of its padded range,
+ * empty chunks after them and in the GNNREC_TILED_QUAD_TAIL tail chunks (slot word =
+ * rows_per_block: column offset 0, the scratch row; class 0 / value 0; header 0); then the
+ * slot words and the class bytes (slot_class != NULL, a factored plan) or the values of
+ * chunks 4q .. 4q+3 as [q][lane][4]; headers stay [chunk][4]. */
+int gnnrec_tiled_plan_quad_layout(const int64_t* wave_ptr, const int64_t* wave_ptr_out,
+                                  int64_t n_waves, int64_t total_chunks, int32_t rows_per_block,
+                                  const uint32_t* slot, const float* val,
+                                  const uint8_t* slot_class, const uint32_t* hdr,
+                                  uint32_t* slot_out, float* val_out, uint8_t* class_out,
+                                  uint32_t* hdr_out, gnnrec_stream_t stream);
 
 /* Factored plans (ABI 8): when every value of the operand is fl(row_factor[r] *
  * class_table[k]) for a class k of its column (the symmetric normalisation fl(dis_r * dis_c)

@@ -277,39 +277,3 @@ def test_tiled_plan_build_with_offsets_past_2_31():
     for a, b in zip(*plans):
         assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
 
-
-def test_quad_plan_layout_is_padding_plus_permutation():
-    """CsrGraph._quad_plan (the layout of a GNNREC_TILED_QUAD kernel build): every wave's
-    chunk range is padded to a multiple of 4 with empty chunks (scratch row, header 0), the
-    slots of 4 chunks are interleaved per lane, the headers stay chunk-major, and the real
-    chunks are exactly the chunk-major plan's, in order."""
-    import torch
-    from src.ops import CsrGraph, _lib
-    rng = np.random.default_rng(4)
-    g = CsrGraph.from_interactions(rng.integers(0, 3000, 60000), rng.integers(0, 2000, 60000),
-                                   3000, 2000)
-    R = 333
-    plan = g._tiled_plan_host(R, 4096, 512)
-    plan.update(rows_per_block=R)
-    std = {k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in plan.items()}
-    CsrGraph._quad_plan(plan)
-    W, CH = _lib.TILED_WAVES, _lib.TILED_CHUNK
-    wp_old, wp = std["wave_ptr"].numpy(), plan["wave_ptr"].numpy()
-    assert np.all(np.diff(wp) % 4 == 0) and np.all(wp % 4 == 0)
-    total = int(wp[-1])
-    assert plan["n_chunks"] == total and plan["slot"].numel() == (total + 16) * CH
-    slot = plan["slot"].view(-1, CH, 4).transpose(1, 2).reshape(-1, CH).numpy()
-    val = plan["val"].view(-1, CH, 4).transpose(1, 2).reshape(-1, CH).numpy()
-    hdr = plan["hdr"].view(-1, 4).numpy()
-    s_old = std["slot"].view(-1, CH).numpy()
-    v_old = std["val"].view(-1, CH).numpy()
-    h_old = std["hdr"].view(-1, 4).numpy()
-    for w in range(wp_old.size - 1):
-        a, b = wp_old[w], wp_old[w + 1]
-        na = wp[w]
-        np.testing.assert_array_equal(slot[na:na + b - a], s_old[a:b])
-        np.testing.assert_array_equal(val[na:na + b - a], v_old[a:b])
-        np.testing.assert_array_equal(hdr[na:na + b - a], h_old[a:b])
-        pad = slice(na + b - a, wp[w + 1])
-        assert np.all(slot[pad] == R) and np.all(hdr[pad] == 0) and np.all(val[pad] == 0)
-    assert np.all(slot[total:] == R) and np.all(hdr[total:] == 0)

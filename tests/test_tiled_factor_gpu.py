@@ -89,11 +89,9 @@ def test_factor_kernel_counts_mismatches(cuda):
     """gnnrec_tiled_plan_factor through the C ABI: zero mismatches for the operand's own
     factors, one per perturbed slot value."""
     g, _ = _binary(5000, 4000, 100000, 9, cuda)
-    G.TILED_FACTOR, was = False, G.TILED_FACTOR
-    try:
-        plan = g.tiled_plan(rows_per_block=200, panel=2048, sub_panel=256)
-    finally:
-        G.TILED_FACTOR = was
+    # the planner's chunk-major arrays (what the factor kernel reads; a quad-layout build
+    # interleaves the plan only after factoring)
+    plan = g._tiled_plan_device(200, 2048, 256)
     rowf, col_class, table = g.degree_factors()
     L = _lib.lib()
 

@@ -120,3 +120,54 @@ def test_device_plan_retries_a_small_step_cap(cuda, monkeypatch):
     for p in (dev, host):
         p["n_slots"] = p["n_chunks"] * 64
     _same(dev, host)
+
+
+def test_quad_plan_layout_is_padding_plus_permutation(cuda):
+    """CsrGraph._quad_plan (the layout of a GNNREC_TILED_QUAD kernel build): every wave's
+    chunk range is padded to a multiple of 4 with empty chunks (scratch row, header 0), the
+    slots of 4 chunks are interleaved per lane, the headers stay chunk-major, and the real
+    chunks are exactly the chunk-major plan's, in order."""
+    from src.ops import _lib
+    rng = np.random.default_rng(4)
+    g = CsrGraph.from_interactions(rng.integers(0, 3000, 60000), rng.integers(0, 2000, 60000),
+                                   3000, 2000).to(cuda)
+    R = 333
+    plan = g._tiled_plan_host(R, 4096, 512)
+    plan.update(rows_per_block=R)
+    std = {k: (v.clone() if isinstance(v, torch.Tensor) else v) for k, v in plan.items()}
+    CsrGraph._quad_plan(plan)
+    W, CH = _lib.TILED_WAVES, _lib.TILED_CHUNK
+    wp_old, wp = std["wave_ptr"].cpu().numpy(), plan["wave_ptr"].cpu().numpy()
+    assert np.all(np.diff(wp) % 4 == 0) and np.all(wp % 4 == 0)
+    total = int(wp[-1])
+    assert plan["n_chunks"] == total and plan["slot"].numel() == (total + 16) * CH
+    slot = plan["slot"].view(-1, CH, 4).transpose(1, 2).reshape(-1, CH).cpu().numpy()
+    val = plan["val"].view(-1, CH, 4).transpose(1, 2).reshape(-1, CH).cpu().numpy()
+    hdr = plan["hdr"].view(-1, 4).cpu().numpy()
+    s_old = std["slot"].view(-1, CH).cpu().numpy()
+    v_old = std["val"].view(-1, CH).cpu().numpy()
+    h_old = std["hdr"].view(-1, 4).cpu().numpy()
+    for w in range(wp_old.size - 1):
+        a, b = wp_old[w], wp_old[w + 1]
+        na = wp[w]
+        np.testing.assert_array_equal(slot[na:na + b - a], s_old[a:b])
+        np.testing.assert_array_equal(val[na:na + b - a], v_old[a:b])
+        np.testing.assert_array_equal(hdr[na:na + b - a], h_old[a:b])
+        pad = slice(na + b - a, wp[w + 1])
+        assert np.all(slot[pad] == R) and np.all(hdr[pad] == 0) and np.all(val[pad] == 0)
+    assert np.all(slot[total:] == R) and np.all(hdr[total:] == 0)
+    # a factored plan's class bytes move the same way
+    g2 = CsrGraph.from_interactions(rng.integers(0, 3000, 60000), rng.integers(0, 2000, 60000),
+                                    3000, 2000, binary=True).to(cuda)
+    p2 = g2._tiled_plan_device(R, 4096, 512)
+    p2.update(rows_per_block=R)
+    assert g2._factor_plan(p2)
+    c_old = p2["cls"].view(-1, CH).cpu().numpy().copy()
+    w2 = p2["wave_ptr"].cpu().numpy().copy()
+    CsrGraph._quad_plan(p2)
+    cls = p2["cls"].view(-1, CH, 4).transpose(1, 2).reshape(-1, CH).cpu().numpy()
+    wq = p2["wave_ptr"].cpu().numpy()
+    for w in range(w2.size - 1):
+        n = w2[w + 1] - w2[w]
+        np.testing.assert_array_equal(cls[wq[w]:wq[w] + n], c_old[w2[w]:w2[w + 1]])
+        assert np.all(cls[wq[w] + n:wq[w + 1]] == 0)
