@@ -148,6 +148,7 @@ class Layout:
         self.grid = RankGrid(full, rank, world, device, d, fg,
                              exchange="p2p" if exchange == "auto" else exchange)
         self.dg = self.grid.dg
+        log(f"layout F={self.grid.F} x R={self.grid.R}: shard on the device")
         self.src = distinct_cols(self.dg.shard, self.dg.shard.shape[1])
         self.x0_pad = None
         self.work = None
@@ -160,6 +161,7 @@ class Layout:
     def prepare(self, x0: torch.Tensor, device) -> "Layout":
         self.x0_pad = self.grid.x0_table(x0)
         self.work = make_work(self.dg, self.x0_pad.shape[1], device)
+        log(f"layout F={self.grid.F} x R={self.grid.R}: tables ready, planning")
         # operand re-layout for the column-ordered hop (built once, outside the timed region)
         t1 = time.perf_counter()
         plan = F.tiled_plan_for(self.dg.shard, self.x0_pad)
@@ -535,6 +537,7 @@ def main(argv=None) -> int:
                     + (f"_r{c[3]}" if c[3] else ""))
         tried = {}
         for cand in cands:
+            log(f"timing candidate {cname(cand)} ...")
             lay = layouts[cand[0]]
             cur.update(lay=lay, chunks=cand[2], reserve=cand[3])
             lay.dg.exchange_mode = cand[1]

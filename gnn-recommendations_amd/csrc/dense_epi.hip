@@ -35,8 +35,6 @@ struct DenseParams {
   int64_t ld_self;
   float* y;
   int64_t ldy;
-  float* y2;    // MODE 0: optional second copy of the output rows (a compact next-layer input)
-  int64_t ldy2;
   // MODE 0
   const float* W1;
   const float* b1;
@@ -284,7 +282,6 @@ __global__ __launch_bounds__(64 * NW) void spmm_mfma_kernel(DenseParams p) {
         }
       }
       if (p.y) stv<VEC>(p.y + r * p.ldy + VEC * gl, o);
-      if (MODE == 0 && p.y2) stv<VEC>(p.y2 + r * p.ldy2 + VEC * gl, o);
     }
   }
 }
@@ -571,8 +568,6 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
         }
       }
       if (p.y) *reinterpret_cast<float4*>(p.y + r * p.ldy + lc) = make_float4(o[0], o[1], o[2], o[3]);
-      if (MODE == 0 && p.y2)
-        *reinterpret_cast<float4*>(p.y2 + r * p.ldy2 + lc) = make_float4(o[0], o[1], o[2], o[3]);
     }
   }
 }
@@ -769,17 +764,16 @@ bool rows_ok(const float* p, int64_t ld) { return p && aligned16(p) && !(ld & 3)
 extern "C" int gnnrec_spmm_ngcf_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
                                     int64_t n_rows, const float* x, int64_t ldx,
                                     const float* x_self, int64_t ld_self, float* y, int64_t ldy,
-                                    float* y2, int64_t ldy2, int32_t d, const float* W1,
-                                    const float* b1, const float* W2, const float* b2, float slope,
-                                    const float* gas_blocks, const int32_t* gas_perm,
-                                    int32_t gas_bs, float* work, gnnrec_stream_t stream) {
+                                    int32_t d, const float* W1, const float* b1, const float* W2,
+                                    const float* b2, float slope, const float* gas_blocks,
+                                    const int32_t* gas_perm, int32_t gas_bs, float* work,
+                                    gnnrec_stream_t stream) {
   GNNREC_REQUIRE(n_rows >= 0, "spmm_ngcf: n_rows < 0");
   if (n_rows == 0) return GNNREC_OK;
   GNNREC_REQUIRE(row_ptr && col && val && W1 && b1 && W2 && b2, "spmm_ngcf: null operand");
   GNNREC_REQUIRE(ldx >= d && ld_self >= d && ldy >= d, "spmm_ngcf: leading dimension < d");
   GNNREC_REQUIRE(rows_ok(x, ldx) && rows_ok(x_self, ld_self) && rows_ok(y, ldy),
                  "spmm_ngcf: x/x_self/y must be 16-B aligned with ld %% 4 == 0");
-  GNNREC_REQUIRE(!y2 || (rows_ok(y2, ldy2) && ldy2 >= d), "spmm_ngcf: bad y2");
   if (gas_blocks) {
     GNNREC_REQUIRE(gas_perm && gas_bs >= 1 && gas_bs <= 32 && d % gas_bs == 0,
                    "spmm_ngcf: bad GAS block size %d", gas_bs);
@@ -787,7 +781,6 @@ extern "C" int gnnrec_spmm_ngcf_f32(const int64_t* row_ptr, const int32_t* col, 
   DenseParams p{};
   p.A = Csr{row_ptr, col, val, n_rows};
   p.x = x; p.ldx = ldx; p.x_self = x_self; p.ld_self = ld_self; p.y = y; p.ldy = ldy;
-  p.y2 = y2; p.ldy2 = ldy2;
   p.W1 = W1; p.b1 = b1; p.W2 = W2; p.b2 = b2; p.slope = slope;
   p.gas_blocks = gas_blocks; p.gas_perm = gas_perm; p.gas_bs = gas_bs;
   GNNREC_REQUIRE(!work || aligned16(work), "spmm_ngcf: work must be 16-B aligned");
@@ -824,8 +817,7 @@ extern "C" int gnnrec_spmm_dense_f32(const int64_t* row_ptr, const int32_t* col,
 // the rest exactly as the split form of the two calls above.
 extern "C" int gnnrec_ngcf_transform_f32(int64_t n_rows, const float* n, int64_t ldn,
                                          const float* x_self, int64_t ld_self, float* y,
-                                         int64_t ldy, float* y2, int64_t ldy2, int32_t d,
-                                         const float* W1, const float* b1,
+                                         int64_t ldy, int32_t d, const float* W1, const float* b1,
                                          const float* W2, const float* b2, float slope,
                                          const float* gas_blocks, const int32_t* gas_perm,
                                          int32_t gas_bs, gnnrec_stream_t stream) {
@@ -835,7 +827,6 @@ extern "C" int gnnrec_ngcf_transform_f32(int64_t n_rows, const float* n, int64_t
   GNNREC_REQUIRE(ldn >= d && ld_self >= d && ldy >= d, "ngcf_transform: leading dimension < d");
   GNNREC_REQUIRE(rows_ok(n, ldn) && rows_ok(x_self, ld_self) && rows_ok(y, ldy),
                  "ngcf_transform: n/x_self/y must be 16-B aligned with ld %% 4 == 0");
-  GNNREC_REQUIRE(!y2 || (rows_ok(y2, ldy2) && ldy2 >= d), "ngcf_transform: bad y2");
   if (gas_blocks) {
     GNNREC_REQUIRE(gas_perm && gas_bs >= 1 && gas_bs <= 32 && d % gas_bs == 0,
                    "ngcf_transform: bad GAS block size %d", gas_bs);
@@ -843,7 +834,6 @@ extern "C" int gnnrec_ngcf_transform_f32(int64_t n_rows, const float* n, int64_t
   DenseParams p{};
   p.A = Csr{nullptr, nullptr, nullptr, n_rows};
   p.x = n; p.ldx = ldn; p.x_self = x_self; p.ld_self = ld_self; p.y = y; p.ldy = ldy;
-  p.y2 = y2; p.ldy2 = ldy2;
   p.W1 = W1; p.b1 = b1; p.W2 = W2; p.b2 = b2; p.slope = slope;
   p.gas_blocks = gas_blocks; p.gas_perm = gas_perm; p.gas_bs = gas_bs;
   return launch_dense<0, false>(p, d, as_hip(stream));

@@ -102,23 +102,14 @@ class NGCF(BaseRecommender):
         n = self.n_users + self.n_items
         w = self.user_embedding.weight
         out = torch.empty((n, d * (self.n_layers + 1)), dtype=w.dtype, device=w.device)
-        # every layer's input is also kept as a compact [N, d] table: the hop gathers from it
-        # (128-B lines of a 256-B-stride table, not of the 1-KB-stride concat table) — the
-        # kernel stores its output rows twice (out2), no extra pass
-        cur = torch.empty((n, d), dtype=w.dtype, device=w.device)
-        cur[:self.n_users].copy_(self.user_embedding.weight.detach())
-        cur[self.n_users:].copy_(self.item_embedding.weight.detach())
-        out[:, :d].copy_(cur)
-        nxt = torch.empty_like(cur) if self.n_layers > 1 else None
+        out[:self.n_users, :d].copy_(self.user_embedding.weight.detach())
+        out[self.n_users:, :d].copy_(self.item_embedding.weight.detach())
         for k, (layer, gs) in enumerate(zip(self.layers, gs_layers)):
             blocks, perm = (gs.blocks(), gs.perm) if gs is not None else (None, None)
-            last = k + 1 == self.n_layers
-            ops.ngcf_layer(a, cur, layer.W1.weight, layer.W1.bias,
+            ops.ngcf_layer(a, out[:, k * d:(k + 1) * d], layer.W1.weight, layer.W1.bias,
                            layer.W2.weight, layer.W2.bias, layer.activation.negative_slope,
                            gas_blocks=blocks, gas_perm=perm, fused=layer.single_kernel,
-                           out=out[:, (k + 1) * d:(k + 2) * d], out2=None if last else nxt)
-            if not last:
-                cur, nxt = nxt, cur
+                           out=out[:, (k + 1) * d:(k + 2) * d])
         return out
 
     def predict(self, users, items, adj_matrix=None) -> torch.Tensor:

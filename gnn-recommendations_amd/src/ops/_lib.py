@@ -81,12 +81,12 @@ _SIGNATURES = {
                                   _i64, _i64, _p],
     "gnnrec_gas_f32": [_p, _i64, _i64, _i32, _i32, _p, _p, _p, _i64, _p],
     "gnnrec_spmm_gas_f32": [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i32, _i32, _p, _p, _p],
-    "gnnrec_spmm_ngcf_f32": [_p, _p, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _i32,
-                             _p, _p, _p, _p, _f32, _p, _p, _i32, _p, _p],
+    "gnnrec_spmm_ngcf_f32": [_p, _p, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _i32, _p, _p, _p,
+                             _p, _f32, _p, _p, _i32, _p, _p],
     "gnnrec_spmm_dense_f32": [_p, _p, _p, _i64, _p, _i64, _p, _i64, _i32, _p, _f32, _p, _i64,
                               _f32, _p, _i64, _i32, _f32, _f32, _p, _p],
-    "gnnrec_ngcf_transform_f32": [_i64, _p, _i64, _p, _i64, _p, _i64, _p, _i64, _i32, _p, _p,
-                                  _p, _p, _f32, _p, _p, _i32, _p],
+    "gnnrec_ngcf_transform_f32": [_i64, _p, _i64, _p, _i64, _p, _i64, _i32, _p, _p, _p, _p,
+                                  _f32, _p, _p, _i32, _p],
     "gnnrec_dense_transform_f32": [_i64, _p, _i64, _p, _i64, _i32, _p, _f32, _p, _i64, _f32,
                                    _p, _i64, _i32, _f32, _f32, _p],
     "gnnrec_rows_gemm_f32": [_i64, _p, _i64, _i32, _p, _i32, _p, _i64, _i32, _i32, _p, _i64,

@@ -490,14 +490,11 @@ def ngcf_layer(adj: CsrGraph, x: torch.Tensor, W1: torch.Tensor, b1: torch.Tenso
                x_self: Optional[torch.Tensor] = None,
                gas_blocks: Optional[torch.Tensor] = None,
                gas_perm: Optional[torch.Tensor] = None, fused: bool = False,
-               out: Optional[torch.Tensor] = None,
-               out2: Optional[torch.Tensor] = None) -> torch.Tensor:
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """NGCFLayer.forward in eval mode (ngcf.py:69-84), optionally followed by GAS.
     fused=False (default): hop into a scratch table + streaming MFMA transform (faster on
     gather-bound graphs); fused=True: one kernel. x_self: the destination rows' own x (the
-    rows of x by default; a rank's local rows when x is a sharded gather table). out2: an
-    optional second [n_rows, d] row-major table the same rows are stored into (a compact
-    next-layer input beside `out`, a column block of the model's concatenated output)."""
+    rows of x by default; a rank's local rows when x is a sharded gather table)."""
     x = _rowmajor(x)
     if x_self is None:
         x_self = x
@@ -512,11 +509,6 @@ def ngcf_layer(adj: CsrGraph, x: torch.Tensor, W1: torch.Tensor, b1: torch.Tenso
         if y.shape != (adj.n_rows, d) or y.stride(1) != 1 or y.stride(0) % 4:
             raise ValueError("out must be a row-major [n_rows, d] view with ld % 4 == 0")
         _require_device(adj, y)
-    if out2 is not None:
-        if out2.shape != (adj.n_rows, d) or out2.stride(1) != 1 or out2.stride(0) % 4:
-            raise ValueError("out2 must be a row-major [n_rows, d] view with ld % 4 == 0")
-        _require_device(adj, out2)
-    ld2 = out2.stride(0) if out2 is not None else d
     dev = x.device
     w1 = W1.detach().to(dev, torch.float32).contiguous()
     w2 = W2.detach().to(dev, torch.float32).contiguous()
@@ -531,8 +523,7 @@ def ngcf_layer(adj: CsrGraph, x: torch.Tensor, W1: torch.Tensor, b1: torch.Tenso
     stream = _lib.stream_of(adj.device)
     if fused:
         check(_lib.lib().gnnrec_spmm_ngcf_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(x_self),
-                                              x_self.stride(0), ptr(y), y.stride(0),
-                                              ptr(out2), ld2, d, ptr(w1),
+                                              x_self.stride(0), ptr(y), y.stride(0), d, ptr(w1),
                                               ptr(bb1), ptr(w2), ptr(bb2), float(slope), ptr(gb),
                                               ptr(gp), bs, None, stream), "gnnrec_spmm_ngcf_f32")
         return y
@@ -540,8 +531,7 @@ def ngcf_layer(adj: CsrGraph, x: torch.Tensor, W1: torch.Tensor, b1: torch.Tenso
     work = torch.empty((adj.n_rows, d), dtype=torch.float32, device=x.device)
     spmm_into(adj, x, work)
     check(_lib.lib().gnnrec_ngcf_transform_f32(adj.n_rows, ptr(work), d, ptr(x_self),
-                                               x_self.stride(0), ptr(y), y.stride(0),
-                                              ptr(out2), ld2, d, ptr(w1),
+                                               x_self.stride(0), ptr(y), y.stride(0), d, ptr(w1),
                                                ptr(bb1), ptr(w2), ptr(bb2), float(slope), ptr(gb),
                                                ptr(gp), bs, stream), "gnnrec_ngcf_transform_f32")
     return y

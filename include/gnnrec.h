@@ -313,13 +313,10 @@ int gnnrec_spmm_gas_f32(const int64_t* row_ptr, const int32_t* col, const float*
  * work: NULL = one fused kernel; else an [n_rows, d] scratch table (16-B aligned): the hop
  * runs as gnnrec_spmm_csr_f32 into it and a streaming MFMA kernel applies the rest (faster
  * on gather-bound graphs: the hop keeps its occupancy). Same results either way.
- * y2 (ABI 9, optional, NULL = none): a second copy of the output rows ([n_rows, ldy2]), e.g. a
- * compact next-layer input beside y's column block of the model's concatenated output.
  * d must be 32, 64 or 128 (MFMA f32 16x16x4 tiles). */
 int gnnrec_spmm_ngcf_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
                          int64_t n_rows, const float* x, int64_t ldx, const float* x_self,
-                         int64_t ld_self, float* y, int64_t ldy, float* y2, int64_t ldy2,
-                         int32_t d, const float* W1,
+                         int64_t ld_self, float* y, int64_t ldy, int32_t d, const float* W1,
                          const float* b1, const float* W2, const float* b2, float slope,
                          const float* gas_blocks, const int32_t* gas_perm, int32_t gas_bs,
                          float* work, gnnrec_stream_t stream);
@@ -346,8 +343,7 @@ int gnnrec_spmm_dense_f32(const int64_t* row_ptr, const int32_t* col, const floa
  * gnnrec_spmm_csr_split_f32, whose heavy-row kernel keeps power-law operands fast); the
  * rest is applied exactly as in their split form. n: [n_rows, ldn]. */
 int gnnrec_ngcf_transform_f32(int64_t n_rows, const float* n, int64_t ldn, const float* x_self,
-                              int64_t ld_self, float* y, int64_t ldy, float* y2, int64_t ldy2,
-                              int32_t d, const float* W1,
+                              int64_t ld_self, float* y, int64_t ldy, int32_t d, const float* W1,
                               const float* b1, const float* W2, const float* b2, float slope,
                               const float* gas_blocks, const int32_t* gas_perm, int32_t gas_bs,
                               gnnrec_stream_t stream);

@@ -40,7 +40,7 @@ for d in (64, 128):
     perm = torch.randperm(d, device=dev).to(torch.int32)
     for gas in (False, True):
         f = lambda: check(L.gnnrec_ngcf_transform_f32(  # noqa: E731
-            n, ptr(work), d, ptr(x), d, ptr(y), d, None, d, d, ptr(W1), ptr(b1), ptr(W2), ptr(b2), 0.2,
+            n, ptr(work), d, ptr(x), d, ptr(y), d, d, ptr(W1), ptr(b1), ptr(W2), ptr(b2), 0.2,
             ptr(blocks) if gas else None, ptr(perm) if gas else None, 8 if gas else 0, st), "t")
         ms = t_ms(f)
         res.append({"kind": "ngcf" + ("+gas" if gas else ""), "d": d, "ms": ms,
