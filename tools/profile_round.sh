@@ -11,10 +11,10 @@ BA=${BENCH_ARGS:-}
 CPU=""
 [ -n "${NO_CPU:-}" ] && CPU="--no-cpu-baseline"
 timeout -k 10 600 python bench.py $BA $CPU > $OUT/bench.json 2> $OUT/bench.err
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 bench.py $BA --no-cpu-baseline --steps 10 > $OUT/kt_bench.json 2> $OUT/kt.err
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py $BA --no-cpu-baseline --steps 3 --warmup 1 > $OUT/pmc_fetch_bench.json 2> $OUT/pmc_fetch.err
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py $BA --no-cpu-baseline --steps 3 --warmup 1 > $OUT/pmc_write_bench.json 2> $OUT/pmc_write.err
-timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/pmc_l2 -o run -- python3 bench.py $BA --no-cpu-baseline --steps 3 --warmup 1 > $OUT/pmc_l2_bench.json 2> $OUT/pmc_l2.err
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 bench.py $BA --no-cpu-baseline --no-vendor --steps 10 > $OUT/kt_bench.json 2> $OUT/kt.err
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py $BA --no-cpu-baseline --no-vendor --steps 3 --warmup 1 > $OUT/pmc_fetch_bench.json 2> $OUT/pmc_fetch.err
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py $BA --no-cpu-baseline --no-vendor --steps 3 --warmup 1 > $OUT/pmc_write_bench.json 2> $OUT/pmc_write.err
+timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/pmc_l2 -o run -- python3 bench.py $BA --no-cpu-baseline --no-vendor --steps 3 --warmup 1 > $OUT/pmc_l2_bench.json 2> $OUT/pmc_l2.err
 K=${KERNEL:-tiled_hop_kernel}
 F=$(find $OUT/pmc_fetch -name "*counter_collection.csv" -print -quit)
 W=$(find $OUT/pmc_write -name "*counter_collection.csv" -print -quit)
