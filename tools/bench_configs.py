@@ -112,9 +112,13 @@ def config5_model(shape, device):
 
 
 def _close(got, ref, rtol=1e-4, atol=1e-6) -> dict:
+    """Elementwise rtol 1e-4 (+ atol 1e-6), and the north star's bar: embeddings within 1e-4
+    (absolute, fp32)."""
     err = (got - ref).abs()
-    return {"max_abs_diff": float(err.max()), "max_abs_ref": float(ref.abs().max()),
-            "within_rtol_1e-4": bool((err <= atol + rtol * ref.abs()).all())}
+    mx = float(err.max())
+    return {"max_abs_diff": mx, "max_abs_ref": float(ref.abs().max()),
+            "within_rtol_1e-4": bool((err <= atol + rtol * ref.abs()).all()),
+            "within_north_star_1e-4": mx <= 1e-4}
 
 
 def torch_csr(g, device):
