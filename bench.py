@@ -536,8 +536,7 @@ def main(argv=None) -> int:
                                                        else "no_exchange")
                     + (f"_r{c[3]}" if c[3] else ""))
         tried = {}
-        for cand in cands:
-            log(f"timing candidate {cname(cand)} ...")
+        def time_candidate(cand):
             lay = layouts[cand[0]]
             cur.update(lay=lay, chunks=cand[2], reserve=cand[3])
             lay.dg.exchange_mode = cand[1]
@@ -552,20 +551,42 @@ def main(argv=None) -> int:
                 step()
             torch.cuda.synchronize()
             dist.barrier()
-            tt = torch.tensor([(time.perf_counter() - t0) / 3 * 1e3,
-                               float(np.sum(lay.timer.durations_ms())) / (3 * K),
-                               (float(np.sum(lay.xtimer.durations_ms())) / (3 * max(1, K - 1))
-                                if lay.xtimer is not None else 0.0)],
-                              dtype=torch.float64, device=device)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            out = [(time.perf_counter() - t0) / 3 * 1e3,
+                   float(np.sum(lay.timer.durations_ms())) / (3 * K),
+                   (float(np.sum(lay.xtimer.durations_ms())) / (3 * max(1, K - 1))
+                    if lay.xtimer is not None else 0.0)]
             lay.timer.reset(False)
             if lay.xtimer is not None:
                 lay.xtimer.reset(False)
+            return out
+
+        for cand in cands:
+            log(f"timing candidate {cname(cand)} ...")
+            lay = layouts[cand[0]]
+            # a candidate that raises (e.g. a collective form the backend rejects) is dropped
+            # on every rank — the flag's MAX reduction keeps the ranks' choices identical —
+            # instead of failing the whole run
+            try:
+                vals, failed = time_candidate(cand), 0.0
+            except Exception as ex:  # noqa: BLE001
+                log(f"candidate {cname(cand)} failed: {type(ex).__name__}: {ex}"[:300])
+                vals, failed = [float("inf")] * 3, 1.0
+                lay.timer.reset(False)
+                if lay.xtimer is not None:
+                    lay.xtimer.reset(False)
+            tt = torch.tensor(vals + [failed], dtype=torch.float64, device=device)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            if float(tt[3]) > 0:
+                tried[cname(cand)] = {"failed": True}
+                continue
             tried[cname(cand)] = {"ms_per_step": float(tt[0]), "compute_ms_per_hop": float(tt[1]),
                                   "exchange_ms_per_hop": float(tt[2]),
                                   "recv_bytes_per_hop_per_rank":
                                       lay.dg.recv_rows() * lay.x0_pad.shape[1] * 4}
             log(f"candidate {cname(cand)}: {tried[cname(cand)]}")
+        cands = [c for c in cands if not tried[cname(c)].get("failed")]
+        if not cands:
+            raise SystemExit("every exchange candidate failed")
         best = min(cands, key=lambda c: tried[cname(c)]["ms_per_step"])
         lay = layouts[best[0]]
         cur.update(lay=lay, chunks=best[2], reserve=best[3])
