@@ -300,6 +300,12 @@ __global__ __launch_bounds__(64 * NW) void spmm_mfma_kernel(DenseParams p) {
 #ifndef GNNREC_TRANSFORM_EXP
 #define GNNREC_TRANSFORM_EXP 0
 #endif
+// the next tile's rows in flight in registers during this tile's MFMAs (1), or loaded at the
+// tile start (0: 32 fewer VGPRs, e.g. for 16 waves per workgroup)
+#ifndef GNNREC_TRANSFORM_PREFETCH
+#define GNNREC_TRANSFORM_PREFETCH 1
+#endif
+constexpr bool kTransformPrefetch = GNNREC_TRANSFORM_PREFETCH != 0;
 #ifndef GNNREC_TRANSFORM_GAS_DPP
 #define GNNREC_TRANSFORM_GAS_DPP 0
 #endif
@@ -413,8 +419,9 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
   // output rows: lane covers rows 4 it + (lane >> 4), columns 4 (lane & 15) .. +3, it = 0..3
   const int lr = lane >> 4, lc = 4 * (lane & 15);
   int64_t tile = (int64_t)blockIdx.x * NW + wave;
-  load(tile);
+  if (kTransformPrefetch) load(tile);
   for (; tile < n_tiles; tile += stride) {
+    if (!kTransformPrefetch) load(tile);
     float an[4][4], ax[4][4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -433,7 +440,7 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
                                 : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
-    load(tile + stride);
+    if (kTransformPrefetch) load(tile + stride);
     floatx4 c1[4], c2[4];
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) c1[nt] = c2[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
