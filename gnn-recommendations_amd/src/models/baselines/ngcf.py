@@ -101,7 +101,10 @@ class NGCF(BaseRecommender):
             return None
         n = self.n_users + self.n_items
         w = self.user_embedding.weight
-        out = torch.empty((n, d * (self.n_layers + 1)), dtype=w.dtype, device=w.device)
+        # placed so that the gathered blocks x0 .. x_{K-1} avoid the slow line offset
+        # (ops.functional.gather_table); still a contiguous [N, (K+1) d] tensor
+        out = ops.functional.gather_table(n, d * (self.n_layers + 1), d * self.n_layers,
+                                          dtype=w.dtype, device=w.device)
         out[:self.n_users, :d].copy_(self.user_embedding.weight.detach())
         out[self.n_users:, :d].copy_(self.item_embedding.weight.detach())
         for k, (layer, gs) in enumerate(zip(self.layers, gs_layers)):

@@ -494,7 +494,9 @@ def ngcf_forward_dist(dg: DistributedGraph, model, x0_pad: torch.Tensor, *,
     x_local = dg.local_slice(x0_pad)
     widths = [x_local.shape[1]] + [layer.W1.out_features for layer in model.layers]
     # every layer writes its column block of the final cat(x0, ..., xK) table directly
-    local = torch.empty((n, sum(widths)), dtype=torch.float32, device=x0_pad.device)
+    # (placed so that the blocks the hops gather avoid the slow line offset, gather_table)
+    from .functional import gather_table
+    local = gather_table(n, sum(widths), sum(widths[:-1]), device=x0_pad.device)
     local[:, :widths[0]].copy_(x_local)
     c0 = widths[0]
     x_in = x0_pad

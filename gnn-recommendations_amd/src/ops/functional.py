@@ -101,6 +101,43 @@ def _tiled_supported(device, rows_per_block: int) -> bool:
     return _TILED_OK[key]
 
 
+# Gathering from a table whose rows are a multiple of 1 KB apart, the hop runs ~40 % slower
+# on a 32-feature slice whose 128-B lines start at byte 384 of a 1-KB window than at any
+# other line offset (G100M d = 32: 2.33 ms against 1.66-1.76 ms; d = 64 blocks covering that
+# line 3.99-4.06 ms against 3.31-3.36 ms; tools/exp_hop_offset2.py,
+# profiles/r04/exp_hop_line_offset.jsonl). Config 3's [N, 4d] concat table put layer 2's
+# input block exactly there. Tables this package allocates for its own gathered blocks are
+# placed so that none of their lines does.
+SLOW_GATHER_LINE = 384
+
+
+def gather_table_shift(addr: int, width: int, gathered_cols: int, esz: int = 4):
+    """Elements to skip from a buffer at byte address `addr` so that rows of `width` elements
+    whose columns [0, gathered_cols) are gathered keep every 128-B line of those columns off
+    SLOW_GATHER_LINE of a 1-KB window; None when there is nothing to choose (rows not a
+    multiple of 1 KB apart, `addr` not 128-B aligned, or the columns cover every offset)."""
+    if (width * esz) % 1024 or addr % 128:
+        return None
+    lines = range(0, -(-gathered_cols * esz // 128) * 128, 128)
+    good = [s for s in range(0, 1024, 128)
+            if all((s + o) % 1024 != SLOW_GATHER_LINE for o in lines)]
+    if not good:
+        return None
+    return min((s - addr) % 1024 for s in good) // esz
+
+
+def gather_table(n_rows: int, width: int, gathered_cols: int, *, dtype=torch.float32,
+                 device=None) -> torch.Tensor:
+    """torch.empty((n_rows, width)) — a contiguous row-major tensor, possibly at a storage
+    offset — whose columns [0, gathered_cols) are hop inputs, placed by gather_table_shift."""
+    esz = torch.empty((), dtype=dtype).element_size()
+    if (width * esz) % 1024 or n_rows == 0:
+        return torch.empty((n_rows, width), dtype=dtype, device=device)
+    buf = torch.empty(n_rows * width + 1024 // esz, dtype=dtype, device=device)
+    start = gather_table_shift(buf.data_ptr(), width, gathered_cols, esz) or 0
+    return buf[start:start + n_rows * width].view(n_rows, width)
+
+
 def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None,
                    reserve_cus: int = 0, outputs=()):
     """The column-ordered plan spmm_into would use for (adj, x) (and the `outputs` tables
