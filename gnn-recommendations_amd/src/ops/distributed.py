@@ -111,10 +111,16 @@ class DistributedGraph:
         owner = np.searchsorted(b, r, side="right") - 1
         return owner * self.rows_pad + (r - b[owner])
 
-    def pad_table(self, x: torch.Tensor) -> torch.Tensor:
-        """[N, d] global table -> [world*rows_pad, d] padded table on this rank's device."""
-        out = torch.zeros((self.world * self.rows_pad, x.shape[1]), dtype=x.dtype,
-                          device=self.device)
+    def pad_table(self, x: torch.Tensor, hop_layout: bool = False) -> torch.Tensor:
+        """[N, d] global table -> [world*rows_pad, d] padded table on this rank's device.
+        hop_layout (one rank, fp32): a functional.hop_table view, placed for the hops that
+        gather from it (a gathered table of several ranks stays compact: RCCL writes it)."""
+        if hop_layout and self.world == 1 and x.dtype == torch.float32:
+            from .functional import hop_table
+            out = hop_table(self.rows_pad, x.shape[1], device=self.device, zero=True)
+        else:
+            out = torch.zeros((self.world * self.rows_pad, x.shape[1]), dtype=x.dtype,
+                              device=self.device)
         idx = torch.from_numpy(self.padded_index()).to(self.device)
         out[idx] = x.to(self.device)
         return out
@@ -249,7 +255,7 @@ class RankGrid:
     def x0_table(self, x0: torch.Tensor) -> torch.Tensor:
         """This rank's columns of the [N, d] initial table in the row shards' padded layout."""
         c0, c1 = self.cols
-        return self.dg.pad_table(x0[:, c0:c1].contiguous())
+        return self.dg.pad_table(x0[:, c0:c1].contiguous(), hop_layout=True)
 
     def gather_features(self, local: torch.Tensor) -> torch.Tensor:
         """[n, d/F] column block of this rank -> [n, d] rows of its row shard (all F column
@@ -391,7 +397,9 @@ def _propagate_deferred(dg, x0_pad, K, hop, mkw, work, self_rows, chunked, overl
     n, d, dev = dg.n_local, x0_pad.shape[1], x0_pad.device
     if dg.world == 1:
         # y1 is gathered by hop 2 straight from the output rows: pad them to the table's rows
-        acc_piece = torch.empty((Xa.shape[0], d), dtype=torch.float32, device=dev)
+        # and place them like a hop table (the result is then a row-major strided view)
+        from .functional import hop_table
+        acc_piece = hop_table(Xa.shape[0], d, device=dev)
         acc_piece[n:].zero_()
         piece = {"acc": acc_piece, "a": Xa, "b": Xb}
         gath = dict(piece)
@@ -546,7 +554,12 @@ def gat_forward_dist(dg: DistributedGraph, model, x0_pad: torch.Tensor, *,
 def make_work(dg: DistributedGraph, d: int, device) -> tuple:
     """Hop buffers: Y [rows_pad, d] (zero padded tail) and two [world*rows_pad, d] tables."""
     rows = dg.world * dg.rows_pad
-    # world == 1 ping-pongs Xa/Xb directly, so Y is a placeholder
+    # world == 1 ping-pongs Xa/Xb directly, so Y is a placeholder, and the hops gather from
+    # Xa/Xb themselves: functional.hop_table's placement (several ranks: RCCL writes them)
     Y = torch.zeros((dg.rows_pad if dg.world > 1 else 1, d), dtype=torch.float32, device=device)
+    if dg.world == 1:
+        from .functional import hop_table
+        return (Y, hop_table(rows, d, device=device, zero=True),
+                hop_table(rows, d, device=device, zero=True))
     return (Y, torch.zeros((rows, d), dtype=torch.float32, device=device),
             torch.zeros((rows, d), dtype=torch.float32, device=device))

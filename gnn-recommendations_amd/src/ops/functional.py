@@ -138,6 +138,35 @@ def gather_table(n_rows: int, width: int, gathered_cols: int, *, dtype=torch.flo
     return buf[start:start + n_rows * width].view(n_rows, width)
 
 
+# Row stride of the tables the propagation gathers from, by width (floats -> (ld, start byte
+# of the 1-KB window)): compact rows put one line in eight at SLOW_GATHER_LINE; 256-B / 512-B
+# rows starting 1-KB aligned (d = 32 / 64), or 1-KB rows starting at byte 512 (d = 128), keep
+# every line off it. G100M LightGCN K = 3 on the bench path, same bits
+# (profiles/r04/exp_hop_tables.jsonl): d = 64 10.29 -> 9.88 ms, d = 32 5.08 -> 4.95 ms,
+# d = 128 20.70-20.81 -> 20.52 ms.
+HOP_TABLE_LAYOUT = {32: (64, 0), 64: (128, 0), 128: (256, 512)}
+
+
+def hop_table(n_rows: int, d: int, *, device=None, zero: bool = False,
+              layout: Optional[Tuple[int, int]] = None) -> torch.Tensor:
+    """A [n_rows, d] fp32 table for hops to gather from: a row-major view (row stride ld >= d,
+    16-B aligned rows) of a wider buffer placed per HOP_TABLE_LAYOUT (or `layout` = (ld,
+    start byte mod 1 KB)); a compact tensor for other widths. zero: the d columns are zeroed
+    (the padding columns are never read)."""
+    ld, start = layout if layout is not None else HOP_TABLE_LAYOUT.get(d, (d, None))
+    if start is None or n_rows == 0:
+        mk = torch.zeros if zero else torch.empty
+        return mk((n_rows, d), dtype=torch.float32, device=device)
+    if ld < d or ld % 4 or start % 128:
+        raise ValueError(f"hop_table layout ({ld}, {start}) for d = {d}")
+    buf = torch.empty(n_rows * ld + 256, dtype=torch.float32, device=device)
+    s = ((start - buf.data_ptr()) % 1024) // 4
+    t = buf[s:s + n_rows * ld].view(n_rows, ld)[:, :d]
+    if zero:
+        t.zero_()
+    return t
+
+
 def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None,
                    reserve_cus: int = 0, outputs=()):
     """The column-ordered plan spmm_into would use for (adj, x) (and the `outputs` tables
@@ -353,8 +382,9 @@ def _lightgcn_hops(op: CsrGraph, x0: torch.Tensor, K: int, masks,
     bufs = {"x0": x0, "acc": out, None: None}
     for k, (xn, yn, epi) in enumerate(lightgcn_hop_schedule(K, deferred), start=1):
         for name in (xn, yn):
-            if name not in bufs:
-                bufs[name] = torch.empty_like(x0)
+            if name not in bufs:   # scratch hop outputs: placed tables (hop_table) when tiled
+                bufs[name] = (hop_table(x0.shape[0], x0.shape[1], device=x0.device) if deferred
+                              else torch.empty_like(x0))
         xm, ya = masks(k, bufs[xn])
         if isinstance(xm, SparseSrc) and epi == 0:
             spmm_sparse_src_into(xm, bufs[xn], bufs[yn])

@@ -34,3 +34,17 @@ def test_gather_table_is_a_contiguous_view_of_the_requested_shape():
             shift = F.gather_table_shift(t.untyped_storage().data_ptr(), w, g)
             if shift is not None:
                 assert t.storage_offset() == shift
+
+
+def test_hop_table_layout_keeps_every_row_line_off_the_slow_offset():
+    for d, (ld, start) in F.HOP_TABLE_LAYOUT.items():
+        t = F.hop_table(64, d, zero=True)
+        assert t.shape == (64, d) and t.stride() == (ld, 1)
+        assert float(t.abs().sum()) == 0.0
+        base = t.data_ptr()
+        if base % 128 == 0:      # placement is by the actual address
+            assert (base - start) % 1024 == 0
+            for r in range(64):
+                assert F.SLOW_GATHER_LINE not in _lines(base + 4 * ld * r, d)
+    t = F.hop_table(5, 48)       # no layout for this width: a compact tensor
+    assert t.is_contiguous() and t.shape == (5, 48)
