@@ -124,8 +124,10 @@ def lightgcn_train_step_dist(dg: DistributedGraph, emb_local: torch.nn.Parameter
                 xm = row_nonzero(x_in)
                 ya = dg.local_slice(_reach(dg, dg.local_slice(xm))) if k == 1 else None
                 return xm, ya
+        # (one rank: the deferred schedule returns a row-major view of its placed output
+        # table, functional.hop_table; the optimizers take dense gradients)
         grad = lightgcn_propagate_dist(dg, _exchanged(dg, dy), K, hop_fn=hop_fn,
-                                       masks=bwd_masks)
+                                       masks=bwd_masks).contiguous()
         coef = None
         if max_grad_norm > 0:
             sq = (torch.linalg.vector_norm(grad, 2, dtype=torch.float64) ** 2).view(1)

@@ -84,6 +84,34 @@ def test_sharded_step_world1_native_matches_reference(cuda):
     np.testing.assert_allclose(emb.detach()[nu:].cpu().numpy(), f["item_w"], atol=2e-5)
 
 
+def test_sharded_step_world1_tiled_native_adam(cuda, monkeypatch):
+    """The same step with the column-ordered kernel forced onto the golden graph: the
+    deferred schedule on one rank (placed hop tables, a strided gradient view) feeds
+    NativeAdam, and the result still matches the reference trainer golden."""
+    from conftest import load_golden
+    from src.models import LightGCN
+    from src.ops import functional as F
+    from src.ops.distributed import DistributedGraph
+    from src.training import lightgcn_train_step_dist, make_adam
+    monkeypatch.setattr(F, "TILED_MIN_ROWS", 1)
+    monkeypatch.setattr(F, "TILED_MIN_TABLE_BYTES", 0)
+    f = load_golden("bpr_train_K3_d64")
+    g, nu, ni = _golden_graph()
+    torch.manual_seed(56)
+    m = LightGCN(nu, ni, embedding_dim=64, n_layers=3, init_scale=0.1)
+    x0 = torch.cat([m.user_embedding.weight, m.item_embedding.weight]).detach()
+    dg = DistributedGraph(g, 0, 1, cuda)
+    assert F.tiled_plan_for(dg.shard, dg.pad_table(x0, hop_layout=True)) is not None
+    emb = torch.nn.Parameter(x0.to(cuda).clone())
+    opt = make_adam([emb], 1e-2, 1e-4, cuda)
+    losses = [float(lightgcn_train_step_dist(dg, emb, 3, nu,
+                                             *[torch.from_numpy(f[k][b]).to(cuda)
+                                               for k in ("users", "pos", "neg")], opt))
+              for b in range(3)]
+    np.testing.assert_allclose(losses, f["losses"], rtol=1e-5)
+    np.testing.assert_allclose(emb.detach()[:nu].cpu().numpy(), f["user_w"], atol=2e-5)
+
+
 def test_sharded_step_row_subset_same_bits(cuda):
     """The sharded step's row-subset forward and masked backward (native hops) give the
     same bits as its full propagation."""
