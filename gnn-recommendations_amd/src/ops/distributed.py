@@ -290,7 +290,8 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
 
     x0_pad: [world*rows_pad, d] padded initial table (identical on every rank).
     Returns this rank's rows of mean(x0..xK) ([n_local, d]), or the full [N, d] table when
-    gather_output. `work` (from `make_work`) holds reusable hop buffers. With world == 1
+    gather_output — on one rank with the deferred schedule a row-major view of a placed
+    table (functional.hop_table: row stride > d), not a contiguous tensor. `work` (from `make_work`) holds reusable hop buffers. With world == 1
     the hop outputs feed the next hop directly (no gather, no copy).
     overlap_chunks > 1 (point-to-point exchange only): the hop runs in that many row chunks
     and each chunk's transfer is posted as soon as its kernel is queued, so the exchange of
