@@ -708,6 +708,9 @@ def main(argv=None) -> int:
                     + (f", {exchange_info['reserved_cus']} CUs left to RCCL"
                        if exchange_info.get('reserved_cus') else "") + ")"
                     if grid.R > 1 else ""),
+                # row stride (floats) of the gathered x0 table: functional.hop_table's
+                # placement on one rank, compact across ranks
+                "gather_table_ld": int(x0_pad.stride(0)),
             },
             "roofline": {
                 "bound": "hbm",
