@@ -405,17 +405,144 @@ def vendor_baseline(g: CsrGraph, x0: torch.Tensor, K: int, hip_out: torch.Tensor
     return res
 
 
-def verify(dg, full: CsrGraph, x0, x0_pad, K, out, device, rank, cols) -> dict:
-    """Full-size parity: this rank's rows of the timed (possibly sharded) propagation must equal,
-    bit for bit, a single-device propagation of the whole graph (the oracle itself is checked
-    against that kernel in tests/, at sizes it finishes in seconds)."""
-    from src.ops import functional as F
+ROCSPARSE_ALGS = {"csr": 1, "csr_row_split": 4, "csr_nnz_split": 5, "csr_merge_path": 9}
+
+
+def rocsparse_baseline(g: CsrGraph, x0: torch.Tensor, K: int, hip_out: torch.Tensor, hip_ms: float,
+                       device, reps: int = 5) -> dict:
+    """rocSPARSE's generic SpMM called directly (lib/libgnnrec_vendor.so, a ctypes-loaded shim
+    of rocsparse_spmm; vendor/rocsparse_spmm.cpp) on the same CSR (int64 row_ptr, int32 col,
+    fp32 val) and x0: K x `y = A x` + torch.stack(layers).mean(0) — the library call the
+    reference's `torch.sparse.mm(adj, x)` (lightgcn.py:88) stands for, without ATen's sparse
+    dispatch. Descriptors, buffer-size and preprocess stages outside the timing; every CSR
+    algorithm of rocsparse_spmm timed (HIP events on torch's stream, 1 untimed rep, then
+    `reps`, median), the fastest reported as `best`."""
+    import ctypes
+    libp = ROOT / "gnn-recommendations_amd" / "lib" / "libgnnrec_vendor.so"
+    res = {"what": f"K={K} x rocsparse_spmm(CSR i64/i32 f32, row-major B/C, alpha 1, beta 0) + "
+                   f"stack().mean(0)", "reps": reps, "statistic": "median"}
+    try:
+        lib = ctypes.CDLL(str(libp))
+    except OSError as ex:
+        res["error"] = f"{libp.name} not loadable: {ex}"[:300]
+        return res
+    vp, i64 = ctypes.c_void_p, ctypes.c_int64
+    lib.vendor_spmm_create.argtypes = [ctypes.POINTER(vp), vp, vp, vp, i64, i64, i64, vp, i64, vp,
+                                       i64, i64, ctypes.c_int, vp]
+    lib.vendor_spmm_run.argtypes = [vp, vp, vp, vp]
+    lib.vendor_spmm_destroy.argtypes = [vp]
+    lib.vendor_spmm_buffer_bytes.argtypes = [vp]
+    lib.vendor_spmm_buffer_bytes.restype = i64
+    lib.vendor_spmm_last_error.restype = ctypes.c_char_p
+    res["rocsparse_version"] = int(lib.vendor_spmm_version())
+    N, d = g.shape[0], x0.shape[1]
+    rp = g.row_ptr.to(device)
+    col = g.col.to(device)
+    val = g.val.to(device)
+    xd = x0.to(device).contiguous()
+    ys = [torch.empty_like(xd) for _ in range(K)]
+    stream = torch.cuda.current_stream(device).cuda_stream
+    best = None
+    for name, alg in ROCSPARSE_ALGS.items():
+        ctx = vp()
+        try:
+            st = lib.vendor_spmm_create(ctypes.byref(ctx), rp.data_ptr(), col.data_ptr(),
+                                        val.data_ptr(), N, N, g.nnz, xd.data_ptr(), d,
+                                        ys[0].data_ptr(), d, d, alg, stream)
+            if st != 0:
+                res[name] = {"error": lib.vendor_spmm_last_error().decode()}
+                continue
+
+            def prop():
+                x = xd
+                for k in range(K):
+                    s = lib.vendor_spmm_run(ctx, x.data_ptr(), ys[k].data_ptr(), stream)
+                    if s != 0:
+                        raise RuntimeError(lib.vendor_spmm_last_error().decode())
+                    x = ys[k]
+                return torch.stack([xd] + ys, dim=0).mean(dim=0)
+            out = prop()
+            torch.cuda.synchronize()
+            ms = []
+            for _ in range(reps):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                o2 = prop()
+                e.record()
+                torch.cuda.synchronize()
+                ms.append(s.elapsed_time(e))
+                del o2
+            t = float(np.median(ms))
+            res[name] = {"ms_per_step": t, "ms_samples": ms, "edges_per_s": K * g.nnz / (t * 1e-3),
+                         "buffer_bytes": int(lib.vendor_spmm_buffer_bytes(ctx)),
+                         "max_abs_diff_vs_hip": float((out - hip_out).abs().max()),
+                         "bit_exact_vs_hip": bool(torch.equal(out.view(torch.int32),
+                                                              hip_out.view(torch.int32))),
+                         "hip_speedup": t / hip_ms}
+            if best is None or t < res[best]["ms_per_step"]:
+                best = name
+            del out
+        except Exception as ex:  # noqa: BLE001 — recorded, not fatal to the bench line
+            res[name] = {"error": f"{type(ex).__name__}: {ex}"[:300]}
+        finally:
+            torch.cuda.synchronize()
+            if ctx.value:
+                lib.vendor_spmm_destroy(ctx)
+            torch.cuda.empty_cache()
+        log(f"vendor rocsparse {name}: {res[name]}")
+    res["best"] = best
+    del rp, col, val, xd, ys
+    torch.cuda.empty_cache()
+    return res
+
+
+def probe_exchange(dg, mode: str, x0_pad: torch.Tensor) -> None:
+    """One exchange of `mode` on an 8-row slice of every piece (the pre-flight of a
+    candidate): the same collective calls as a timed hop's exchange, on a small buffer."""
+    rows = min(8, dg.rows_pad)
+    d = x0_pad.shape[1]
+    piece = torch.zeros((rows, d), dtype=torch.float32, device=x0_pad.device)
+    out = torch.zeros((dg.world * rows, d), dtype=torch.float32, device=x0_pad.device)
+    saved = (dg.exchange_mode, dg.rows_pad)
+    try:
+        dg.exchange_mode, dg.rows_pad = mode, rows
+        dg.exchange(out, piece)
+        if x0_pad.is_cuda:
+            torch.cuda.synchronize()
+    finally:
+        dg.exchange_mode, dg.rows_pad = saved
+
+
+def resolve_verify(flag, world: int) -> bool:
+    """--verify / --no-verify as given; unset: on for N > 1 (the driver runs bench.py without
+    flags, so its multi-GPU line checks itself), off at N = 1 (the CPU baseline already
+    compares the output bit for bit with the reference's CPU path)."""
+    return bool(world > 1) if flag is None else bool(flag)
+
+
+def _single_device_forward(full: CsrGraph, x0: torch.Tensor, K: int, device) -> torch.Tensor:
     g1 = full.to(device)
     ref, _ = F.lightgcn_forward(g1, x0.to(device), K)
+    return ref
+
+
+def verify(dg, full: CsrGraph, x0, K, out, device, cols, world: int,
+           reference_fn=_single_device_forward) -> dict:
+    """Full-size parity: this rank's rows of the timed (possibly sharded) propagation must equal,
+    bit for bit, a single-device propagation of the whole graph (the oracle itself is checked
+    against that kernel in tests/, at sizes it finishes in seconds). N > 1: every rank's flag
+    is MIN-reduced into `all_ranks_bit_exact` (a collective: every rank calls this).
+    reference_fn(full, x0, K, device) -> [N, d]: the single-device propagation (tests inject
+    the CPU oracle)."""
+    ref = reference_fn(full, x0, K, device)
     mine = out
     same = torch.equal(ref[dg.row_begin:dg.row_end, cols[0]:cols[1]], mine)
     res = {"bit_exact_vs_single_device": bool(same), "rows": int(mine.shape[0])}
-    del g1, ref
+    del ref
+    if world > 1:
+        ok = torch.tensor([1 if same else 0], device=device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        res["all_ranks_bit_exact"] = bool(ok.item())
     return res
 
 
@@ -435,9 +562,10 @@ def main(argv=None) -> int:
                     help="skip the vendor comparator (torch.sparse.mm on the device, N = 1)")
     ap.add_argument("--cpu-reps", type=int, default=2,
                     help="timed reps of the reference CPU path (median reported)")
-    ap.add_argument("--verify", action="store_true",
+    ap.add_argument("--verify", action=argparse.BooleanOptionalAction, default=None,
                     help="after timing, compare this rank's rows bit for bit with a single-device "
-                         "propagation of the whole graph")
+                         "propagation of the whole graph (default: on when N > 1, so the "
+                         "driver's multi-GPU line carries its own check; --no-verify skips it)")
     ap.add_argument("--exchange", default="auto", choices=["auto", "allgather", "p2p"],
                     help="per-hop exchange: allgather, bipartite point-to-point, or auto "
                          "(time both before the timed region, keep the faster)")
@@ -452,6 +580,7 @@ def main(argv=None) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    a.verify = resolve_verify(a.verify, world)
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus N > 1 needs one process per GPU: launch with "
@@ -508,7 +637,8 @@ def main(argv=None) -> int:
     def step():
         lay = cur["lay"]
         return lightgcn_propagate_dist(lay.dg, lay.x0_pad, K, hop_fn=lay.timer.hop, work=lay.work,
-                                       overlap_chunks=cur["chunks"], reserve_cus=cur["reserve"])
+                                       overlap_chunks=cur["chunks"], reserve_cus=cur["reserve"],
+                                       placed_output=True)
 
     # Exchange form (N > 1): time whole steps of each candidate (layout, exchange, overlap
     # chunks, CUs left to RCCL) before the timed region and keep the fastest (same decision on
@@ -560,21 +690,40 @@ def main(argv=None) -> int:
                 lay.xtimer.reset(False)
             return out
 
+        # Pre-flight: every rank runs each (layout, exchange form) once on a small piece, in
+        # lock-step, catching a form the backend rejects (it raises at the same call on every
+        # rank: the calls do not depend on data); the ranks agree on the outcome (MAX) before
+        # any timed collective runs.
+        preflight = {}
+        for key in sorted({c[:2] for c in cands if layouts[c[0]].dg.world > 1}):
+            dgk = layouts[key[0]].dg
+            try:
+                probe_exchange(dgk, key[1], layouts[key[0]].x0_pad)
+                bad = 0.0
+            except Exception as ex:  # noqa: BLE001
+                log(f"pre-flight {key[1]} on layout {key[0]} failed: {type(ex).__name__}: {ex}"[:300])
+                bad = 1.0
+            flag = torch.tensor([bad], dtype=torch.float64, device=device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            preflight[key] = float(flag.item()) == 0.0
         for cand in cands:
             log(f"timing candidate {cname(cand)} ...")
             lay = layouts[cand[0]]
-            # a candidate that raises (e.g. a collective form the backend rejects) is dropped
-            # on every rank — the flag's MAX reduction keeps the ranks' choices identical —
-            # instead of failing the whole run
+            # a candidate whose exchange form failed the pre-flight probe on any rank is
+            # dropped on every rank (the flag's MAX reduction keeps the choices identical)
+            if not preflight.get(cand[:2] if lay.dg.world > 1 else None, True):
+                tried[cname(cand)] = {"failed": True, "why": "exchange pre-flight failed"}
+                continue
             try:
-                vals, failed = time_candidate(cand), 0.0
+                vals = time_candidate(cand)
             except Exception as ex:  # noqa: BLE001
-                log(f"candidate {cname(cand)} failed: {type(ex).__name__}: {ex}"[:300])
-                vals, failed = [float("inf")] * 3, 1.0
-                lay.timer.reset(False)
-                if lay.xtimer is not None:
-                    lay.xtimer.reset(False)
-            tt = torch.tensor(vals + [failed], dtype=torch.float64, device=device)
+                # past the pre-flight a failure may be on this rank only, with its peers
+                # inside a collective: no collective can follow safely, so end the job (the
+                # launcher tears the other ranks down) instead of hanging the node
+                print(f"[bench rank {rank}] candidate {cname(cand)} failed after the "
+                      f"pre-flight: {type(ex).__name__}: {ex}"[:400], file=sys.stderr, flush=True)
+                os._exit(3)
+            tt = torch.tensor(vals + [0.0], dtype=torch.float64, device=device)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             if float(tt[3]) > 0:
                 tried[cname(cand)] = {"failed": True}
@@ -653,11 +802,7 @@ def main(argv=None) -> int:
 
     check = None
     if a.verify:
-        check = verify(dg, verify_graph, x0, x0_pad, K, out, device, rank, grid.cols)
-        if world > 1:
-            ok = torch.tensor([1 if check["bit_exact_vs_single_device"] else 0], device=device)
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-            check["all_ranks_bit_exact"] = bool(ok.item())
+        check = verify(dg, verify_graph, x0, K, out, device, grid.cols, world)
         del verify_graph
 
     workload_key = f"g100m_lightgcn_k{K}_d{d}_n{world}" + ("_tiled" if tiled else "")
@@ -668,6 +813,8 @@ def main(argv=None) -> int:
     if vendor_graph is not None:
         log("timing the vendor comparator (torch.sparse.mm on the device) ...")
         vendor = vendor_baseline(vendor_graph, x0, K, out, ms_per_step, device)
+        log("timing rocsparse_spmm called directly ...")
+        vendor["rocsparse"] = rocsparse_baseline(vendor_graph, x0, K, out, ms_per_step, device)
         del vendor_graph
 
     cpu = None
@@ -682,6 +829,12 @@ def main(argv=None) -> int:
         cpu = cpu_baseline(cpu_graph, x0, K, a.users, gpu_hop1, gpu_out, reps=a.cpu_reps)
         del gpu_hop1, gpu_out
 
+    # the backend that actually carried the exchange: "nccl" is RCCL on ROCm; the gloo
+    # harness (several ranks sharing one GPU) stages every exchange through the host
+    exchange_backend = None
+    if world > 1:
+        be = dist.get_backend(dg.group)
+        exchange_backend = "RCCL" if be == "nccl" else f"{be} (host-staged harness, not RCCL)"
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -703,7 +856,7 @@ def main(argv=None) -> int:
                 "nnz": int(nnz_total), "n_nodes": N, "n_layers": K, "dim": d,
                 "parallelism": (f"{grid.F} feature groups x " if grid.F > 1 else "")
                 + f"dst-row shards x{grid.R}" + (
-                    f" + per-hop RCCL exchange ({exchange_info['mode']}, "
+                    f" + per-hop {exchange_backend} exchange ({exchange_info['mode']}, "
                     f"{exchange_info['overlap_chunks']} overlap chunks"
                     + (f", {exchange_info['reserved_cus']} CUs left to RCCL"
                        if exchange_info.get('reserved_cus') else "") + ")"
@@ -752,7 +905,8 @@ def main(argv=None) -> int:
             "edges_per_s_per_interaction": value / 2.0,
             "hbm_gbps_algorithmic_step": K * launch_bytes * world / (ms_per_step * 1e-3) / 1e9,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
-            "exchange": dict(exchange_info, recv_bytes_per_hop_per_rank=dg.recv_rows() * d_loc * 4,
+            "exchange": dict(exchange_info, backend=exchange_backend,
+                             recv_bytes_per_hop_per_rank=dg.recv_rows() * d_loc * 4,
                              feature_groups=grid.F, row_shards=grid.R,
                              # rank 0's compute-stream view per exchanged hop (K - 1 per step)
                              exchange_ms_per_hop=(float(np.sum(xtimer.durations_ms()))

@@ -21,6 +21,8 @@ CSRC = PKG_ROOT / "csrc"
 INCLUDE = PKG_ROOT.parent / "include"
 BUILD = PKG_ROOT / "build"
 LIB = PKG_ROOT / "lib" / "libgnnrec.so"
+VENDOR_SRC = PKG_ROOT / "vendor" / "rocsparse_spmm.cpp"
+VENDOR_LIB = PKG_ROOT / "lib" / "libgnnrec_vendor.so"
 
 ARCH = "gfx950"
 # fp-contract off: every FMA in the kernels is an explicit fmaf, nothing else may fuse
@@ -82,7 +84,26 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs),
              "-lpthread"])
         os.replace(tmp, LIB)
+    build_vendor(force=force, verbose=verbose)
     return LIB
+
+
+def build_vendor(force: bool = False, verbose: bool = False) -> Path:
+    """lib/libgnnrec_vendor.so: bench.py's rocSPARSE comparator (vendor/rocsparse_spmm.cpp).
+    Host code only, linked against librocsparse; never loaded by the product path."""
+    src = VENDOR_SRC
+    if not (force or _stale(VENDOR_LIB, [src])):
+        return VENDOR_LIB
+    tmp = VENDOR_LIB.with_suffix(".so.tmp")
+    cmd = [_hipcc(), "-O2", "-fPIC", "-std=c++17", "-shared", "-Wall", str(src), "-o", str(tmp),
+           "-L/opt/rocm/lib", "-lrocsparse", "-Wl,-rpath,/opt/rocm/lib"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, VENDOR_LIB)
+    return VENDOR_LIB
 
 
 def main(argv=None) -> int:

@@ -42,6 +42,12 @@ struct GatParams {
   int64_t ld_acc;
   float acc_div;
   int64_t max_row_len;  // rows longer than this are left to the split path (0: none)
+  // attention vectors (ATT kernels): att[0][h][o_dim] (self), att[1][h][o_dim] (neighbour):
+  // s_self[r, h] = att[0][h] . row_r,h and s_neigh[j, h] = att[1][h] . row_j,h from the rows
+  // the kernel reads anyway (s_self / s_neigh / ld_* unused)
+  const float* att;
+  const float* hself;   // ATT: destination row r's own row (hself + r * ld_hself, head_stride)
+  int64_t ld_hself;
 };
 
 // Softmax normalisation + head mean + ELU + store + layer-mean epilogue of one row.
@@ -92,6 +98,33 @@ __device__ __forceinline__ float gat_logit2(float ss, float sn, float slope, boo
   return valid ? e * kLog2e : -INFINITY;
 }
 
+// ---- scores from the gathered rows (ATT kernels) -------------------------------------------
+// s_neigh[j, h] = a_h . row_j,h is a dot product of a row the kernel gathers for the weighted
+// sum anyway, so it is formed in registers instead of gathered: 2 instead of 3 128-B lines per
+// neighbour of a 256-B row (the score table's line was a third random request per edge). The
+// dot of a head spans its hl = o_dim / 4 lanes (4 features each); the lane sums reduce with DPP
+// moves inside the aligned hl-lane group, in an order that gives every lane the same bits.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                               CTRL, 0xF, 0xF, false));
+}
+constexpr int kDppRowMirror = 0x140, kDppHalfMirror = 0x141, kDppXor2 = 0x4E, kDppXor1 = 0xB1,
+              kDppRor8 = 0x128;
+
+// sum over the aligned group of hl lanes (hl in {1, 2, 4, 8, 16}), in every lane of it
+__device__ __forceinline__ float group_sum(float v, int hl) {
+  if (hl >= 16) v += dpp_f<kDppRowMirror>(v);   // lane i + lane 15 - i
+  if (hl >= 8) v += dpp_f<kDppHalfMirror>(v);   // lane i + lane 7 - i (8-lane halves)
+  if (hl >= 4) v += dpp_f<kDppXor2>(v);
+  if (hl >= 2) v += dpp_f<kDppXor1>(v);
+  return v;
+}
+
+__device__ __forceinline__ float dot4(const float4& a, const float4& b) {
+  return __builtin_fmaf(a.w, b.w, __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)));
+}
+
 // One softmax block of one head: logits E[0..kSoftBlock), rows xv[0..kSoftBlock).
 __device__ __forceinline__ void gat_block(const float (&E)[kSoftBlock], const float4* xv,
                                           float& m, float& l, float4& a) {
@@ -113,14 +146,23 @@ __device__ __forceinline__ void gat_block(const float (&E)[kSoftBlock], const fl
 
 // Online-softmax accumulation of neighbours [beg, end) of row r (head of this lane); m is in
 // the base-2 logit domain.
-template <int GROUP>
+template <int GROUP, bool ATT>
 __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, int64_t beg,
                                                int64_t end, int gl, float& m, float& l,
                                                float4& a) {
   static_assert(kChunk % kSoftBlock == 0, "a gather step holds whole softmax blocks");
   const int hl = p.o_dim / 4;
   const int head = gl / hl;
-  const float ss = p.s_self[r * p.ld_ss + head];
+  const int fo = 4 * (gl - head * hl);   // this lane's features of its head's row
+  float ss;
+  float4 an = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (ATT) {
+    const float4 as = ld4(p.att + head * p.o_dim + fo);
+    an = ld4(p.att + (p.heads + head) * p.o_dim + fo);
+    ss = group_sum(dot4(ld4(p.hself + r * p.ld_hself + head * p.head_stride + fo), as), hl);
+  } else {
+    ss = p.s_self[r * p.ld_ss + head];
+  }
   for (int64_t k0 = beg; k0 < end; k0 += kChunk) {
     constexpr int PER = (GROUP >= kChunk) ? 1 : kChunk / GROUP;
     int cm[PER];
@@ -135,8 +177,12 @@ __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, in
 #pragma unroll
     for (int t = 0; t < kChunk; ++t) {
       const int c = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
-      xv[t] = ld4(p.h + (int64_t)c * p.ldh + head * p.head_stride + 4 * (gl - head * hl));
-      sn[t] = p.s_neigh[(int64_t)c * p.ld_sn + head];
+      xv[t] = ld4(p.h + (int64_t)c * p.ldh + head * p.head_stride + fo);
+      if constexpr (!ATT) sn[t] = p.s_neigh[(int64_t)c * p.ld_sn + head];
+    }
+    if constexpr (ATT) {
+#pragma unroll
+      for (int t = 0; t < kChunk; ++t) sn[t] = group_sum(dot4(xv[t], an), hl);
     }
 #pragma unroll
     for (int b = 0; b < kChunk / kSoftBlock; ++b) {
@@ -150,7 +196,7 @@ __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, in
   }
 }
 
-template <int F>
+template <int F, bool ATT>
 __global__ __launch_bounds__(kBlock) void gat_kernel(GatParams p) {
   constexpr int GROUP = F / 4;
   constexpr int RPW = 64 / GROUP;
@@ -162,7 +208,7 @@ __global__ __launch_bounds__(kBlock) void gat_kernel(GatParams p) {
   if (p.max_row_len > 0 && end - beg > p.max_row_len) return;  // heavy row: split path
   float m = -INFINITY, l = 0.f;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  gat_accumulate<GROUP>(p, r, beg, end, gl, m, l, a);
+  gat_accumulate<GROUP, ATT>(p, r, beg, end, gl, m, l, a);
   // softmax normalisation (l = 0 for an empty row -> 0/0 = NaN, like the reference)
   gat_finish<GROUP>(p, r, make_float4(a.x / l, a.y / l, a.z / l, a.w / l), gl);
 }
@@ -189,6 +235,45 @@ __device__ __forceinline__ void gat_apply16(std::integer_sequence<int, T...>, fl
     l[3] += row_bcast<T + 8>(pb), a[3] = fma4(row_bcast<T + 8>(pb), xv[T], a[3])), ...);
 }
 
+// ATT form of the shared-row scores: every lane holds 4 of the 64 features of the 8 neighbour
+// rows, so s_neigh[t, h] = v_h . x_t is 16 lanes' partial dots; a reduce-scatter over the
+// 16-lane row group (DPP: lanes L / L^8 exchange head pairs, then the 8-lane halves split the
+// neighbours 4 / 2 / 1) leaves lane gl exactly the two sums it turns into logits below:
+// neighbour gl & 7, heads 2 (gl >> 3) and 2 (gl >> 3) + 1.
+__device__ __forceinline__ void shared_scores16(const float4 (&xv)[8], const float4 (&an)[4],
+                                                int gl, float& sa, float& sb) {
+  const bool hi = gl >= 8, b2 = gl & 4, b1 = gl & 2, b0 = gl & 1;
+  float Q[8][2];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float mine = dot4(xv[t], an[j]), other = dot4(xv[t], an[2 + j]);
+      const float keep = hi ? other : mine, send = hi ? mine : other;
+      Q[t][j] = keep + dpp_f<kDppRor8>(send);        // lanes L, L^8: heads 2hi, 2hi + 1
+    }
+  }
+  float R[4][2];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)                          // lanes t, 7 - t: neighbours 4 b2 + k
+      R[k][j] = (b2 ? Q[4 + k][j] : Q[k][j]) + dpp_f<kDppHalfMirror>(b2 ? Q[k][j] : Q[4 + k][j]);
+  float S[2][2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)                          // lanes t, t^2: neighbours .. + 2 b1 + k
+      S[k][j] = (b1 ? R[2 + k][j] : R[k][j]) + dpp_f<kDppXor2>(b1 ? R[k][j] : R[2 + k][j]);
+  float T[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)                            // lanes t, t^1: neighbour t
+    T[j] = (b0 ? S[1][j] : S[0][j]) + dpp_f<kDppXor1>(b0 ? S[0][j] : S[1][j]);
+  sa = T[0];
+  sb = T[1];
+}
+
+template <bool ATT>
 __device__ __forceinline__ void gat_shared_rows16(const GatParams& p, int64_t r, int64_t beg,
                                                   int64_t end, int gl, const float (&ss)[4],
                                                   float (&m)[4], float (&l)[4],
@@ -196,6 +281,11 @@ __device__ __forceinline__ void gat_shared_rows16(const GatParams& p, int64_t r,
   const int tl = gl & 7;
   const bool hi = gl >= 8;                       // heads 2, 3 (else 0, 1)
   const float ssa = hi ? ss[2] : ss[0], ssb = hi ? ss[3] : ss[1];
+  float4 an[4];
+  if constexpr (ATT) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) an[h] = ld4(p.att + (4 + h) * 64 + 4 * gl);
+  }
   for (int64_t k0 = beg; k0 < end; k0 += 8) {
     int64_t k = k0 + gl;
     k = k < end ? k : end - 1;
@@ -206,11 +296,18 @@ __device__ __forceinline__ void gat_shared_rows16(const GatParams& p, int64_t r,
       const int c = __shfl(cm, t, 16);
       xv[t] = ld4(p.h + (int64_t)c * p.ldh + 4 * gl);
     }
-    const int co = __shfl(cm, tl, 16);
-    const float4 s4 = ld4(p.s_neigh + (int64_t)co * p.ld_sn);
+    float sna, snb;
+    if constexpr (ATT) {
+      shared_scores16(xv, an, gl, sna, snb);
+    } else {
+      const int co = __shfl(cm, tl, 16);
+      const float4 s4 = ld4(p.s_neigh + (int64_t)co * p.ld_sn);
+      sna = hi ? s4.z : s4.x;
+      snb = hi ? s4.w : s4.y;
+    }
     const bool valid = k0 + tl < end;
-    const float ea = gat_logit2(ssa, hi ? s4.z : s4.x, p.slope, valid);
-    const float eb = gat_logit2(ssb, hi ? s4.w : s4.y, p.slope, valid);
+    const float ea = gat_logit2(ssa, sna, p.slope, valid);
+    const float eb = gat_logit2(ssb, snb, p.slope, valid);
     float ma = ea, mb = eb;   // block max per head over the 8 lanes of the half-row
 #pragma unroll
     for (int d = 1; d < 8; d <<= 1) {
@@ -239,14 +336,15 @@ __device__ __forceinline__ void gat_shared_rows16(const GatParams& p, int64_t r,
 // kernel would spread the heads over H times as many lanes that all load the same bytes).
 // Per (row, head, feature) the arithmetic is the generic kernel's, step for step.
 // Neighbours [beg, end) of row r in shared-row mode (the online-softmax state of H heads).
-template <int O, int H, int CH>
+template <int O, int H, int CH, bool ATT>
 __device__ __forceinline__ void gat_shared_range(const GatParams& p, int64_t r, int64_t beg,
                                                  int64_t end, int gl, const float (&ss)[H],
                                                  float (&m)[H], float (&l)[H], float4 (&a)[H]) {
   constexpr int GROUP = O / 4;
   static_assert(CH == kSoftBlock, "one softmax block per gather step (same blocks as gat_kernel)");
+  static_assert(!ATT || (GROUP == 16 && H == 4 && CH == 8), "ATT: the 16-lane, 4-head form");
   if constexpr (GROUP == 16 && H == 4 && CH == 8) {
-    gat_shared_rows16(p, r, beg, end, gl, ss, m, l, a);
+    gat_shared_rows16<ATT>(p, r, beg, end, gl, ss, m, l, a);
   } else {
   for (int64_t k0 = beg; k0 < end; k0 += CH) {
     constexpr int PER = (GROUP >= CH) ? 1 : CH / GROUP;
@@ -282,7 +380,22 @@ __device__ __forceinline__ void gat_shared_range(const GatParams& p, int64_t r, 
   }
 }
 
-template <int O, int H, int CH>
+// the H self scores of row r for the shared-row kernels: from s_self, or (ATT) as dots of the
+// row's own x with att[0][h] over the 16 lanes (every lane gets the same bits)
+template <int O, int H, bool ATT>
+__device__ __forceinline__ void shared_self_scores(const GatParams& p, int64_t r, int gl,
+                                                   float (&ss)[H]) {
+  if constexpr (ATT) {
+    const float4 xr = ld4(p.hself + r * p.ld_hself + 4 * gl);
+#pragma unroll
+    for (int h = 0; h < H; ++h) ss[h] = group_sum(dot4(xr, ld4(p.att + h * O + 4 * gl)), O / 4);
+  } else {
+#pragma unroll
+    for (int h = 0; h < H; ++h) ss[h] = p.s_self[r * p.ld_ss + h];
+  }
+}
+
+template <int O, int H, int CH, bool ATT>
 __global__ __launch_bounds__(kBlock) void gat_shared_kernel(GatParams p) {
   constexpr int GROUP = O / 4;
   constexpr int RPW = 64 / GROUP;
@@ -294,14 +407,14 @@ __global__ __launch_bounds__(kBlock) void gat_shared_kernel(GatParams p) {
   if (p.max_row_len > 0 && end - beg > p.max_row_len) return;  // heavy row: split path
   float ss[H], m[H], l[H];
   float4 a[H];
+  shared_self_scores<O, H, ATT>(p, r, gl, ss);
 #pragma unroll
   for (int h = 0; h < H; ++h) {
-    ss[h] = p.s_self[r * p.ld_ss + h];
     m[h] = -INFINITY;
     l[h] = 0.f;
     a[h] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  gat_shared_range<O, H, CH>(p, r, beg, end, gl, ss, m, l, a);
+  gat_shared_range<O, H, CH, ATT>(p, r, beg, end, gl, ss, m, l, a);
 #pragma unroll
   for (int h = 0; h < H; ++h)
     st4(p.out + r * p.ldo + h * O + 4 * gl,
@@ -318,19 +431,32 @@ struct GatSplit {
   const int64_t* heavy_seg_ptr;
   int64_t n_heavy;
   float* work;  // [n_seg][F] acc | [n_seg][H] m | [n_seg][H] l
+  // ATT entry point (ABI 10): the segment arrays may be in any order (e.g. sorted by their
+  // first column, so that segments of different heavy rows over the same columns run
+  // together and share the gathered lines in L2); seg_pos[j] = position of the j-th segment
+  // in heavy_seg_ptr's row-grouped numbering (NULL: identity)
+  const int64_t* seg_pos;
+  int xcd_blocks;   // > 0: grid padded to 8 * xcd_blocks; XCD x runs logical blocks
+                    // [x * xcd_blocks, (x + 1) * xcd_blocks): a contiguous stretch of segments
 };
 
-template <int F>
+// logical block of a partial kernel (blocks are dealt round-robin to the 8 XCDs)
+__device__ __forceinline__ int64_t split_block(const GatSplit& sp) {
+  const int64_t b = blockIdx.x;
+  return sp.xcd_blocks > 0 ? (b % 8) * sp.xcd_blocks + b / 8 : b;
+}
+
+template <int F, bool ATT>
 __global__ __launch_bounds__(kBlock) void gat_partial_kernel(GatParams p, GatSplit sp) {
   constexpr int GROUP = F / 4;
   constexpr int RPW = 64 / GROUP;
   const int lane = threadIdx.x & 63;
   const int gl = lane % GROUP;
-  const int64_t sg = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
+  const int64_t sg = (split_block(sp) * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
   if (sg >= sp.n_seg) return;
   float m = -INFINITY, l = 0.f;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  gat_accumulate<GROUP>(p, sp.seg_row[sg], sp.seg_beg[sg], sp.seg_end[sg], gl, m, l, a);
+  gat_accumulate<GROUP, ATT>(p, sp.seg_row[sg], sp.seg_beg[sg], sp.seg_end[sg], gl, m, l, a);
   st4(sp.work + sg * F + 4 * gl, a);
   const int hl = p.o_dim / 4;
   if (gl % hl == 0) {
@@ -343,25 +469,25 @@ __global__ __launch_bounds__(kBlock) void gat_partial_kernel(GatParams p, GatSpl
 // Heavy rows, pass 1 in shared-row mode: O/4 lanes per segment load each neighbour's x row
 // ONCE for all H heads (gat_partial_kernel<H*O> would load it H times, one head per lane
 // group); the partials have gat_partial_kernel's layout, so gat_merge_kernel<H*O> finishes.
-template <int O, int H, int CH>
+template <int O, int H, int CH, bool ATT>
 __global__ __launch_bounds__(kBlock) void gat_shared_partial_kernel(GatParams p, GatSplit sp) {
   constexpr int GROUP = O / 4;
   constexpr int RPW = 64 / GROUP;
   const int lane = threadIdx.x & 63;
   const int gl = lane % GROUP;
-  const int64_t sg = ((int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
+  const int64_t sg = (split_block(sp) * (kBlock / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
   if (sg >= sp.n_seg) return;
   const int64_t r = sp.seg_row[sg];
   float ss[H], m[H], l[H];
   float4 a[H];
+  shared_self_scores<O, H, ATT>(p, r, gl, ss);
 #pragma unroll
   for (int h = 0; h < H; ++h) {
-    ss[h] = p.s_self[r * p.ld_ss + h];
     m[h] = -INFINITY;
     l[h] = 0.f;
     a[h] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
-  gat_shared_range<O, H, CH>(p, r, sp.seg_beg[sg], sp.seg_end[sg], gl, ss, m, l, a);
+  gat_shared_range<O, H, CH, ATT>(p, r, sp.seg_beg[sg], sp.seg_end[sg], gl, ss, m, l, a);
   float* ml = sp.work + sp.n_seg * (H * O);
 #pragma unroll
   for (int h = 0; h < H; ++h) {
@@ -390,10 +516,14 @@ __global__ __launch_bounds__(kBlock) void gat_merge_kernel(GatParams p, GatSplit
   const float* ll = mm + sp.n_seg * p.heads;
   const int64_t s0 = sp.heavy_seg_ptr[h], s1 = sp.heavy_seg_ptr[h + 1];
   float M = -INFINITY;
-  for (int64_t s = s0 + g; s < s1; s += NG) M = fmaxf(M, mm[s * p.heads + head]);
+  for (int64_t j = s0 + g; j < s1; j += NG) {
+    const int64_t s = sp.seg_pos ? sp.seg_pos[j] : j;
+    M = fmaxf(M, mm[s * p.heads + head]);
+  }
   float L = 0.f;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int64_t s = s0 + g; s < s1; s += NG) {
+  for (int64_t j = s0 + g; j < s1; j += NG) {
+    const int64_t s = sp.seg_pos ? sp.seg_pos[j] : j;
     const float w = gat_exp2(mm[s * p.heads + head] - M);   // base-2 maxima (gat_block)
     const float4 t = ld4(sp.work + s * F + 4 * gl);
     L = __builtin_fmaf(ll[s * p.heads + head], w, L);
@@ -426,6 +556,120 @@ __global__ __launch_bounds__(kBlock) void gat_merge_kernel(GatParams p, GatSplit
 
 using namespace gnnrec;
 
+namespace {
+
+// checks shared by both score forms; fills the epilogue part of GatParams
+int gat_check_common(int64_t n_rows, int32_t heads, int32_t o_dim, const float* hfeat, int64_t ldh,
+                     int64_t head_stride, int32_t mean_heads, float* out, int64_t ldo, int32_t epi,
+                     const float* self, int64_t ld_self, float* acc, int64_t ld_acc) {
+  GNNREC_REQUIRE(n_rows >= 0 && heads >= 1 && o_dim >= 4 && o_dim % 4 == 0, "gat: bad sizes");
+  const int F = heads * o_dim;
+  const int width = mean_heads ? o_dim : F;
+  GNNREC_REQUIRE(head_stride >= 0 && !(head_stride & 3), "gat: head_stride must be >= 0 and %% 4 == 0");
+  GNNREC_REQUIRE(hfeat && aligned16(hfeat) && !(ldh & 3) && ldh >= (heads - 1) * head_stride + o_dim,
+                 "gat: hfeat must be 16-B aligned, ld %% 4 == 0, ld >= (heads-1)*head_stride + o_dim");
+  GNNREC_REQUIRE((epi & GNNREC_EPI_NO_Y) || (out && aligned16(out) && !(ldo & 3) && ldo >= width),
+                 "gat: bad out");
+  GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_INIT) || (self && aligned16(self) && !(ld_self & 3) && ld_self >= width),
+                 "gat: ACC_INIT needs 16-B aligned self rows");
+  GNNREC_REQUIRE(!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) ||
+                     (acc && aligned16(acc) && !(ld_acc & 3) && ld_acc >= width),
+                 "gat: ACC needs 16-B aligned acc");
+  return GNNREC_OK;
+}
+
+// ATT form: scores from the rows (o_dim <= 64: a head's dot spans at most a 16-lane DPP row)
+int gat_check_att(const float* att, const float* hself, int64_t ld_hself, int64_t ldh,
+                  int32_t o_dim) {
+  GNNREC_REQUIRE(att && aligned16(att), "gat_att: att must be a 16-B aligned [2][heads][o_dim] array");
+  GNNREC_REQUIRE(hself && aligned16(hself) && !(ld_hself & 3),
+                 "gat_att: hself must be 16-B aligned with ld %% 4 == 0");
+  GNNREC_REQUIRE(o_dim <= 64 && ((o_dim / 4) & (o_dim / 4 - 1)) == 0,
+                 "gat_att: o_dim must be 4, 8, 16, 32 or 64 (got %d)", (int)o_dim);
+  (void)ldh;
+  return GNNREC_OK;
+}
+
+template <bool ATT>
+int gat_aggregate_launch(const GatParams& p, int64_t n_rows, int heads, int o_dim, int mean_heads,
+                         int apply_elu, int epi, const float* s_neigh, int64_t ld_sn,
+                         hipStream_t s) {
+  const int F = heads * o_dim;
+  auto grid = [&](int f) { return dim3((unsigned)ceil_div(n_rows, (64 / (f / 4)) * (kBlock / 64))); };
+  const bool shared_fast = p.head_stride == 0 && heads == 4 && !mean_heads && !apply_elu && epi == 0 &&
+                           (ATT ? o_dim == 64
+                                : ((o_dim == 16 || o_dim == 32 || o_dim == 64) && aligned16(s_neigh) &&
+                                   !(ld_sn & 3))) &&
+                           aligned16(p.out);
+  if (shared_fast) {
+    if constexpr (ATT) {
+      hipLaunchKernelGGL((gat_shared_kernel<64, 4, 8, true>), grid(64), dim3(kBlock), 0, s, p);
+    } else {
+      switch (o_dim) {
+        case 16: hipLaunchKernelGGL((gat_shared_kernel<16, 4, 8, false>), grid(16), dim3(kBlock), 0, s, p); break;
+        case 32: hipLaunchKernelGGL((gat_shared_kernel<32, 4, 8, false>), grid(32), dim3(kBlock), 0, s, p); break;
+        default: hipLaunchKernelGGL((gat_shared_kernel<64, 4, 8, false>), grid(64), dim3(kBlock), 0, s, p); break;
+      }
+    }
+    return check_launch("gat_aggregate (shared rows)");
+  }
+  switch (F) {
+    case 16: hipLaunchKernelGGL((gat_kernel<16, ATT>), grid(16), dim3(kBlock), 0, s, p); break;
+    case 32: hipLaunchKernelGGL((gat_kernel<32, ATT>), grid(32), dim3(kBlock), 0, s, p); break;
+    case 64: hipLaunchKernelGGL((gat_kernel<64, ATT>), grid(64), dim3(kBlock), 0, s, p); break;
+    case 128: hipLaunchKernelGGL((gat_kernel<128, ATT>), grid(128), dim3(kBlock), 0, s, p); break;
+    case 256: hipLaunchKernelGGL((gat_kernel<256, ATT>), grid(256), dim3(kBlock), 0, s, p); break;
+    default: set_error("gat: heads*o_dim = %d unsupported (16..256, power of two)", F); return GNNREC_EUNSUPPORTED;
+  }
+  return check_launch("gat_aggregate");
+}
+
+template <bool ATT>
+int gat_heavy_launch(const GatParams& p, const GatSplit& sp, int heads, int o_dim,
+                     const float* s_neigh, int64_t ld_sn, hipStream_t s) {
+  const int F = heads * o_dim;
+  auto g = [&](int64_t n, int f) {
+    const int64_t nb = ceil_div(n, (64 / (f / 4)) * (kBlock / 64));
+    return dim3((unsigned)(sp.xcd_blocks > 0 ? 8 * ceil_div(nb, 8) : nb));
+  };
+  const bool shared = p.head_stride == 0 && heads == 4 &&
+                      (ATT ? o_dim == 64
+                           : ((o_dim == 16 || o_dim == 32 || o_dim == 64) && aligned16(s_neigh) &&
+                              !(ld_sn & 3)));
+  if (shared) {
+    // shared rows: one x load per neighbour for the 4 heads, then the generic merge
+    if constexpr (ATT) {
+      hipLaunchKernelGGL((gat_shared_partial_kernel<64, 4, 8, true>), g(sp.n_seg, 64), dim3(kBlock), 0, s, p, sp);
+      hipLaunchKernelGGL(gat_merge_kernel<256>, dim3((unsigned)sp.n_heavy), dim3(kBlock), 0, s, p, sp);
+    } else {
+      switch (o_dim) {
+#define GAT_SHARED_HEAVY(OO)                                                                        \
+  case OO:                                                                                          \
+    hipLaunchKernelGGL((gat_shared_partial_kernel<OO, 4, 8, false>), g(sp.n_seg, OO), dim3(kBlock), 0, \
+                       s, p, sp);                                                                   \
+    hipLaunchKernelGGL(gat_merge_kernel<4 * OO>, dim3((unsigned)sp.n_heavy), dim3(kBlock), 0, s, p, sp); \
+    break;
+        GAT_SHARED_HEAVY(16) GAT_SHARED_HEAVY(32) GAT_SHARED_HEAVY(64)
+#undef GAT_SHARED_HEAVY
+      }
+    }
+    return check_launch("gat_heavy (shared rows)");
+  }
+  switch (F) {
+#define GAT_HEAVY(FF)                                                                               \
+  case FF:                                                                                          \
+    hipLaunchKernelGGL((gat_partial_kernel<FF, ATT>), g(sp.n_seg, FF), dim3(kBlock), 0, s, p, sp);  \
+    hipLaunchKernelGGL(gat_merge_kernel<FF>, dim3((unsigned)sp.n_heavy), dim3(kBlock), 0, s, p, sp); \
+    break;
+    GAT_HEAVY(16) GAT_HEAVY(32) GAT_HEAVY(64) GAT_HEAVY(128) GAT_HEAVY(256)
+#undef GAT_HEAVY
+    default: set_error("gat_heavy: heads*o_dim = %d unsupported", F); return GNNREC_EUNSUPPORTED;
+  }
+  return check_launch("gat_heavy");
+}
+
+}  // namespace
+
 extern "C" int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* col, int64_t n_rows,
                                         const float* hfeat, int64_t ldh, int64_t head_stride,
                                         const float* s_self, const float* s_neigh, int64_t ld_ss,
@@ -435,46 +679,39 @@ extern "C" int gnnrec_gat_aggregate_f32(const int64_t* row_ptr, const int32_t* c
                                         float* out, int64_t ldo, int32_t epi, const float* self,
                                         int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
                                         int64_t max_row_len, gnnrec_stream_t stream) {
-  GNNREC_REQUIRE(n_rows >= 0 && heads >= 1 && o_dim >= 4 && o_dim % 4 == 0, "gat: bad sizes");
+  if (int st = gat_check_common(n_rows, heads, o_dim, hfeat, ldh, head_stride, mean_heads, out, ldo,
+                                epi, self, ld_self, acc, ld_acc))
+    return st;
   if (n_rows == 0) return GNNREC_OK;
-  const int F = heads * o_dim;
-  const int width = mean_heads ? o_dim : F;
-  GNNREC_REQUIRE(row_ptr && col && hfeat && s_self && s_neigh, "gat: null operand");
+  GNNREC_REQUIRE(row_ptr && col && s_self && s_neigh, "gat: null operand");
   GNNREC_REQUIRE(ld_ss >= heads && ld_sn >= heads, "gat: score row strides must be >= heads");
-  GNNREC_REQUIRE(head_stride >= 0 && !(head_stride & 3), "gat: head_stride must be >= 0 and %% 4 == 0");
-  GNNREC_REQUIRE(aligned16(hfeat) && !(ldh & 3) && ldh >= (heads - 1) * head_stride + o_dim,
-                 "gat: hfeat must be 16-B aligned, ld %% 4 == 0, ld >= (heads-1)*head_stride + o_dim");
-  GNNREC_REQUIRE((epi & GNNREC_EPI_NO_Y) || (out && aligned16(out) && !(ldo & 3) && ldo >= width),
-                 "gat: bad out");
-  GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_INIT) || (self && aligned16(self) && !(ld_self & 3) && ld_self >= width),
-                 "gat: ACC_INIT needs 16-B aligned self rows");
-  GNNREC_REQUIRE(!(epi & (GNNREC_EPI_ACC_INIT | GNNREC_EPI_ACC_ADD)) ||
-                     (acc && aligned16(acc) && !(ld_acc & 3) && ld_acc >= width),
-                 "gat: ACC needs 16-B aligned acc");
   GatParams p{Csr{row_ptr, col, nullptr, n_rows}, hfeat, ldh, head_stride, s_self, s_neigh, ld_ss, ld_sn, heads, o_dim, slope,
-              mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, max_row_len};
-  hipStream_t s = as_hip(stream);
-  auto grid = [&](int f) { return dim3((unsigned)ceil_div(n_rows, (64 / (f / 4)) * (kBlock / 64))); };
-  const bool shared_fast = head_stride == 0 && heads == 4 && !mean_heads && !apply_elu && epi == 0 &&
-                           (o_dim == 16 || o_dim == 32 || o_dim == 64) && aligned16(s_neigh) && !(ld_sn & 3) &&
-                           aligned16(out);
-  if (shared_fast) {
-    switch (o_dim) {
-      case 16: hipLaunchKernelGGL((gat_shared_kernel<16, 4, 8>), grid(16), dim3(kBlock), 0, s, p); break;
-      case 32: hipLaunchKernelGGL((gat_shared_kernel<32, 4, 8>), grid(32), dim3(kBlock), 0, s, p); break;
-      default: hipLaunchKernelGGL((gat_shared_kernel<64, 4, 8>), grid(64), dim3(kBlock), 0, s, p); break;
-    }
-    return check_launch("gat_aggregate (shared rows)");
-  }
-  switch (F) {
-    case 16: hipLaunchKernelGGL(gat_kernel<16>, grid(16), dim3(kBlock), 0, s, p); break;
-    case 32: hipLaunchKernelGGL(gat_kernel<32>, grid(32), dim3(kBlock), 0, s, p); break;
-    case 64: hipLaunchKernelGGL(gat_kernel<64>, grid(64), dim3(kBlock), 0, s, p); break;
-    case 128: hipLaunchKernelGGL(gat_kernel<128>, grid(128), dim3(kBlock), 0, s, p); break;
-    case 256: hipLaunchKernelGGL(gat_kernel<256>, grid(256), dim3(kBlock), 0, s, p); break;
-    default: set_error("gat: heads*o_dim = %d unsupported (16..256, power of two)", F); return GNNREC_EUNSUPPORTED;
-  }
-  return check_launch("gat_aggregate");
+              mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, max_row_len,
+              nullptr, nullptr, 0};
+  return gat_aggregate_launch<false>(p, n_rows, heads, o_dim, mean_heads, apply_elu, epi, s_neigh,
+                                     ld_sn, as_hip(stream));
+}
+
+extern "C" int gnnrec_gat_aggregate_att_f32(const int64_t* row_ptr, const int32_t* col,
+                                            int64_t n_rows, const float* hfeat, int64_t ldh,
+                                            int64_t head_stride, const float* hself,
+                                            int64_t ld_hself, const float* att, int32_t heads,
+                                            int32_t o_dim, float slope, int32_t mean_heads,
+                                            int32_t apply_elu, float* out, int64_t ldo, int32_t epi,
+                                            const float* self, int64_t ld_self, float* acc,
+                                            int64_t ld_acc, float acc_div, int64_t max_row_len,
+                                            gnnrec_stream_t stream) {
+  if (int st = gat_check_common(n_rows, heads, o_dim, hfeat, ldh, head_stride, mean_heads, out, ldo,
+                                epi, self, ld_self, acc, ld_acc))
+    return st;
+  if (n_rows == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(row_ptr && col, "gat_att: null operand");
+  if (int st = gat_check_att(att, hself, ld_hself, ldh, o_dim)) return st;
+  GatParams p{Csr{row_ptr, col, nullptr, n_rows}, hfeat, ldh, head_stride, nullptr, nullptr, 0, 0, heads, o_dim, slope,
+              mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, max_row_len,
+              att, hself, ld_hself};
+  return gat_aggregate_launch<true>(p, n_rows, heads, o_dim, mean_heads, apply_elu, epi, nullptr, 0,
+                                    as_hip(stream));
 }
 
 extern "C" int gnnrec_gat_heavy_f32(const int32_t* col, const int64_t* seg_row,
@@ -495,37 +732,45 @@ extern "C" int gnnrec_gat_heavy_f32(const int32_t* col, const int64_t* seg_row,
                      head_stride >= 0 && !(head_stride & 3),
                  "gat_heavy: null or misaligned operand");
   GNNREC_REQUIRE(ld_ss >= heads && ld_sn >= heads, "gat_heavy: score row strides must be >= heads");
-  const int F = heads * o_dim;
   GatParams p{Csr{nullptr, col, nullptr, 0}, hfeat, ldh, head_stride, s_self, s_neigh, ld_ss, ld_sn, heads, o_dim, slope,
-              mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, 0};
-  GatSplit sp{seg_row, seg_beg, seg_end, n_seg, heavy_rows, heavy_seg_ptr, n_heavy, work};
-  hipStream_t s = as_hip(stream);
-  auto g = [&](int64_t n, int f) { return dim3((unsigned)ceil_div(n, (64 / (f / 4)) * (kBlock / 64))); };
-  if (head_stride == 0 && heads == 4 && (o_dim == 16 || o_dim == 32 || o_dim == 64) &&
-      aligned16(s_neigh) && !(ld_sn & 3)) {
-    // shared rows: one x load per neighbour for the 4 heads, then the generic merge
-    switch (o_dim) {
-#define GAT_SHARED_HEAVY(OO)                                                                   \
-  case OO:                                                                                     \
-    hipLaunchKernelGGL((gat_shared_partial_kernel<OO, 4, 8>), g(n_seg, OO), dim3(kBlock), 0, s, \
-                       p, sp);                                                                 \
-    hipLaunchKernelGGL(gat_merge_kernel<4 * OO>, dim3((unsigned)n_heavy), dim3(kBlock), 0, s, \
-                       p, sp);                                                                 \
-    break;
-      GAT_SHARED_HEAVY(16) GAT_SHARED_HEAVY(32) GAT_SHARED_HEAVY(64)
-#undef GAT_SHARED_HEAVY
-    }
-    return check_launch("gat_heavy (shared rows)");
+              mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, 0,
+              nullptr, nullptr, 0};
+  GatSplit sp{seg_row, seg_beg, seg_end, n_seg, heavy_rows, heavy_seg_ptr, n_heavy, work,
+              nullptr, 0};
+  return gat_heavy_launch<false>(p, sp, heads, o_dim, s_neigh, ld_sn, as_hip(stream));
+}
+
+extern "C" int gnnrec_gat_heavy_att_f32(const int32_t* col, const int64_t* seg_row,
+                                        const int64_t* seg_beg, const int64_t* seg_end,
+                                        int64_t n_seg, const int64_t* heavy_rows,
+                                        const int64_t* heavy_seg_ptr, int64_t n_heavy, float* work,
+                                        const float* hfeat, int64_t ldh, int64_t head_stride,
+                                        const float* hself, int64_t ld_hself, const float* att,
+                                        int32_t heads, int32_t o_dim, float slope,
+                                        int32_t mean_heads, int32_t apply_elu, float* out,
+                                        int64_t ldo, int32_t epi, const float* self,
+                                        int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
+                                        const int64_t* seg_pos, int32_t xcd_order,
+                                        gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(n_seg >= 0 && n_heavy >= 0 && heads >= 1 && o_dim >= 4 && o_dim % 4 == 0,
+                 "gat_heavy_att: bad sizes");
+  if (n_heavy == 0) return GNNREC_OK;
+  GNNREC_REQUIRE(col && seg_row && seg_beg && seg_end && heavy_rows && heavy_seg_ptr && work &&
+                     hfeat && aligned16(work) && aligned16(hfeat) && !(ldh & 3) &&
+                     head_stride >= 0 && !(head_stride & 3),
+                 "gat_heavy_att: null or misaligned operand");
+  if (int st = gat_check_att(att, hself, ld_hself, ldh, o_dim)) return st;
+  GatParams p{Csr{nullptr, col, nullptr, 0}, hfeat, ldh, head_stride, nullptr, nullptr, 0, 0, heads, o_dim, slope,
+              mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, 0,
+              att, hself, ld_hself};
+  // xcd_blocks: logical blocks per XCD of the partial kernel's grid (16 segment lanes groups
+  // per block at o_dim <= 64 rows of 64 floats; the kernel derives its own geometry)
+  int64_t xb = 0;
+  if (xcd_order) {
+    const int f = (head_stride == 0 && heads == 4 && o_dim == 64) ? 64 : heads * o_dim;
+    xb = ceil_div(ceil_div(n_seg, (64 / (f / 4)) * (kBlock / 64)), 8);
   }
-  switch (F) {
-#define GAT_HEAVY(FF)                                                                          \
-  case FF:                                                                                     \
-    hipLaunchKernelGGL(gat_partial_kernel<FF>, g(n_seg, FF), dim3(kBlock), 0, s, p, sp);       \
-    hipLaunchKernelGGL(gat_merge_kernel<FF>, dim3((unsigned)n_heavy), dim3(kBlock), 0, s, p, sp); \
-    break;
-    GAT_HEAVY(16) GAT_HEAVY(32) GAT_HEAVY(64) GAT_HEAVY(128) GAT_HEAVY(256)
-#undef GAT_HEAVY
-    default: set_error("gat_heavy: heads*o_dim = %d unsupported", F); return GNNREC_EUNSUPPORTED;
-  }
-  return check_launch("gat_heavy");
+  GatSplit sp{seg_row, seg_beg, seg_end, n_seg, heavy_rows, heavy_seg_ptr, n_heavy, work,
+              seg_pos, (int)xb};
+  return gat_heavy_launch<true>(p, sp, heads, o_dim, nullptr, 0, as_hip(stream));
 }

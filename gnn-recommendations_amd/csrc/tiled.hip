@@ -551,7 +551,14 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     const int64_t b = wptr[s], e = (GNNREC_TILED_EXP & 32) ? b : wptr[s + 1];
     int cur = 0;
     f4 sink = {0.f, 0.f, 0.f, 0.f};   // diagnostic builds only (GNNREC_TILED_EXP & 1)
-    if (kQuad && b < e) {
+    if (kQuad && b < e && (b & 3)) {
+      // a chunk-major plan passed to a quad build: the quads would straddle waves' ranges.
+      // Flag it (the caller checks GNNREC_TILED_SYNC_ERR_WORD after the launch) and leave the
+      // rows untouched instead of computing garbage.
+      if (lane == 0)
+        __hip_atomic_fetch_or(sync + GNNREC_TILED_SYNC_ERR_WORD, 1u, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+    } else if (kQuad && b < e) {
       // quad layout: a ring of 3 quads (12 chunks) and kGatherAhead + 1 gathered chunks; stage
       // c (c % 4 == 0) loads quad c / 4 + 2, every stage gathers chunk c + kGatherAhead and
       // applies chunk c (wave ranges start on a quad, so c % 4 is the unrolled stage's)
@@ -594,6 +601,9 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
         return ++c >= nc;
       };
       static_assert(12 % kXRing == 0, "quad ring: 12 stages cover the gather ring");
+      // stage 4k loads quad k + 2, so at stage I the ring holds the chunks up to
+      // 4 (I / 4) + 11: the chunk I + kGatherAhead it gathers is loaded for kGatherAhead <= 8
+      static_assert(kGatherAhead <= 8, "quad ring: gathers at most 8 chunks ahead");
       run_ring(std::make_integer_sequence<int, 12>{}, stage);
     } else if (b < e) {
       // a ring of kPlanAhead + 1 slot sets and kGatherAhead + 1 gathered chunks: stage c loads

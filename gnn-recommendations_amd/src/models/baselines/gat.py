@@ -11,6 +11,7 @@ and creation order. Semantics difference, documented: an isolated node yields a 
 for that node only (softmax over an empty set); the reference's dense matmul spreads that
 NaN to every node.
 """
+import os
 import warnings
 from typing import Optional, Tuple
 
@@ -23,26 +24,76 @@ from ... import ops
 from ...ops._lib import EPI_ACC_ADD, EPI_ACC_DIV, EPI_ACC_INIT, EPI_NO_Y
 from ...ops.graph import CsrGraph
 
-# The reference's dense path (gat.py:99-141) holds an [N, N] mask plus, per head, [N, N]
-# scores and attention: ~16 N^2 bytes at once (N = 20 000: 6.4 GB). The native kernel has no
-# backward, so a native operand with autograd on (GAT training) or with dropout in training
-# mode falls back to that path only up to this many nodes and raises above it — never a
-# silent O(N^2) allocation on a large graph.
-GAT_DENSE_MAX_NODES = 20_000
+# The reference's dense path (gat.py:99-141) holds an [N, N] fp32 mask plus, per head, [N, N]
+# scores, their masked copy and the attention matrix; with autograd on, every head's [N, N]
+# intermediates stay alive for the backward. A native operand that the sparse kernel cannot
+# take (autograd on with parameters that require grad, attention dropout in training mode, a
+# width without a kernel instance) runs that path only when its estimated footprint fits the
+# device's free memory (a 288 GB MI355X holds it up to N ~ 8e4 for inference), and raises
+# otherwise — never an allocation that is known not to fit. GNNREC_GAT_DENSE_MAX_NODES=<n>
+# (or setting GAT_DENSE_MAX_NODES here) replaces the memory test with a fixed node cap.
+GAT_DENSE_MAX_NODES = None
+
+# Native layers form the attention scores in the kernel from the rows it gathers
+# (gnnrec_gat_aggregate_att_f32) instead of reading projected score tables per neighbour
+# (DESIGN §3.4, round 5); False keeps the score-table kernels (A/B and tests).
+GAT_SCORES_FROM_ROWS = os.environ.get("GNNREC_GAT_SCORES_FROM_ROWS", "1") != "0"
+DENSE_FALLBACK_MEM_FRACTION = 0.9
 
 
-def check_dense_fallback(n_nodes: int, why: str) -> None:
-    """Refuse (RuntimeError) the dense masked-softmax path for a native operand of more than
-    GAT_DENSE_MAX_NODES nodes; warn below it. `why` says what ruled the native kernel out."""
-    if n_nodes > GAT_DENSE_MAX_NODES:
+def dense_fallback_bytes(n_nodes: int, heads: int, grad: bool) -> int:
+    """Peak bytes of the reference's dense masked softmax for one layer: the [N, N] mask plus
+    three [N, N] per-head intermediates (scores, masked scores, attention), all heads' kept
+    alive when autograd records them."""
+    nn2 = 4 * int(n_nodes) * int(n_nodes)
+    return nn2 * (1 + 3 * (max(1, int(heads)) if grad else 1))
+
+
+def _available_bytes(device) -> int:
+    if device is not None and torch.device(device).type == "cuda":
+        free, _ = torch.cuda.mem_get_info(device)
+        # blocks torch's caching allocator holds but does not use are free for this path too
+        cached = torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device)
+        return int(free + max(0, cached))
+    try:
+        import psutil
+        return int(psutil.virtual_memory().available)
+    except Exception:  # noqa: BLE001
+        return 1 << 62
+
+
+def _node_cap():
+    env = os.environ.get("GNNREC_GAT_DENSE_MAX_NODES")
+    if env:
+        return int(env)
+    return GAT_DENSE_MAX_NODES
+
+
+def check_dense_fallback(n_nodes: int, why: str, heads: int = 1, grad: bool = False,
+                         device=None) -> None:
+    """Refuse (RuntimeError) the dense masked-softmax path for a native operand when its
+    estimated footprint (dense_fallback_bytes) exceeds DENSE_FALLBACK_MEM_FRACTION of the
+    device's available memory, or when N exceeds a configured node cap
+    (GNNREC_GAT_DENSE_MAX_NODES / GAT_DENSE_MAX_NODES); warn otherwise. `why` says what
+    ruled the native kernel out."""
+    need = dense_fallback_bytes(n_nodes, heads, grad)
+    cap = _node_cap()
+    if cap is not None:
+        refuse = n_nodes > cap
+        limit = f"the node cap GNNREC_GAT_DENSE_MAX_NODES = {cap}"
+    else:
+        avail = _available_bytes(device)
+        refuse = need > DENSE_FALLBACK_MEM_FRACTION * avail
+        limit = (f"{DENSE_FALLBACK_MEM_FRACTION:.0%} of the {avail / 1e9:.1f} GB available "
+                 f"(GNNREC_GAT_DENSE_MAX_NODES sets a node cap instead)")
+    if refuse:
         raise RuntimeError(
             f"GATLayer: the native sparse kernel does not apply ({why}) and the reference's "
-            f"dense [N, N] softmax path would allocate O(N^2) memory for N = {n_nodes} "
-            f"(> GAT_DENSE_MAX_NODES = {GAT_DENSE_MAX_NODES}). GAT on the native path is "
-            f"inference-only: run the forward under torch.no_grad() / eval(), or train on a "
-            f"graph of at most {GAT_DENSE_MAX_NODES} nodes.")
+            f"dense [N, N] softmax path would need ~{need / 1e9:.1f} GB for N = {n_nodes} "
+            f"({heads} heads, autograd {'on' if grad else 'off'}), above {limit}. Run the "
+            f"forward under torch.no_grad() / eval(), or on a smaller graph.")
     warnings.warn(f"GATLayer: dense O(N^2) reference path on a native operand "
-                  f"(N = {n_nodes}; {why})", RuntimeWarning, stacklevel=3)
+                  f"(N = {n_nodes}, ~{need / 1e9:.2f} GB; {why})", RuntimeWarning, stacklevel=3)
 
 
 class GATLayer(nn.Module):
@@ -128,6 +179,78 @@ class GATLayer(nn.Module):
         """[H*in, out] = vstack(W_h^T) / H: z (per-head aggregates of x) @ this = the head mean."""
         return torch.cat([w.weight.t() for w in self.W], dim=0) / self.n_heads
 
+    # ---- scores from the rows (gnnrec_gat_aggregate_att_f32): the projection writes h only --
+    def att_dim(self) -> int:
+        """Width of the row a head's scores are dotted with: in_dim (shared rows) or out_dim."""
+        return self.in_dim if self.shares_input() else self.out_dim
+
+    def att_ok(self) -> bool:
+        """The ATT kernels take this layer (and GAT_SCORES_FROM_ROWS is on)."""
+        return GAT_SCORES_FROM_ROWS and ops.functional.gat_att_supported(self.att_dim())
+
+    def att_vectors(self) -> torch.Tensor:
+        """[2, H, w]: the self / neighbour attention vectors the kernel dots rows with —
+        a_self_h, a_neigh_h (w = out_dim, against h_h = W_h x), or for shared rows the row
+        vectors a_h^T W_h (w = in_dim, against x itself). Cached until a parameter changes."""
+        from ..orthogonal_bundle.group_shuffle_layer import param_key
+        params = list(self.W.parameters()) + list(self.a_self) + list(self.a_neigh)
+        key = param_key(params)
+        if getattr(self, "_att_key", None) == key:
+            return self._att
+        with torch.no_grad():
+            if self.shares_input():
+                vs = [a[:, 0] @ w.weight for a, w in zip(self.a_self, self.W)]
+                vn = [a[:, 0] @ w.weight for a, w in zip(self.a_neigh, self.W)]
+            else:
+                vs = [a[:, 0] for a in self.a_self]
+                vn = [a[:, 0] for a in self.a_neigh]
+            att = torch.stack([torch.stack(vs), torch.stack(vn)]).float().contiguous()
+        self._att, self._att_key = att, key
+        return att
+
+    def head_weight(self) -> torch.Tensor:
+        """[H*o, in]: the stacked head projections (h = x @ this^T)."""
+        from ..orthogonal_bundle.group_shuffle_layer import param_key
+        params = list(self.W.parameters())
+        key = param_key(params)
+        if getattr(self, "_hw_key", None) == key:
+            return self._hw
+        with torch.no_grad():
+            w = torch.cat([w.weight for w in self.W], dim=0).float().contiguous()
+        self._hw, self._hw_key = w, key
+        return w
+
+    def native_rows(self, x: torch.Tensor) -> torch.Tensor:
+        """The table the ATT aggregation gathers for the rows of x: x itself (shared rows), or
+        h = [W_0 x | ... | W_H x] written by the row GEMM into a gather-placed table
+        (functional.hop_table: aligned rows, no line at the slow offset)."""
+        if self.shares_input():
+            return x
+        w = self.head_weight()
+        ho = w.shape[0]
+        if x.is_cuda and ops.functional.rows_gemm_supported(x.shape[1], ho):
+            if not ops.functional._rows_view_ok(x):
+                x = x.contiguous()
+            out = ops.functional.hop_table(x.shape[0], ho, device=x.device)
+            ops.functional.rows_gemm(x, w.t(), out=out)
+            return out
+        return x @ w.t()
+
+    def native_forward_att(self, a, feat, hself, *, apply_elu: bool = False, epi: int = 0,
+                           self_rows=None, acc=None, acc_div: float = 1.0) -> torch.Tensor:
+        """The native layer from native_rows: `feat` the gathered table (maybe exchanged),
+        `hself` the destination rows' own rows of it."""
+        att = self.att_vectors().to(feat.device)
+        if not self.shares_input():
+            return ops.functional.gat_aggregate_att(
+                a, feat, hself, att, self.n_heads, self.out_dim, self.alpha,
+                mean_heads=not self.concat_heads, apply_elu=apply_elu, epi=epi,
+                self_rows=self_rows, acc=acc, acc_div=acc_div)
+        z = ops.functional.gat_aggregate_att(a, feat, hself, att, self.n_heads, self.in_dim,
+                                             self.alpha, shared_rows=True)
+        return ops.functional.rows_gemm(z, self.head_mean_weight(), apply_elu=apply_elu, epi=epi,
+                                        self_rows=self_rows, acc=acc, acc_div=acc_div)
+
     def native_inputs(self, x: torch.Tensor):
         """(table gathered per neighbour, s_self, s_neigh) for the rows of x."""
         if self.shares_input():
@@ -155,10 +278,16 @@ class GATLayer(nn.Module):
         a = ops.as_operand(adj_matrix)
         why = self.native_block(a)
         if why is None:
+            if self.att_ok():
+                feat = self.native_rows(x)
+                return self.native_forward_att(a, feat, feat, apply_elu=apply_elu, epi=epi,
+                                               self_rows=self_rows, acc=acc, acc_div=acc_div)
             return self.native_forward(a, *self.native_inputs(x), apply_elu=apply_elu, epi=epi,
                                        self_rows=self_rows, acc=acc, acc_div=acc_div)
         if isinstance(a, CsrGraph):
-            check_dense_fallback(a.shape[0], why)
+            grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+            check_dense_fallback(a.shape[0], why, heads=self.n_heads, grad=grad,
+                                 device=a.row_ptr.device)
         out = self._dense_forward(x, a)
         return F.elu(out) if apply_elu else out
 

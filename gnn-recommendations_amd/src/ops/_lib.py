@@ -17,7 +17,7 @@ import torch  # noqa: F401  (load order: torch's HIP runtime first)
 
 _PKG_ROOT = Path(__file__).resolve().parents[2]
 LIB_PATH = Path(os.environ.get("GNNREC_LIB", _PKG_ROOT / "lib" / "libgnnrec.so"))
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 # gnnrec.h epilogue flags
 EPI_ACC_INIT = 1
@@ -34,6 +34,7 @@ TILED_TAIL = 8
 TILED_QUAD_TAIL = 16
 TILED_MAX_ROWS = 1279
 TILED_SYNC_WORDS = 256
+TILED_SYNC_ERR_WORD = 1   # GNNREC_TILED_SYNC_ERR_WORD: a non-quad plan on a quad build
 TILED_HDR_WORDS = 4
 TILED_MAX_LDX = 1024
 TILED_MAX_PANEL = 1 << 20
@@ -97,6 +98,12 @@ _SIGNATURES = {
     "gnnrec_gat_heavy_f32": [_p, _p, _p, _p, _i64, _p, _p, _i64, _p, _p, _i64, _i64, _p, _p,
                              _i64, _i64, _i32, _i32, _f32, _i32, _i32, _p, _i64, _i32, _p, _i64,
                              _p, _i64, _f32, _p],
+    "gnnrec_gat_aggregate_att_f32": [_p, _p, _i64, _p, _i64, _i64, _p, _i64, _p, _i32, _i32,
+                                     _f32, _i32, _i32, _p, _i64, _i32, _p, _i64, _p, _i64, _f32,
+                                     _i64, _p],
+    "gnnrec_gat_heavy_att_f32": [_p, _p, _p, _p, _i64, _p, _p, _i64, _p, _p, _i64, _i64, _p,
+                                 _i64, _p, _i32, _i32, _f32, _i32, _i32, _p, _i64, _i32, _p, _i64,
+                                 _p, _i64, _f32, _p, _i32, _p],
     "gnnrec_score_topk_f32": [_p, _i64, _i64, _p, _i64, _i64, _i32, _p, _p, _i32, _p, _p, _p],
     "gnnrec_score_topk_split_f32": [_p, _i64, _i64, _p, _i64, _i64, _i32, _p, _p, _i32, _i32,
                                     _p, _p, _p, _p, _p],

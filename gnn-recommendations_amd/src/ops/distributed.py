@@ -285,13 +285,17 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
                             work: Optional[tuple] = None, overlap_chunks: int = 1,
                             masks: Optional[Callable] = None,
                             reserve_cus: int = 0,
-                            deferred: Optional[bool] = None) -> torch.Tensor:
+                            deferred: Optional[bool] = None,
+                            placed_output: bool = False) -> torch.Tensor:
     """LightGCN propagation over a row-sharded operand.
 
     x0_pad: [world*rows_pad, d] padded initial table (identical on every rank).
     Returns this rank's rows of mean(x0..xK) ([n_local, d]), or the full [N, d] table when
-    gather_output — on one rank with the deferred schedule a row-major view of a placed
-    table (functional.hop_table: row stride > d), not a contiguous tensor. `work` (from `make_work`) holds reusable hop buffers. With world == 1
+    gather_output, as a contiguous tensor. On one rank the deferred schedule forms the mean
+    in a placed table (functional.hop_table: row stride > d, twice the compact bytes);
+    placed_output=True returns that row-major strided view itself instead of a compact copy
+    (bench.py's timed step: the same values, without the extra 4*d*N-byte copy).
+    `work` (from `make_work`) holds reusable hop buffers. With world == 1
     the hop outputs feed the next hop directly (no gather, no copy).
     overlap_chunks > 1 (point-to-point exchange only): the hop runs in that many row chunks
     and each chunk's transfer is posted as soon as its kernel is queued, so the exchange of
@@ -331,8 +335,9 @@ def lightgcn_propagate_dist(dg: DistributedGraph, x0_pad: torch.Tensor, n_layers
     if deferred is None:
         deferred = native and tiled_plan_for(dg.shard, x0_pad) is not None
     if deferred and n_layers >= 2 and (n_layers <= 3 or not chunked):
-        return _propagate_deferred(dg, x0_pad, n_layers, hop, mkw, work, self_rows, chunked,
-                                   overlap_chunks, chunk_kw, masks, gather_output)
+        out = _propagate_deferred(dg, x0_pad, n_layers, hop, mkw, work, self_rows, chunked,
+                                  overlap_chunks, chunk_kw, masks, gather_output)
+        return out if placed_output else out.contiguous()
     acc = torch.empty((dg.n_local, d), dtype=torch.float32, device=x0_pad.device)
     if n_layers == 0:
         acc.copy_(self_rows)
@@ -540,13 +545,21 @@ def gat_forward_dist(dg: DistributedGraph, model, x0_pad: torch.Tensor, *,
     acc = torch.empty_like(x_local)
     L = len(model.layers)
     for k, layer in enumerate(model.layers, start=1):
+        epi = EPI_ACC_INIT if k == 1 else EPI_ACC_ADD
+        if k == L:
+            epi |= EPI_ACC_DIV | EPI_NO_Y   # only the layer mean is read after it
+        if layer_fn is _native_gat_layer and layer.att_ok():
+            # scores from the rows: only the gathered table travels (no score columns), and
+            # the destination rows' own scores come from this rank's rows of it
+            feat = layer.native_rows(x_local)
+            x_local = layer.native_forward_att(dg.shard, _exchanged(dg, feat), feat,
+                                               apply_elu=True, epi=epi, self_rows=x_local,
+                                               acc=acc, acc_div=float(L + 1))
+            continue
         feat, ss, sn = layer.native_inputs(x_local)
         # scores travel as their (strided) projection columns: no compaction copy, and on one
         # device the kernel reads them next to the gathered rows
         featp, snp = _exchanged(dg, feat), _exchanged(dg, sn)
-        epi = EPI_ACC_INIT if k == 1 else EPI_ACC_ADD
-        if k == L:
-            epi |= EPI_ACC_DIV | EPI_NO_Y   # only the layer mean is read after it
         x_local = layer_fn(dg.shard, featp, ss, snp, layer, apply_elu=True, epi=epi,
                            self_rows=x_local, acc=acc, acc_div=float(L + 1))
     return gather_rows(dg, acc) if gather_output else acc

@@ -9,6 +9,7 @@ models use them only when no gradient is required.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -154,6 +155,8 @@ def hop_table(n_rows: int, d: int, *, device=None, zero: bool = False,
     start byte mod 1 KB)); a compact tensor for other widths. zero: the d columns are zeroed
     (the padding columns are never read)."""
     ld, start = layout if layout is not None else HOP_TABLE_LAYOUT.get(d, (d, None))
+    if layout is None and start is not None and not _placed_tables_fit(n_rows, d, ld, device):
+        start = None
     if start is None or n_rows == 0:
         mk = torch.zeros if zero else torch.empty
         return mk((n_rows, d), dtype=torch.float32, device=device)
@@ -165,6 +168,24 @@ def hop_table(n_rows: int, d: int, *, device=None, zero: bool = False,
     if zero:
         t.zero_()
     return t
+
+
+# The placed tables cost ld / d times the compact bytes (2x at d = 32 / 64 / 128). They are
+# used only while that extra space is a small part of the device's free memory, and never with
+# GNNREC_HOP_TABLE_LAYOUT=0 (compact tables everywhere; same bits, the hop is ~4 % slower).
+HOP_TABLE_MAX_EXTRA_FRACTION = 0.25
+
+
+def _placed_tables_fit(n_rows: int, d: int, ld: int, device) -> bool:
+    if os.environ.get("GNNREC_HOP_TABLE_LAYOUT", "1") == "0":
+        return False
+    dev = torch.device(device) if device is not None else None
+    if dev is None or dev.type != "cuda" or n_rows == 0:
+        return True
+    extra = n_rows * (ld - d) * 4
+    free, _ = torch.cuda.mem_get_info(dev)
+    cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+    return extra <= HOP_TABLE_MAX_EXTRA_FRACTION * (free + max(0, cached))
 
 
 def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None,
@@ -250,6 +271,9 @@ def spmm_tiled_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], p
     ([n_rows, >= d]; None: x's own rows)."""
     _require_device(adj, x, y, self_rows, acc, prev)
     d = x.shape[1]
+    if bool(_lib.lib().gnnrec_tiled_plan_quad()) != (plan.get("layout") == "quad"):
+        raise ValueError("spmm_tiled_into: the plan's layout does not match the kernel's "
+                         "(gnnrec_tiled_plan_quad); build it with CsrGraph.tiled_plan()")
     check(_lib.lib().gnnrec_spmm_tiled_f32(
         ptr(plan["slot"]), ptr(plan.get("val")), ptr(plan.get("cls")),
         ptr(plan.get("row_factor")), ptr(plan.get("class_table")), int(plan.get("n_classes", 0)),
@@ -681,6 +705,73 @@ def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh:
                                      ptr(plan["seg_end"]), n_seg, ptr(plan["heavy_rows"]),
                                      ptr(plan["heavy_seg_ptr"]), plan["heavy_rows"].numel(),
                                      ptr(work), *common, stream), "gnnrec_gat_heavy_f32")
+    return out
+
+
+# Heavy-row segments of the scores-from-rows kernels: "column" runs them sorted by their first
+# column (CsrGraph.heavy_plan_by_column), "row" in row order; GAT_XCD_ORDER gives each XCD a
+# contiguous eighth of that list.
+GAT_SEGMENT_ORDER = os.environ.get("GNNREC_GAT_SEGMENT_ORDER", "column")
+GAT_XCD_ORDER = os.environ.get("GNNREC_GAT_XCD_ORDER", "1") != "0"
+
+
+def gat_att_supported(o_dim: int) -> bool:
+    """o_dim the ATT kernels take (a head's score dot spans o_dim / 4 <= 16 lanes)."""
+    q = o_dim // 4
+    return o_dim % 4 == 0 and 1 <= q <= 16 and (q & (q - 1)) == 0
+
+
+def gat_aggregate_att(adj: CsrGraph, h: torch.Tensor, hself: torch.Tensor, att: torch.Tensor,
+                      heads: int, o_dim: int, slope: float = 0.2, mean_heads: bool = False,
+                      apply_elu: bool = False, *, out: Optional[torch.Tensor] = None,
+                      epi: int = 0, self_rows: Optional[torch.Tensor] = None,
+                      acc: Optional[torch.Tensor] = None, acc_div: float = 1.0,
+                      heavy_threshold: Optional[int] = None,
+                      shared_rows: bool = False) -> Optional[torch.Tensor]:
+    """gat_aggregate with the attention scores formed in the kernel from the rows it reads
+    (gnnrec_gat_aggregate_att_f32 / gnnrec_gat_heavy_att_f32): att [2, heads, o_dim] holds
+    the self and neighbour attention vectors (shared_rows: the row vectors W_h^T a_h acting on
+    the shared o_dim-wide row); hself: the destination rows' own rows of h's layout (row r of
+    adj -> hself[r]). No score tables are read: a neighbour costs its feature row only."""
+    if heavy_threshold is None:
+        heavy_threshold = GAT_HEAVY_THRESHOLD
+    if not gat_att_supported(o_dim):
+        raise ValueError(f"gat_aggregate_att: o_dim = {o_dim} unsupported")
+    h, hself = _rowmajor(h), _rowmajor(hself)
+    att = att.to(device=h.device, dtype=torch.float32).contiguous()
+    if att.numel() != 2 * heads * o_dim:
+        raise ValueError("att must hold [2, heads, o_dim] floats")
+    _require_device(adj, h, hself, self_rows, acc)
+    if h.shape[1] < (o_dim if shared_rows else heads * o_dim) or hself.shape[0] < adj.n_rows:
+        raise ValueError("h / hself too small for the aggregated rows")
+    head_stride = 0 if shared_rows else o_dim
+    width = o_dim if mean_heads else heads * o_dim
+    if out is None and not (epi & EPI_NO_Y):
+        out = torch.empty((adj.n_rows, width), dtype=torch.float32, device=h.device)
+    plan = None
+    if heavy_threshold > 0:
+        plan = (adj.heavy_plan_by_column(heavy_threshold, GAT_SEGMENT)
+                if GAT_SEGMENT_ORDER == "column" else adj.heavy_plan(heavy_threshold, GAT_SEGMENT))
+    common = (ptr(h), h.stride(0), head_stride, ptr(hself), hself.stride(0), ptr(att),
+              int(heads), int(o_dim), float(slope), int(mean_heads), int(apply_elu), ptr(out),
+              out.stride(0) if out is not None else width, int(epi), ptr(self_rows),
+              self_rows.stride(0) if self_rows is not None else width, ptr(acc),
+              acc.stride(0) if acc is not None else width, float(acc_div))
+    L = _lib.lib()
+    stream = _lib.stream_of(adj.device)
+    check(L.gnnrec_gat_aggregate_att_f32(ptr(adj.row_ptr), ptr(adj.col), adj.n_rows, *common,
+                                         int(heavy_threshold if plan is not None else 0), stream),
+          "gnnrec_gat_aggregate_att_f32")
+    if plan is not None:
+        n_seg = plan["seg_row"].numel()
+        work = torch.empty(n_seg * (heads * o_dim + 2 * heads) + 4, dtype=torch.float32,
+                           device=h.device)
+        check(L.gnnrec_gat_heavy_att_f32(ptr(adj.col), ptr(plan["seg_row"]),
+                                         ptr(plan["seg_beg"]), ptr(plan["seg_end"]), n_seg,
+                                         ptr(plan["heavy_rows"]), ptr(plan["heavy_seg_ptr"]),
+                                         plan["heavy_rows"].numel(), ptr(work), *common,
+                                         ptr(plan.get("seg_pos")), int(GAT_XCD_ORDER), stream),
+              "gnnrec_gat_heavy_att_f32")
     return out
 
 

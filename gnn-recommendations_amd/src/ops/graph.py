@@ -673,6 +673,28 @@ class CsrGraph:
                                         seg_end=seg_end.contiguous())
         return self._plans[key]
 
+    def heavy_plan_by_column(self, threshold: int, seg_len: int):
+        """heavy_plan with the segment arrays sorted by each segment's first column (stable;
+        cached), plus seg_pos: the sorted position of each segment of the row-grouped
+        numbering heavy_seg_ptr refers to (gnnrec_gat_heavy_att_f32). Segments of different
+        heavy rows over the same columns then run together and share gathered lines in L2."""
+        key = ("heavy_col", threshold, seg_len)
+        if key not in self._plans:
+            base = self.heavy_plan(threshold, seg_len)
+            if base is None:
+                self._plans[key] = None
+            else:
+                first = self.col[base["seg_beg"]].to(torch.int64)
+                order = torch.sort(first, stable=True).indices
+                pos = torch.empty_like(order)
+                pos[order] = torch.arange(order.numel(), device=order.device)
+                self._plans[key] = dict(
+                    heavy_rows=base["heavy_rows"], heavy_seg_ptr=base["heavy_seg_ptr"],
+                    seg_row=base["seg_row"][order].contiguous(),
+                    seg_beg=base["seg_beg"][order].contiguous(),
+                    seg_end=base["seg_end"][order].contiguous(), seg_pos=pos.contiguous())
+        return self._plans[key]
+
     def __repr__(self) -> str:  # keep it short: the tensors are huge
         return (f"CsrGraph(shape={self.shape}, nnz={self.nnz}, device={self.device}, "
                 f"symmetric={self.symmetric}, shard={self.shard_info})")

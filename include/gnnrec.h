@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GNNREC_ABI_VERSION 9
+#define GNNREC_ABI_VERSION 10
 
 typedef struct ihipStream_t* gnnrec_stream_t;
 
@@ -173,6 +173,10 @@ int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col, const
 #define GNNREC_TILED_QUAD_TAIL 16   /* tail chunks of the quad layout (prefetch 11 chunks ahead) */
 #define GNNREC_TILED_MAX_ROWS 1279
 #define GNNREC_TILED_SYNC_WORDS 256
+/* sync[GNNREC_TILED_SYNC_ERR_WORD] != 0 after a gnnrec_spmm_tiled_f32 launch: the plan's wave
+ * ranges were not quad-aligned (chunk-major arrays passed to a quad-layout build, see
+ * gnnrec_tiled_plan_quad); the affected rows were not written. The launch zeroes the word. */
+#define GNNREC_TILED_SYNC_ERR_WORD 1
 #define GNNREC_TILED_HDR_WORDS 4
 #define GNNREC_TILED_MAX_LDX 1024
 #define GNNREC_TILED_MAX_CLASSES 256
@@ -398,6 +402,41 @@ int gnnrec_gat_heavy_f32(const int32_t* col, const int64_t* seg_row, const int64
                          float* out, int64_t ldo, int32_t epi, const float* self,
                          int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
                          gnnrec_stream_t stream);
+
+/* Scores from the rows (ABI 10): the same aggregation and epilogue as gnnrec_gat_aggregate_f32 /
+ * gnnrec_gat_heavy_f32, with the attention scores formed in the kernel from the rows it reads
+ * instead of gathered from score tables (gat.py:113-118: s_self = h_r a_self, s_neigh = h_j
+ * a_neigh, per head): att = [2][heads][o_dim] fp32 (att[0][h] = a_self of head h, att[1][h] =
+ * a_neigh; for head_stride = 0 the row vectors W_h^T a_h acting on the shared row), and
+ *   s_self[r, h]  = att[0][h] . hself[r, h, :]   (hself + r*ld_hself + h*head_stride)
+ *   s_neigh[j, h] = att[1][h] . hfeat[j, h, :]   (the gathered row itself)
+ * in fp32 (tolerance-level: the reference's torch.mm(h, a) summed in another order). A 256-B
+ * gathered row then costs 2 instead of 3 random 128-B lines per neighbour. o_dim <= 64 and
+ * o_dim / 4 a power of two; the shared-row fast path is heads = 4, o_dim = 64. */
+int gnnrec_gat_aggregate_att_f32(const int64_t* row_ptr, const int32_t* col, int64_t n_rows,
+                                 const float* hfeat, int64_t ldh, int64_t head_stride,
+                                 const float* hself, int64_t ld_hself, const float* att,
+                                 int32_t heads, int32_t o_dim, float slope, int32_t mean_heads,
+                                 int32_t apply_elu, float* out, int64_t ldo, int32_t epi,
+                                 const float* self, int64_t ld_self, float* acc, int64_t ld_acc,
+                                 float acc_div, int64_t max_row_len, gnnrec_stream_t stream);
+
+int gnnrec_gat_heavy_att_f32(const int32_t* col, const int64_t* seg_row, const int64_t* seg_beg,
+                             const int64_t* seg_end, int64_t n_seg, const int64_t* heavy_rows,
+                             const int64_t* heavy_seg_ptr, int64_t n_heavy, float* work,
+                             const float* hfeat, int64_t ldh, int64_t head_stride,
+                             const float* hself, int64_t ld_hself, const float* att,
+                             int32_t heads, int32_t o_dim, float slope, int32_t mean_heads,
+                             int32_t apply_elu, float* out, int64_t ldo, int32_t epi,
+                             const float* self, int64_t ld_self, float* acc, int64_t ld_acc,
+                             float acc_div, const int64_t* seg_pos, int32_t xcd_order,
+                             gnnrec_stream_t stream);
+/* gnnrec_gat_heavy_att_f32's segment order: seg_row / seg_beg / seg_end may list the segments
+ * in any order (e.g. by their first column, so that segments of different heavy rows over the
+ * same columns run at the same time and share gathered lines in L2); seg_pos[j] gives the
+ * position of the j-th segment of heavy_seg_ptr's row-grouped numbering (NULL: the arrays are
+ * row-grouped). xcd_order = 1: XCD x runs the x-th eighth of the segment list (blocks are
+ * otherwise dealt round-robin to the 8 XCDs, spreading neighbouring segments over 8 L2s). */
 
 /* Dense projections of the GAT layer (gat.py:113-118 W_h x and the attention halves, one
  * fused weight; and the head-averaged last layer's W_h applied after the aggregation,

@@ -287,16 +287,31 @@ def test_rows_gemm_guards_on_host():
     assert GATLayer(64, 64, 4, concat_heads=False).shares_input()
 
 
-def test_gat_dense_fallback_guard():
-    """GAT training is outside the native path (the sparse kernel has no backward): a native
-    operand that cannot take it falls back to the reference's dense [N, N] softmax only up to
-    GAT_DENSE_MAX_NODES nodes (with a warning) and raises above it; the reason is reported."""
-    from src.models.baselines.gat import (GAT_DENSE_MAX_NODES, GATLayer,
-                                          check_dense_fallback)
-    with pytest.raises(RuntimeError, match="inference-only"):
-        check_dense_fallback(GAT_DENSE_MAX_NODES + 1, "autograd")
+def test_gat_dense_fallback_guard(monkeypatch):
+    """A native operand that the sparse kernel cannot take falls back to the reference's dense
+    [N, N] softmax only when its estimated footprint fits the available memory (with a
+    warning), and raises otherwise; a node cap (GNNREC_GAT_DENSE_MAX_NODES) replaces the
+    memory test when set (the old fixed 20K cap refused graphs a 288 GB device
+    runs). The reason is reported."""
+    from src.models.baselines import gat as gat_mod
+    from src.models.baselines.gat import (GATLayer, check_dense_fallback,
+                                          dense_fallback_bytes)
+    monkeypatch.delenv("GNNREC_GAT_DENSE_MAX_NODES", raising=False)
+    assert dense_fallback_bytes(1000, 4, grad=True) == 4 * 10**6 * 13
+    assert dense_fallback_bytes(1000, 4, grad=False) == 4 * 10**6 * 4
+    with pytest.raises(RuntimeError, match="dense \\[N, N\\] softmax path would need"):
+        check_dense_fallback(10**7, "autograd", heads=4, grad=True)       # 5.2 PB
+    with pytest.warns(RuntimeWarning, match="dense O\\(N\\^2\\)"):
+        check_dense_fallback(100, "autograd", heads=4, grad=True)
+    monkeypatch.setenv("GNNREC_GAT_DENSE_MAX_NODES", "50")
+    with pytest.raises(RuntimeError, match="node cap GNNREC_GAT_DENSE_MAX_NODES = 50"):
+        check_dense_fallback(100, "autograd")
     with pytest.warns(RuntimeWarning):
-        check_dense_fallback(GAT_DENSE_MAX_NODES, "autograd")
+        check_dense_fallback(50, "autograd")
+    monkeypatch.delenv("GNNREC_GAT_DENSE_MAX_NODES")
+    monkeypatch.setattr(gat_mod, "GAT_DENSE_MAX_NODES", 10)
+    with pytest.raises(RuntimeError, match="node cap"):
+        check_dense_fallback(11, "autograd")
     layer = GATLayer(64, 16, 4)
     g = CsrGraph(torch.tensor([0, 1, 2]), torch.tensor([1, 0], dtype=torch.int32),
                  torch.ones(2), (2, 2), 1, 1, True)
@@ -307,3 +322,38 @@ def test_gat_dense_fallback_guard():
         layer.dropout = 0.1
         assert "dropout" in layer.native_block(g)
     assert layer.native_block(torch.zeros(2, 2)) == "not a native operand"
+
+
+def test_gat_sampled_row_checker_matches_reference_dense_layer():
+    """The config-5 sampled-row checker (oracle/gat_sample.py) is itself pinned to the
+    reference layer semantics: at a row sample, layer_rows equals GATLayer's dense masked
+    softmax path (the reference's gat.py:92-151, run here on the CPU) + F.elu, for a concat and
+    a head-averaged layer; sub_csr cuts exactly the sampled rows."""
+    import oracle.gat_sample as gs
+    from src.models.baselines.gat import GATLayer
+    rng = np.random.default_rng(2)
+    nu, ni = 120, 90
+    u = np.concatenate([np.arange(nu), rng.integers(0, nu, ni), rng.integers(0, nu, 1500)])
+    i = np.concatenate([rng.integers(0, ni, nu), np.arange(ni), rng.integers(0, ni, 1500)])
+    g = CsrGraph.from_interactions(u, i, nu, ni)
+    deg = np.diff(g.row_ptr.numpy())
+    rows = gs.sample_rows(deg, n_heavy=5, per_decile=7, seed=0)
+    assert np.all(np.isin(np.argsort(-deg)[:5], rows))
+    rp_sub, col_sub = gs.sub_csr(g.row_ptr, g.col, rows)
+    for j, r in enumerate(rows):
+        np.testing.assert_array_equal(col_sub[rp_sub[j]:rp_sub[j + 1]],
+                                      g.col.numpy()[g.row_ptr[r]:g.row_ptr[r + 1]])
+    torch.manual_seed(0)
+    x = torch.randn(nu + ni, 32) * 0.3
+    A = g.to_torch_sparse_coo()
+    for concat, out_dim in ((True, 8), (False, 32)):
+        layer = GATLayer(32, out_dim, 4, 0.0, 0.2, concat_heads=concat)
+        for w in layer.W:
+            torch.nn.init.xavier_uniform_(w.weight)
+        for p in list(layer.a_self) + list(layer.a_neigh):
+            torch.nn.init.xavier_uniform_(p.data)
+        with torch.no_grad():
+            ref = torch.nn.functional.elu(layer._dense_forward(x, A)).numpy()
+        got = gs.layer_rows(layer, x, rp_sub, col_sub, rows)
+        res = gs.close(got, ref[rows])
+        assert res["within_tolerance"], res

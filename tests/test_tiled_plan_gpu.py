@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 import torch
 
+import oracle
 from src.ops import CsrGraph, functional as F
 
 pytestmark = pytest.mark.gpu
@@ -171,3 +172,47 @@ def test_quad_plan_layout_is_padding_plus_permutation(cuda):
         n = w2[w + 1] - w2[w]
         np.testing.assert_array_equal(cls[wq[w]:wq[w] + n], c_old[w2[w]:w2[w + 1]])
         assert np.all(cls[wq[w] + n:wq[w + 1]] == 0)
+
+
+def test_chunk_major_plan_on_quad_build_is_flagged(cuda):
+    """a raw-ABI caller passing the planner's chunk-major arrays to a quad-layout
+    build gets the error word set (sync[GNNREC_TILED_SYNC_ERR_WORD]) and untouched rows, not
+    silently wrong ones; the Python wrapper refuses such a plan before launching."""
+    from src.ops import _lib
+    L = _lib.lib()
+    if not L.gnnrec_tiled_plan_quad():
+        pytest.skip("chunk-major build")
+    rng = np.random.default_rng(6)
+    g = CsrGraph.from_interactions(rng.integers(0, 3000, 60000), rng.integers(0, 2000, 60000),
+                                   3000, 2000).to(cuda)
+    R = 333
+    plan = g._tiled_plan_host(R, 4096, 512)
+    plan.update(rows_per_block=R)
+    wp = plan["wave_ptr"].cpu().numpy()
+    assert np.any(wp % 4 != 0)          # this plan has ranges a quad build would misread
+    # a quad build prefetches up to 12 chunks past a wave's range: give the chunk-major
+    # arrays the quad layout's tail so no load leaves them
+    pad = _lib.TILED_QUAD_TAIL * _lib.TILED_CHUNK
+    for k, n in (("slot", pad), ("val", pad), ("hdr", _lib.TILED_QUAD_TAIL * 4)):
+        plan[k] = torch.cat([plan[k], torch.zeros(n, dtype=plan[k].dtype, device=cuda)])
+    x = torch.randn(g.shape[0], 32, device=cuda)
+    y = torch.full_like(x, 7.0)
+    with pytest.raises(ValueError, match="layout"):
+        F.spmm_tiled_into(g, x, y, plan)
+    sync = torch.zeros(_lib.TILED_SYNC_WORDS, dtype=torch.int32, device=cuda)
+    _lib.check(L.gnnrec_spmm_tiled_f32(
+        _lib.ptr(plan["slot"]), _lib.ptr(plan["val"]), 0, 0, 0, 0, _lib.ptr(plan["hdr"]),
+        _lib.ptr(plan["wave_ptr"]), _lib.ptr(plan["n_steps"]), plan["n_blocks"], R, _lib.ptr(x),
+        x.shape[0], x.stride(0), _lib.ptr(y), y.stride(0), g.n_rows, 32, 0, 0, 32, 0, 32, 1.0,
+        0, 32, _lib.ptr(sync), 0, _lib.stream_of(cuda)), "tiled")
+    torch.cuda.synchronize()
+    assert int(sync[_lib.TILED_SYNC_ERR_WORD]) != 0
+    # the launch zeroes the word: the quad plan of the same operand runs clean and right
+    qp = g.tiled_plan(rows_per_block=R, panel=4096, sub_panel=512)
+    y2 = torch.empty_like(x)
+    F.spmm_tiled_into(g, x, y2, qp)
+    torch.cuda.synchronize()
+    assert int(qp["sync"][_lib.TILED_SYNC_ERR_WORD]) == 0
+    ref = oracle.spmm(g.row_ptr.cpu().numpy(), g.col.cpu().numpy(), g.val.cpu().numpy(),
+                      x.cpu().numpy())
+    assert np.array_equal(y2.cpu().numpy().view(np.uint32), ref.view(np.uint32))

@@ -449,6 +449,18 @@ def main(argv=None):
                 del g1, u, i
             if world == 1 and not big and not a.no_ref_check:
                 rec["verify_vs_torch_reference"] = verify_config5(g, m, mine, device)
+            if world == 1 and big and not a.no_ref_check:
+                # too large for the whole-graph references: the sampled-row oracle check
+                # (oracle/gat_sample.py) at the 64 heaviest rows + 4096 per degree decile
+                from oracle.gat_sample import check_forward, sample_rows
+                rows = sample_rows(deg, n_heavy=64, per_decile=4096, seed=0)
+                progress(f"sampled-row oracle check: {rows.size} rows")
+                t1 = time.time()
+                gd = g if g.row_ptr.is_cuda else g.to(device)
+                rec["verify"] = check_forward(m, gd, mine, rows)
+                rec["verify"]["seconds"] = time.time() - t1
+                progress(f"check done: all_within_tolerance={rec['verify']['all_within_tolerance']}")
+                del gd
             emit(rec)
     if world > 1:
         dist.destroy_process_group()

@@ -1,26 +1,60 @@
 #!/bin/bash
-# Round profile of the headline bench (run on the GPU box from the repo root):
-#   bench.py with the CPU baseline, rocprofv3 kernel-trace stats, and the two PMC passes.
-# usage: [BENCH_ARGS="--dim 128"] [NO_CPU=1] bash tools/profile_round.sh <tag>
+# One script for a round's GPU records (run on the GPU box from the repo root); every step
+# under its own time limit, chained so the first failure ends the call.
+#
+#   bash tools/profile_round.sh <tag> [step ...]
+#
+# steps (default: tests smoke bench kt pmc):
+#   tests   the whole -m gpu suite                        -> gpu_tests.log
+#   smoke   __graft_entry__.smoke()                       -> smoke.log
+#   bench   bench.py (CPU baseline + vendor comparators)  -> bench.json
+#   kt      rocprofv3 --kernel-trace --stats of bench.py  -> kernel_stats.csv, kt_bench.json
+#   pmc     FETCH_SIZE / WRITE_SIZE / TCC hit-miss passes -> pmc_summary.json, l2_hit.txt
+#   configs tools/bench_configs.py $CONFIGS (default "2 3 4 5 6 9") -> configs.jsonl
+# env: BENCH_ARGS (e.g. "--dim 128"), NO_CPU=1 (bench without the CPU baseline),
+#      KERNEL (the PMC summary's kernel, default tiled_hop_kernel), TESTS (pytest selection)
 set -euo pipefail
-TAG=${1:-r01}
+TAG=${1:?usage: profile_round.sh <tag> [step ...]}
+shift
+STEPS=${*:-tests smoke bench kt pmc}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 BA=${BENCH_ARGS:-}
-CPU=""
-[ -n "${NO_CPU:-}" ] && CPU="--no-cpu-baseline"
-timeout -k 10 600 python bench.py $BA $CPU > $OUT/bench.json 2> $OUT/bench.err
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 bench.py $BA --no-cpu-baseline --no-vendor --steps 10 > $OUT/kt_bench.json 2> $OUT/kt.err
-timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py $BA --no-cpu-baseline --no-vendor --steps 3 --warmup 1 > $OUT/pmc_fetch_bench.json 2> $OUT/pmc_fetch.err
-timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 bench.py $BA --no-cpu-baseline --no-vendor --steps 3 --warmup 1 > $OUT/pmc_write_bench.json 2> $OUT/pmc_write.err
-timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/pmc_l2 -o run -- python3 bench.py $BA --no-cpu-baseline --no-vendor --steps 3 --warmup 1 > $OUT/pmc_l2_bench.json 2> $OUT/pmc_l2.err
-K=${KERNEL:-tiled_hop_kernel}
-F=$(find $OUT/pmc_fetch -name "*counter_collection.csv" -print -quit)
-W=$(find $OUT/pmc_write -name "*counter_collection.csv" -print -quit)
-python tools/pmc_summarize.py "$F" "$W" $OUT/pmc_summary.json $K $OUT/pmc_fetch_bench.json
-L=$(find $OUT/pmc_l2 -name "*counter_collection.csv" -print -quit)
-python tools/pmc_l2.py "$L" > $OUT/l2_hit.txt
-F2=$(find $OUT/kt -name "*kernel_stats.csv" -print -quit)
-cp "$F2" $OUT/kernel_stats.csv
+NOPROF="--no-cpu-baseline --no-vendor"
+for step in $STEPS; do
+  echo "[profile_round] $step" >&2
+  case $step in
+    tests)
+      timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu \
+          ${TESTS:-tests/} > $OUT/gpu_tests.log 2>&1 ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('__SMOKE_OK__')" \
+          > $OUT/smoke.log 2>&1 ;;
+    bench)
+      CPU=""
+      [ -n "${NO_CPU:-}" ] && CPU="--no-cpu-baseline"
+      timeout -k 10 600 python bench.py $BA $CPU > $OUT/bench.json 2> $OUT/bench.err ;;
+    kt)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- \
+          python3 bench.py $BA $NOPROF --steps 10 > $OUT/kt_bench.json 2> $OUT/kt.err
+      cp "$(find $OUT/kt -name "*kernel_stats.csv" -print -quit)" $OUT/kernel_stats.csv ;;
+    pmc)
+      for pass in "FETCH_SIZE:fetch" "WRITE_SIZE:write" "TCC_HIT_sum TCC_MISS_sum:l2"; do
+        ctr=${pass%%:*}; name=${pass##*:}
+        timeout -k 10 600 rocprofv3 --pmc $ctr --output-format csv -d $OUT/pmc_$name -o run -- \
+            python3 bench.py $BA $NOPROF --steps 3 --warmup 1 > $OUT/pmc_${name}_bench.json \
+            2> $OUT/pmc_$name.err
+      done
+      python tools/pmc_summarize.py "$(find $OUT/pmc_fetch -name "*counter_collection.csv" -print -quit)" \
+          "$(find $OUT/pmc_write -name "*counter_collection.csv" -print -quit)" $OUT/pmc_summary.json \
+          ${KERNEL:-tiled_hop_kernel} $OUT/pmc_fetch_bench.json
+      python tools/pmc_l2.py "$(find $OUT/pmc_l2 -name "*counter_collection.csv" -print -quit)" \
+          > $OUT/l2_hit.txt ;;
+    configs)
+      timeout -k 10 900 python -u tools/bench_configs.py --configs ${CONFIGS:-2 3 4 5 6 9} \
+          > $OUT/configs.jsonl 2> $OUT/configs.err ;;
+    *) echo "unknown step $step" >&2; exit 2 ;;
+  esac
+done
 echo done

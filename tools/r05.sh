@@ -1,0 +1,41 @@
+#!/bin/bash
+# Round-5 GPU calls (one file for the round; each call is a case). Run from the repo root on
+# the GPU box:  bash tools/r05.sh <call>
+set -euo pipefail
+OUT=gpurun_out/r05
+mkdir -p $OUT
+export TMPDIR=/tmp
+C5="--configs 5 --c5-shape 5000000 5000000 250000000"
+case ${1:?call} in
+  c1)
+    # the whole -m gpu suite after the round's first changes, the headline bench with the
+    # rocSPARSE comparator, config 5 at 5M x 5M with the sampled-row oracle check, and the
+    # GAT kernels' L2 hit/miss and fabric bytes at that size
+    timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests/ \
+        > $OUT/c1_gpu_tests.log 2>&1
+    timeout -k 10 600 python bench.py > $OUT/c1_bench.json 2> $OUT/c1_bench.err
+    timeout -k 10 600 python -u tools/bench_configs.py $C5 --steps 5 > $OUT/c1_config5_g250m.jsonl \
+        2> $OUT/c1_config5_g250m.err
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c1_c5kt -o run -- \
+        python3 tools/bench_configs.py $C5 --steps 3 --warmup 1 --no-ref-check > $OUT/c1_c5kt.jsonl 2> $OUT/c1_c5kt.err
+    timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/c1_c5l2 -o run -- \
+        python3 tools/bench_configs.py $C5 --steps 3 --warmup 1 --no-ref-check > $OUT/c1_c5l2.jsonl 2> $OUT/c1_c5l2.err
+    timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/c1_c5fetch -o run -- \
+        python3 tools/bench_configs.py $C5 --steps 3 --warmup 1 --no-ref-check > $OUT/c1_c5fetch.jsonl 2> $OUT/c1_c5fetch.err
+    ;;
+  c2)
+    # scores-from-rows GAT kernels (ABI 10): their tests and the GAT model / golden tests,
+    # config 5 at 5M x 5M (checked) + its kernel trace, then G1B with the sampled-row check
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+        tests/test_gat_att_gpu.py tests/test_models_gpu.py tests/test_real_shapes_gpu.py \
+        tests/test_offsets_gpu.py tests/test_tiled_plan_gpu.py > $OUT/c2_gat_tests.log 2>&1
+    timeout -k 10 600 python -u tools/bench_configs.py $C5 --steps 5 > $OUT/c2_config5_g250m.jsonl \
+        2> $OUT/c2_config5_g250m.err
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c2_c5kt -o run -- \
+        python3 tools/bench_configs.py $C5 --steps 3 --warmup 1 --no-ref-check > $OUT/c2_c5kt.jsonl 2> $OUT/c2_c5kt.err
+    timeout -k 10 900 python -u tools/bench_configs.py --configs 5 --g1b --steps 5 \
+        > $OUT/c2_config5_g1b.jsonl 2> $OUT/c2_config5_g1b.err
+    ;;
+  *) echo "unknown call $1" >&2; exit 2 ;;
+esac
+echo done
