@@ -15,6 +15,7 @@
 // layer-mean accumulator (gat.py:287-288, GNNREC_EPI_* flags).
 #include <math.h>
 
+#include <type_traits>
 #include <utility>
 
 #include "gather.h"
@@ -87,6 +88,16 @@ __device__ __forceinline__ void gat_finish(const GatParams& p, int64_t r, float4
 // own dense softmax. Neighbours past the row end get E = -inf (p = 0: the sums are unchanged,
 // no branch). Every kernel below uses the same blocks from the row's (or segment's) first
 // neighbour, so the shared-row and the head-major kernels agree bit for bit.
+// The ATT kernels keep the score dots in registers: cap them at 128 VGPRs, 4 waves per SIMD
+// like the score-table kernels (uncapped they take 132-176 and drop to 2-3 waves)
+#ifndef GAT_ATT_WAVES
+#define GAT_ATT_WAVES 4
+#endif
+#ifndef GAT_ATT_CHUNK
+#define GAT_ATT_CHUNK 16
+#endif
+#define GAT_OCCUPANCY(ATT) __attribute__((amdgpu_waves_per_eu((ATT) ? GAT_ATT_WAVES : 1)))
+
 constexpr int kSoftBlock = 8;
 constexpr float kLog2e = 1.4426950408889634f;
 
@@ -112,12 +123,14 @@ __device__ __forceinline__ float dpp_f(float v) {
 constexpr int kDppRowMirror = 0x140, kDppHalfMirror = 0x141, kDppXor2 = 0x4E, kDppXor1 = 0xB1,
               kDppRor8 = 0x128;
 
-// sum over the aligned group of hl lanes (hl in {1, 2, 4, 8, 16}), in every lane of it
-__device__ __forceinline__ float group_sum(float v, int hl) {
-  if (hl >= 16) v += dpp_f<kDppRowMirror>(v);   // lane i + lane 15 - i
-  if (hl >= 8) v += dpp_f<kDppHalfMirror>(v);   // lane i + lane 7 - i (8-lane halves)
-  if (hl >= 4) v += dpp_f<kDppXor2>(v);
-  if (hl >= 2) v += dpp_f<kDppXor1>(v);
+// sum over the aligned group of HL lanes (HL in {1, 2, 4, 8, 16}), in every lane of it
+template <int HL>
+__device__ __forceinline__ float group_sum(float v) {
+  static_assert(HL >= 1 && HL <= 16 && (HL & (HL - 1)) == 0, "group of 1..16 lanes");
+  if constexpr (HL >= 16) v += dpp_f<kDppRowMirror>(v);   // lane i + lane 15 - i
+  if constexpr (HL >= 8) v += dpp_f<kDppHalfMirror>(v);   // lane i + lane 7 - i (8-lane halves)
+  if constexpr (HL >= 4) v += dpp_f<kDppXor2>(v);
+  if constexpr (HL >= 2) v += dpp_f<kDppXor1>(v);
   return v;
 }
 
@@ -146,12 +159,14 @@ __device__ __forceinline__ void gat_block(const float (&E)[kSoftBlock], const fl
 
 // Online-softmax accumulation of neighbours [beg, end) of row r (head of this lane); m is in
 // the base-2 logit domain.
-template <int GROUP, bool ATT>
+// HL: lanes per head (o_dim / 4) as a compile-time constant for the ATT kernels (0: runtime)
+template <int GROUP, bool ATT, int HL = 0>
 __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, int64_t beg,
                                                int64_t end, int gl, float& m, float& l,
                                                float4& a) {
   static_assert(kChunk % kSoftBlock == 0, "a gather step holds whole softmax blocks");
-  const int hl = p.o_dim / 4;
+  static_assert(!ATT || (HL >= 1 && HL <= GROUP), "ATT needs the lanes per head");
+  const int hl = HL > 0 ? HL : p.o_dim / 4;
   const int head = gl / hl;
   const int fo = 4 * (gl - head * hl);   // this lane's features of its head's row
   float ss;
@@ -159,12 +174,17 @@ __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, in
   if constexpr (ATT) {
     const float4 as = ld4(p.att + head * p.o_dim + fo);
     an = ld4(p.att + (p.heads + head) * p.o_dim + fo);
-    ss = group_sum(dot4(ld4(p.hself + r * p.ld_hself + head * p.head_stride + fo), as), hl);
+    ss = group_sum<(HL > 0 ? HL : 1)>(dot4(ld4(p.hself + r * p.ld_hself + head * p.head_stride + fo), as));
   } else {
     ss = p.s_self[r * p.ld_ss + head];
   }
-  for (int64_t k0 = beg; k0 < end; k0 += kChunk) {
-    constexpr int PER = (GROUP >= kChunk) ? 1 : kChunk / GROUP;
+  // neighbours per gather step: the score-table kernels keep kChunk rows in flight per lane;
+  // the ATT kernels hold each row until its score is reduced, so they gather GAT_ATT_CHUNK at
+  // a time and win the occupancy back
+  constexpr int CH = ATT ? GAT_ATT_CHUNK : kChunk;
+  static_assert(CH % kSoftBlock == 0, "a gather step holds whole softmax blocks");
+  for (int64_t k0 = beg; k0 < end; k0 += CH) {
+    constexpr int PER = (GROUP >= CH) ? 1 : CH / GROUP;
     int cm[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
@@ -172,20 +192,20 @@ __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, in
       k = k < end ? k : end - 1;
       cm[q] = p.A.col[k];
     }
-    float4 xv[kChunk];
-    float sn[kChunk];
+    float4 xv[CH];
+    float sn[CH];
 #pragma unroll
-    for (int t = 0; t < kChunk; ++t) {
+    for (int t = 0; t < CH; ++t) {
       const int c = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
       xv[t] = ld4(p.h + (int64_t)c * p.ldh + head * p.head_stride + fo);
       if constexpr (!ATT) sn[t] = p.s_neigh[(int64_t)c * p.ld_sn + head];
     }
     if constexpr (ATT) {
 #pragma unroll
-      for (int t = 0; t < kChunk; ++t) sn[t] = group_sum(dot4(xv[t], an), hl);
+      for (int t = 0; t < CH; ++t) sn[t] = group_sum<(HL > 0 ? HL : 1)>(dot4(xv[t], an));
     }
 #pragma unroll
-    for (int b = 0; b < kChunk / kSoftBlock; ++b) {
+    for (int b = 0; b < CH / kSoftBlock; ++b) {
       if (k0 + b * kSoftBlock >= end) break;
       float E[kSoftBlock];
 #pragma unroll
@@ -196,8 +216,8 @@ __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, in
   }
 }
 
-template <int F, bool ATT>
-__global__ __launch_bounds__(kBlock) void gat_kernel(GatParams p) {
+template <int F, bool ATT, int HL = 0>
+__global__ __launch_bounds__(kBlock) GAT_OCCUPANCY(ATT) void gat_kernel(GatParams p) {
   constexpr int GROUP = F / 4;
   constexpr int RPW = 64 / GROUP;
   const int lane = threadIdx.x & 63;
@@ -208,7 +228,7 @@ __global__ __launch_bounds__(kBlock) void gat_kernel(GatParams p) {
   if (p.max_row_len > 0 && end - beg > p.max_row_len) return;  // heavy row: split path
   float m = -INFINITY, l = 0.f;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  gat_accumulate<GROUP, ATT>(p, r, beg, end, gl, m, l, a);
+  gat_accumulate<GROUP, ATT, HL>(p, r, beg, end, gl, m, l, a);
   // softmax normalisation (l = 0 for an empty row -> 0/0 = NaN, like the reference)
   gat_finish<GROUP>(p, r, make_float4(a.x / l, a.y / l, a.z / l, a.w / l), gl);
 }
@@ -240,37 +260,42 @@ __device__ __forceinline__ void gat_apply16(std::integer_sequence<int, T...>, fl
 // 16-lane row group (DPP: lanes L / L^8 exchange head pairs, then the 8-lane halves split the
 // neighbours 4 / 2 / 1) leaves lane gl exactly the two sums it turns into logits below:
 // neighbour gl & 7, heads 2 (gl >> 3) and 2 (gl >> 3) + 1.
-__device__ __forceinline__ void shared_scores16(const float4 (&xv)[8], const float4 (&an)[4],
+#ifndef GAT_ATT_LDS
+#define GAT_ATT_LDS 1
+#endif
+// an: the 4 heads' neighbour vectors, this lane's float4 of each (registers: an[h]; LDS:
+// an[h * 16 + gl])
+template <class AN>
+__device__ __forceinline__ float4 an_of(const AN& an, int h, int gl) {
+  if constexpr (std::is_pointer_v<std::decay_t<AN>>) return an[h * 16 + gl];
+  else return an[h];
+}
+
+template <class AN>
+__device__ __forceinline__ void shared_scores16(const float4 (&xv)[8], const AN& an,
                                                 int gl, float& sa, float& sb) {
   const bool hi = gl >= 8, b2 = gl & 4, b1 = gl & 2, b0 = gl & 1;
-  float Q[8][2];
-#pragma unroll
-  for (int t = 0; t < 8; ++t) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const float mine = dot4(xv[t], an[j]), other = dot4(xv[t], an[2 + j]);
-      const float keep = hi ? other : mine, send = hi ? mine : other;
-      Q[t][j] = keep + dpp_f<kDppRor8>(send);        // lanes L, L^8: heads 2hi, 2hi + 1
-    }
-  }
-  float R[4][2];
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)                          // lanes t, 7 - t: neighbours 4 b2 + k
-      R[k][j] = (b2 ? Q[4 + k][j] : Q[k][j]) + dpp_f<kDppHalfMirror>(b2 ? Q[k][j] : Q[4 + k][j]);
-  float S[2][2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)                          // lanes t, t^2: neighbours .. + 2 b1 + k
-      S[k][j] = (b1 ? R[2 + k][j] : R[k][j]) + dpp_f<kDppXor2>(b1 ? R[k][j] : R[2 + k][j]);
   float T[2];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)                            // lanes t, t^1: neighbour t
-    T[j] = (b0 ? S[1][j] : S[0][j]) + dpp_f<kDppXor1>(b0 ? S[0][j] : S[1][j]);
-  sa = T[0];
-  sb = T[1];
+  for (int j = 0; j < 2; ++j) {   // one head of each pair per pass: 16 partial dots live, not 32
+    float Q[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const float mine = dot4(xv[t], an_of(an, j, gl)), other = dot4(xv[t], an_of(an, 2 + j, gl));
+      Q[t] = (hi ? other : mine) + dpp_f<kDppRor8>(hi ? mine : other);   // lanes L, L^8
+    }
+    float R[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)           // lanes t, 7 - t: neighbours 4 b2 + k
+      R[k] = (b2 ? Q[4 + k] : Q[k]) + dpp_f<kDppHalfMirror>(b2 ? Q[k] : Q[4 + k]);
+    float S[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)           // lanes t, t^2: neighbours ... + 2 b1 + k
+      S[k] = (b1 ? R[2 + k] : R[k]) + dpp_f<kDppXor2>(b1 ? R[k] : R[2 + k]);
+    T[j] = (b0 ? S[1] : S[0]) + dpp_f<kDppXor1>(b0 ? S[0] : S[1]);   // lanes t, t^1: neighbour t
+  }
+  sa = T[0];   // neighbour gl & 7, head 2 hi
+  sb = T[1];   // head 2 hi + 1
 }
 
 template <bool ATT>
@@ -281,11 +306,22 @@ __device__ __forceinline__ void gat_shared_rows16(const GatParams& p, int64_t r,
   const int tl = gl & 7;
   const bool hi = gl >= 8;                       // heads 2, 3 (else 0, 1)
   const float ssa = hi ? ss[2] : ss[0], ssb = hi ? ss[3] : ss[1];
+#if GAT_ATT_LDS
+  // the neighbour vectors parked in LDS instead of 16 VGPRs: every lane writes the 4 float4 it
+  // reads back itself (all row groups write the same values), so no barrier is needed
+  __shared__ float4 s_an[4 * 16];
+  if constexpr (ATT) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) s_an[h * 16 + gl] = ld4(p.att + (4 + h) * 64 + 4 * gl);
+  }
+  const float4* an = s_an;
+#else
   float4 an[4];
   if constexpr (ATT) {
 #pragma unroll
     for (int h = 0; h < 4; ++h) an[h] = ld4(p.att + (4 + h) * 64 + 4 * gl);
   }
+#endif
   for (int64_t k0 = beg; k0 < end; k0 += 8) {
     int64_t k = k0 + gl;
     k = k < end ? k : end - 1;
@@ -388,7 +424,7 @@ __device__ __forceinline__ void shared_self_scores(const GatParams& p, int64_t r
   if constexpr (ATT) {
     const float4 xr = ld4(p.hself + r * p.ld_hself + 4 * gl);
 #pragma unroll
-    for (int h = 0; h < H; ++h) ss[h] = group_sum(dot4(xr, ld4(p.att + h * O + 4 * gl)), O / 4);
+    for (int h = 0; h < H; ++h) ss[h] = group_sum<O / 4>(dot4(xr, ld4(p.att + h * O + 4 * gl)));
   } else {
 #pragma unroll
     for (int h = 0; h < H; ++h) ss[h] = p.s_self[r * p.ld_ss + h];
@@ -396,7 +432,7 @@ __device__ __forceinline__ void shared_self_scores(const GatParams& p, int64_t r
 }
 
 template <int O, int H, int CH, bool ATT>
-__global__ __launch_bounds__(kBlock) void gat_shared_kernel(GatParams p) {
+__global__ __launch_bounds__(kBlock) GAT_OCCUPANCY(ATT) void gat_shared_kernel(GatParams p) {
   constexpr int GROUP = O / 4;
   constexpr int RPW = 64 / GROUP;
   const int lane = threadIdx.x & 63;
@@ -446,8 +482,8 @@ __device__ __forceinline__ int64_t split_block(const GatSplit& sp) {
   return sp.xcd_blocks > 0 ? (b % 8) * sp.xcd_blocks + b / 8 : b;
 }
 
-template <int F, bool ATT>
-__global__ __launch_bounds__(kBlock) void gat_partial_kernel(GatParams p, GatSplit sp) {
+template <int F, bool ATT, int HL = 0>
+__global__ __launch_bounds__(kBlock) GAT_OCCUPANCY(ATT) void gat_partial_kernel(GatParams p, GatSplit sp) {
   constexpr int GROUP = F / 4;
   constexpr int RPW = 64 / GROUP;
   const int lane = threadIdx.x & 63;
@@ -456,7 +492,7 @@ __global__ __launch_bounds__(kBlock) void gat_partial_kernel(GatParams p, GatSpl
   if (sg >= sp.n_seg) return;
   float m = -INFINITY, l = 0.f;
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-  gat_accumulate<GROUP, ATT>(p, sp.seg_row[sg], sp.seg_beg[sg], sp.seg_end[sg], gl, m, l, a);
+  gat_accumulate<GROUP, ATT, HL>(p, sp.seg_row[sg], sp.seg_beg[sg], sp.seg_end[sg], gl, m, l, a);
   st4(sp.work + sg * F + 4 * gl, a);
   const int hl = p.o_dim / 4;
   if (gl % hl == 0) {
@@ -470,7 +506,7 @@ __global__ __launch_bounds__(kBlock) void gat_partial_kernel(GatParams p, GatSpl
 // ONCE for all H heads (gat_partial_kernel<H*O> would load it H times, one head per lane
 // group); the partials have gat_partial_kernel's layout, so gat_merge_kernel<H*O> finishes.
 template <int O, int H, int CH, bool ATT>
-__global__ __launch_bounds__(kBlock) void gat_shared_partial_kernel(GatParams p, GatSplit sp) {
+__global__ __launch_bounds__(kBlock) GAT_OCCUPANCY(ATT) void gat_shared_partial_kernel(GatParams p, GatSplit sp) {
   constexpr int GROUP = O / 4;
   constexpr int RPW = 64 / GROUP;
   const int lane = threadIdx.x & 63;
@@ -558,6 +594,33 @@ using namespace gnnrec;
 
 namespace {
 
+// f(integral_constant<F>, integral_constant<HL>) for the instantiated (F, HL) pair of the ATT
+// kernels: F = heads * o_dim in {16 .. 256}, HL = o_dim / 4 in {1 .. 16}, HL <= F / 4
+template <int FF, class Fn>
+void for_hl_f(int hl, Fn&& f) {
+  auto one = [&](auto hc) {
+    if constexpr (decltype(hc)::value <= FF / 4)
+      if (hl == decltype(hc)::value) f(std::integral_constant<int, FF>{}, hc);
+  };
+  one(std::integral_constant<int, 1>{});
+  one(std::integral_constant<int, 2>{});
+  one(std::integral_constant<int, 4>{});
+  one(std::integral_constant<int, 8>{});
+  one(std::integral_constant<int, 16>{});
+}
+
+template <class Fn>
+void for_hl(int F, int hl, Fn&& f) {
+  switch (F) {
+    case 16: for_hl_f<16>(hl, f); break;
+    case 32: for_hl_f<32>(hl, f); break;
+    case 64: for_hl_f<64>(hl, f); break;
+    case 128: for_hl_f<128>(hl, f); break;
+    case 256: for_hl_f<256>(hl, f); break;
+    default: break;
+  }
+}
+
 // checks shared by both score forms; fills the epilogue part of GatParams
 int gat_check_common(int64_t n_rows, int32_t heads, int32_t o_dim, const float* hfeat, int64_t ldh,
                      int64_t head_stride, int32_t mean_heads, float* out, int64_t ldo, int32_t epi,
@@ -613,12 +676,26 @@ int gat_aggregate_launch(const GatParams& p, int64_t n_rows, int heads, int o_di
     }
     return check_launch("gat_aggregate (shared rows)");
   }
+  if constexpr (ATT) {
+    const int hl = o_dim / 4;
+    bool ok = false;
+    for_hl(F, hl, [&](auto fc, auto hc) {
+      constexpr int FF = decltype(fc)::value, HH = decltype(hc)::value;
+      hipLaunchKernelGGL((gat_kernel<FF, true, HH>), grid(FF), dim3(kBlock), 0, s, p);
+      ok = true;
+    });
+    if (!ok) {
+      set_error("gat_att: heads*o_dim = %d with o_dim = %d unsupported", F, o_dim);
+      return GNNREC_EUNSUPPORTED;
+    }
+    return check_launch("gat_aggregate_att");
+  }
   switch (F) {
-    case 16: hipLaunchKernelGGL((gat_kernel<16, ATT>), grid(16), dim3(kBlock), 0, s, p); break;
-    case 32: hipLaunchKernelGGL((gat_kernel<32, ATT>), grid(32), dim3(kBlock), 0, s, p); break;
-    case 64: hipLaunchKernelGGL((gat_kernel<64, ATT>), grid(64), dim3(kBlock), 0, s, p); break;
-    case 128: hipLaunchKernelGGL((gat_kernel<128, ATT>), grid(128), dim3(kBlock), 0, s, p); break;
-    case 256: hipLaunchKernelGGL((gat_kernel<256, ATT>), grid(256), dim3(kBlock), 0, s, p); break;
+    case 16: hipLaunchKernelGGL((gat_kernel<16, false>), grid(16), dim3(kBlock), 0, s, p); break;
+    case 32: hipLaunchKernelGGL((gat_kernel<32, false>), grid(32), dim3(kBlock), 0, s, p); break;
+    case 64: hipLaunchKernelGGL((gat_kernel<64, false>), grid(64), dim3(kBlock), 0, s, p); break;
+    case 128: hipLaunchKernelGGL((gat_kernel<128, false>), grid(128), dim3(kBlock), 0, s, p); break;
+    case 256: hipLaunchKernelGGL((gat_kernel<256, false>), grid(256), dim3(kBlock), 0, s, p); break;
     default: set_error("gat: heads*o_dim = %d unsupported (16..256, power of two)", F); return GNNREC_EUNSUPPORTED;
   }
   return check_launch("gat_aggregate");
@@ -655,10 +732,24 @@ int gat_heavy_launch(const GatParams& p, const GatSplit& sp, int heads, int o_di
     }
     return check_launch("gat_heavy (shared rows)");
   }
+  if constexpr (ATT) {
+    bool ok = false;
+    for_hl(F, o_dim / 4, [&](auto fc, auto hc) {
+      constexpr int FF = decltype(fc)::value, HH = decltype(hc)::value;
+      hipLaunchKernelGGL((gat_partial_kernel<FF, true, HH>), g(sp.n_seg, FF), dim3(kBlock), 0, s, p, sp);
+      hipLaunchKernelGGL(gat_merge_kernel<FF>, dim3((unsigned)sp.n_heavy), dim3(kBlock), 0, s, p, sp);
+      ok = true;
+    });
+    if (!ok) {
+      set_error("gat_heavy_att: heads*o_dim = %d with o_dim = %d unsupported", F, o_dim);
+      return GNNREC_EUNSUPPORTED;
+    }
+    return check_launch("gat_heavy_att");
+  }
   switch (F) {
 #define GAT_HEAVY(FF)                                                                               \
   case FF:                                                                                          \
-    hipLaunchKernelGGL((gat_partial_kernel<FF, ATT>), g(sp.n_seg, FF), dim3(kBlock), 0, s, p, sp);  \
+    hipLaunchKernelGGL((gat_partial_kernel<FF, false>), g(sp.n_seg, FF), dim3(kBlock), 0, s, p, sp); \
     hipLaunchKernelGGL(gat_merge_kernel<FF>, dim3((unsigned)sp.n_heavy), dim3(kBlock), 0, s, p, sp); \
     break;
     GAT_HEAVY(16) GAT_HEAVY(32) GAT_HEAVY(64) GAT_HEAVY(128) GAT_HEAVY(256)

@@ -1,0 +1,46 @@
+"""Config-5 forward time for one libgnnrec build (GNNREC_LIB) and GAT switches (env), for
+same-box A/Bs of the GAT kernels: prints one JSON line tagged with --tag.
+
+    GNNREC_LIB=tools/var/x.so python tools/exp_gat_variants.py --tag x [--shape U I PAIRS]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "gnn-recommendations_amd"), str(ROOT), str(ROOT / "tools")]
+from bench_configs import config5_model, powerlaw_graph  # noqa: E402
+from src.ops.distributed import DistributedGraph, gat_forward_dist  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--tag", required=True)
+ap.add_argument("--shape", type=int, nargs=3, default=[5_000_000, 5_000_000, 250_000_000])
+ap.add_argument("--reps", type=int, default=10)
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+g = powerlaw_graph(*a.shape, 0.9, 0, 16, device=dev)
+m = config5_model(tuple(a.shape[:2]), dev)
+dg = DistributedGraph(g, 0, 1, dev)
+x0 = dg.pad_table(m._initial_table())
+with torch.no_grad():
+    out = gat_forward_dist(dg, m, x0)
+    torch.cuda.synchronize()
+    ms = []
+    for _ in range(a.reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        out = gat_forward_dist(dg, m, x0)
+        e.record()
+        torch.cuda.synchronize()
+        ms.append(s.elapsed_time(e))
+sig = float(out.double().abs().sum())
+print(json.dumps({"tag": a.tag, "lib": os.environ.get("GNNREC_LIB", "default"),
+                  "env": {k: v for k, v in os.environ.items() if k.startswith("GNNREC_GAT")},
+                  "shape": a.shape, "nnz": g.nnz, "ms_median": float(np.median(ms)),
+                  "ms": ms, "abs_sum": sig, "time": time.strftime("%H:%M:%S")}), flush=True)

@@ -36,6 +36,23 @@ case ${1:?call} in
     timeout -k 10 900 python -u tools/bench_configs.py --configs 5 --g1b --steps 5 \
         > $OUT/c2_config5_g1b.jsonl 2> $OUT/c2_config5_g1b.err
     ;;
+  c3)
+    # A/B of the ATT GAT kernel builds (tools/var/gat_*.so, built on the CPU with
+    # tools/build_variant.sh) and the score-table kernels, config 5 at 5M x 5M, same box
+    timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
+        tests/test_gat_att_gpu.py tests/test_real_shapes_gpu.py > $OUT/c3_gat_tests.log 2>&1
+    : > $OUT/c3_gat_variants.jsonl
+    GNNREC_GAT_SCORES_FROM_ROWS=0 timeout -k 10 300 python -u tools/exp_gat_variants.py --tag tables \
+        >> $OUT/c3_gat_variants.jsonl 2> $OUT/c3.err
+    for v in ch16w4 ch8w6 ch8w5 ch16w4_nolds ch16w4; do
+      GNNREC_LIB=tools/var/gat_$v.so timeout -k 10 300 python -u tools/exp_gat_variants.py --tag $v \
+          >> $OUT/c3_gat_variants.jsonl 2>> $OUT/c3.err
+    done
+    GNNREC_GAT_SEGMENT_ORDER=row GNNREC_GAT_XCD_ORDER=0 GNNREC_LIB=tools/var/gat_ch16w4.so \
+        timeout -k 10 300 python -u tools/exp_gat_variants.py --tag ch16w4_roworder >> $OUT/c3_gat_variants.jsonl 2>> $OUT/c3.err
+    GNNREC_GAT_XCD_ORDER=0 GNNREC_LIB=tools/var/gat_ch16w4.so \
+        timeout -k 10 300 python -u tools/exp_gat_variants.py --tag ch16w4_colorder_noxcd >> $OUT/c3_gat_variants.jsonl 2>> $OUT/c3.err
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
