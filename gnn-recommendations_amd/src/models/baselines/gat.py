@@ -38,6 +38,11 @@ GAT_DENSE_MAX_NODES = None
 # (gnnrec_gat_aggregate_att_f32) instead of reading projected score tables per neighbour
 # (DESIGN §3.4, round 5); False keeps the score-table kernels (A/B and tests).
 GAT_SCORES_FROM_ROWS = os.environ.get("GNNREC_GAT_SCORES_FROM_ROWS", "1") != "0"
+
+# Training (autograd on, or attention dropout in training mode) on a native operand runs the
+# native aggregation with its backward (gnnrec_gat_train_*) when the operand's pattern is
+# symmetric; otherwise the reference's dense path, within check_dense_fallback's bound.
+GAT_NATIVE_TRAIN = os.environ.get("GNNREC_GAT_NATIVE_TRAIN", "1") != "0"
 DENSE_FALLBACK_MEM_FRACTION = 0.9
 
 
@@ -251,6 +256,30 @@ class GATLayer(nn.Module):
         return ops.functional.rows_gemm(z, self.head_mean_weight(), apply_elu=apply_elu, epi=epi,
                                         self_rows=self_rows, acc=acc, acc_div=acc_div)
 
+    # ---- training on the native operand (gnnrec_gat_train_*: aggregation + backward) -------
+    def train_ok(self, a) -> bool:
+        """The differentiable native aggregation takes this layer on operand `a`."""
+        return GAT_NATIVE_TRAIN and ops.functional.gat_train_supported(a, self.n_heads,
+                                                                        self.out_dim)
+
+    def native_train_forward(self, x: torch.Tensor, a) -> torch.Tensor:
+        """gat.py:92-151 with autograd: h_q = W_q x, s_self = h_q a_self_q, s_neigh = h_q
+        a_neigh_q in torch (the reference's ops), the masked softmax + dropout + weighted sum
+        per head on the native kernels (their backward included); then concat or head mean.
+        The dropout mask's seed is drawn from torch's generator (torch.manual_seed makes runs
+        repeatable)."""
+        H, o = self.n_heads, self.out_dim
+        h = torch.cat([w(x) for w in self.W], dim=1)                       # [N, H*o]
+        hs = h.view(-1, H, o)
+        a_s = torch.stack([a[:, 0] for a in self.a_self])                  # [H, o]
+        a_n = torch.stack([a[:, 0] for a in self.a_neigh])
+        s_self = (hs * a_s).sum(-1)                                        # [N, H]
+        s_neigh = (hs * a_n).sum(-1)
+        p = self.dropout if self.training else 0.0
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if p > 0 else 0
+        out = ops.functional.gat_aggregate_train(a, h, s_self, s_neigh, H, o, self.alpha, p, seed)
+        return out if self.concat_heads else out.view(-1, H, o).mean(dim=1)
+
     def native_inputs(self, x: torch.Tensor):
         """(table gathered per neighbour, s_self, s_neigh) for the rows of x."""
         if self.shares_input():
@@ -284,6 +313,9 @@ class GATLayer(nn.Module):
                                                self_rows=self_rows, acc=acc, acc_div=acc_div)
             return self.native_forward(a, *self.native_inputs(x), apply_elu=apply_elu, epi=epi,
                                        self_rows=self_rows, acc=acc, acc_div=acc_div)
+        if self.train_ok(a):
+            out = self.native_train_forward(x, a)
+            return F.elu(out) if apply_elu else out
         if isinstance(a, CsrGraph):
             grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
             check_dense_fallback(a.shape[0], why, heads=self.n_heads, grad=grad,

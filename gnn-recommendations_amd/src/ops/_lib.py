@@ -104,6 +104,11 @@ _SIGNATURES = {
     "gnnrec_gat_heavy_att_f32": [_p, _p, _p, _p, _i64, _p, _p, _i64, _p, _p, _i64, _i64, _p,
                                  _i64, _p, _i32, _i32, _f32, _i32, _i32, _p, _i64, _i32, _p, _i64,
                                  _p, _i64, _f32, _p, _i32, _p],
+    "gnnrec_gat_train_forward_f32": [_p, _p, _i64, _p, _i64, _p, _p, _i64, _i32, _i32, _f32,
+                                     _f32, C.c_uint32, _p, _i64, _p],
+    "gnnrec_gat_train_backward_f32": [_p, _p, _i64, _p, _i64, _p, _p, _i64, _i32, _i32, _f32,
+                                      _f32, C.c_uint32, _p, _i64, _p, _i64, _p, _p, _i64, _p, _p,
+                                      _p],
     "gnnrec_score_topk_f32": [_p, _i64, _i64, _p, _i64, _i64, _i32, _p, _p, _i32, _p, _p, _p],
     "gnnrec_score_topk_split_f32": [_p, _i64, _i64, _p, _i64, _i64, _i32, _p, _p, _i32, _i32,
                                     _p, _p, _p, _p, _p],

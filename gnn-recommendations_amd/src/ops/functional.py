@@ -775,6 +775,71 @@ def gat_aggregate_att(adj: CsrGraph, h: torch.Tensor, hself: torch.Tensor, att: 
     return out
 
 
+# ---- GAT training (gnnrec_gat_train_forward_f32 / _backward_f32, csrc/gat_train.hip) ---------
+def gat_train_supported(adj: CsrGraph, heads: int, o_dim: int) -> bool:
+    """The native differentiable GAT aggregation applies: a square operand with a symmetric
+    pattern on a ROCm device (its backward walks the columns as rows), heads * o_dim in
+    {16 .. 256} and o_dim / 4 a power of two."""
+    q = o_dim // 4
+    return (isinstance(adj, CsrGraph) and adj.device.type == "cuda"
+            and o_dim % 4 == 0 and q >= 1 and (q & (q - 1)) == 0
+            and heads * o_dim in (16, 32, 64, 128, 256) and adj.pattern_symmetric())
+
+
+class _GatTrainAggregate(torch.autograd.Function):
+    """out[:, q*o:(q+1)*o] = dropout(softmax_j(LeakyReLU(s_self[r,q] + s_neigh[j,q]))) @ h_q —
+    one GATLayer's per-head aggregation (gat.py:113-141) with its backward in two native passes;
+    h, s_self and s_neigh are the differentiable inputs (the projections stay in autograd)."""
+
+    @staticmethod
+    def forward(ctx, h, s_self, s_neigh, adj, heads, o_dim, slope, drop_p, seed):
+        h, s_self, s_neigh = h.contiguous(), s_self.contiguous(), s_neigh.contiguous()
+        n = adj.n_rows
+        out = torch.empty((n, heads * o_dim), dtype=torch.float32, device=h.device)
+        check(_lib.lib().gnnrec_gat_train_forward_f32(
+            ptr(adj.row_ptr), ptr(adj.col), n, ptr(h), h.stride(0), ptr(s_self), ptr(s_neigh),
+            s_self.stride(0), int(heads), int(o_dim), float(slope), float(drop_p), int(seed),
+            ptr(out), out.stride(0), _lib.stream_of(adj.device)), "gnnrec_gat_train_forward_f32")
+        ctx.save_for_backward(h, s_self, s_neigh, out)
+        ctx.cfg = (adj, int(heads), int(o_dim), float(slope), float(drop_p), int(seed))
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        h, s_self, s_neigh, out = ctx.saved_tensors
+        adj, heads, o_dim, slope, drop_p, seed = ctx.cfg
+        dout = dout.contiguous()
+        n = adj.n_rows
+        dh = torch.empty_like(h)
+        d_self = torch.empty_like(s_self)
+        d_neigh = torch.empty_like(s_neigh)
+        stats = torch.empty(n * heads * 4 + 4, dtype=torch.float32, device=h.device)
+        check(_lib.lib().gnnrec_gat_train_backward_f32(
+            ptr(adj.row_ptr), ptr(adj.col), n, ptr(h), h.stride(0), ptr(s_self), ptr(s_neigh),
+            s_self.stride(0), heads, o_dim, slope, drop_p, seed, ptr(out), out.stride(0),
+            ptr(dout), dout.stride(0), ptr(stats), ptr(dh), dh.stride(0), ptr(d_self),
+            ptr(d_neigh), _lib.stream_of(adj.device)), "gnnrec_gat_train_backward_f32")
+        return dh, d_self, d_neigh, None, None, None, None, None, None
+
+
+def gat_aggregate_train(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor,
+                        s_neigh: torch.Tensor, heads: int, o_dim: int, slope: float = 0.2,
+                        drop_p: float = 0.0, seed: int = 0) -> torch.Tensor:
+    """Differentiable per-head GAT aggregation on the native kernels: h [N, heads*o_dim]
+    (head-major), s_self / s_neigh [N, heads]; attention dropout drop_p with a counter-based
+    mask of `seed` (regenerated by the backward). Returns [N, heads*o_dim] (heads
+    concatenated)."""
+    if not gat_train_supported(adj, heads, o_dim):
+        raise ValueError("gat_aggregate_train: needs a symmetric square CsrGraph on a ROCm "
+                         "device, heads*o_dim in {16..256}, o_dim/4 a power of two")
+    _require_device(adj, h, s_self, s_neigh)
+    if h.shape != (adj.n_rows, heads * o_dim) or s_self.shape != (adj.n_rows, heads) \
+            or s_neigh.shape != (adj.n_rows, heads):
+        raise ValueError("gat_aggregate_train: h [N, heads*o_dim], s_self / s_neigh [N, heads]")
+    return _GatTrainAggregate.apply(h.float(), s_self.float(), s_neigh.float(), adj, heads,
+                                    o_dim, slope, drop_p, seed & 0xFFFFFFFF)
+
+
 def rows_gemm_supported(k: int, p: int) -> bool:
     """(k, p) shapes gnnrec_rows_gemm_f32 has an instance for (csrc/dense_epi.hip)."""
     return k in (64, 128, 256) and p % 4 == 0 and 0 < p <= (80 if k == 64 else 64)

@@ -117,7 +117,26 @@ class CsrGraph:
         f = self._plans.get("degree_factors")
         if f is not None:   # a shard's factors come from its full graph (shard())
             g._plans["degree_factors"] = tuple(t.to(device) for t in f)
+        if "pattern_sym" in self._plans:
+            g._plans["pattern_sym"] = self._plans["pattern_sym"]
         return g
+
+    def pattern_symmetric(self) -> bool:
+        """The sparsity pattern equals its transpose's (values ignored; cached): True without
+        a check for the interaction graphs the builders make (both directions stored,
+        graph_builder.py:52-61), else compared with t() once. The native GAT backward walks
+        a node's row as the list of rows that aggregate it, which needs this."""
+        if "pattern_sym" not in self._plans:
+            if self.shard_info is not None or self.shape[0] != self.shape[1]:
+                v = False
+            elif self.symmetric:
+                v = True
+            else:
+                tt = self.t()
+                v = bool(torch.equal(tt.row_ptr.cpu(), self.row_ptr.cpu())
+                         and torch.equal(tt.col.cpu(), self.col.cpu()))
+            self._plans["pattern_sym"] = v
+        return self._plans["pattern_sym"]
 
     def cuda(self, device=None) -> "CsrGraph":
         return self.to(torch.device("cuda") if device is None else torch.device("cuda", device)
@@ -188,6 +207,7 @@ class CsrGraph:
             nnz == 0 or np.all(np.frexp(cnt)[0] == 0.5)))
         g = cls(torch.from_numpy(row_ptr), torch.from_numpy(col), torch.from_numpy(val), (N, N),
                 int(n_users), int(n_items), symmetric=sym)
+        g._plans["pattern_sym"] = True      # both directions of every pair are stored
         return g.to(device)
 
     @classmethod
@@ -240,8 +260,10 @@ class CsrGraph:
                 "normalize_values_device")
         sym = normalization == "none" or (normalization == "symmetric" and bool(
             nz == 0 or torch.all(torch.frexp(cnt).mantissa == 0.5)))   # as from_interactions
-        return cls(row_ptr, col.clone(), val.clone(),
-                   (N, N), int(n_users), int(n_items), symmetric=sym)
+        g = cls(row_ptr, col.clone(), val.clone(), (N, N), int(n_users), int(n_items),
+                symmetric=sym)
+        g._plans["pattern_sym"] = True      # both directions of every pair are stored
+        return g
 
     @classmethod
     def from_scipy(cls, adj, n_users: Optional[int] = None, n_items: Optional[int] = None,

@@ -438,6 +438,33 @@ int gnnrec_gat_heavy_att_f32(const int32_t* col, const int64_t* seg_row, const i
  * row-grouped). xcd_order = 1: XCD x runs the x-th eighth of the segment list (blocks are
  * otherwise dealt round-robin to the 8 XCDs, spreading neighbouring segments over 8 L2s). */
 
+/* ---- f1 for GAT: the training aggregation and its backward (csrc/gat_train.hip) ----------
+ * Forward: out[r, q*o:(q+1)*o] = sum_j alpha_rjq keep_rjq / (1 - drop_p) hfeat[j, q*o:(q+1)*o]
+ * with alpha = softmax over the row's neighbours of LeakyReLU_slope(s_self[r, q] +
+ * s_neigh[j, q]) (gat.py:113-141) and keep a Bernoulli(1 - drop_p) draw of a counter-based hash
+ * of (seed, r, j, q) — the reference's F.dropout on the attention weights, gat.py:137 —
+ * regenerated (not stored) by the backward. hfeat: the head-major [N, heads*o_dim] table
+ * (ldh), s_self / s_neigh: [N, heads] (row stride ld_s); out [n_rows, heads*o_dim] (ldo).
+ * No heavy-row split, no epilogue (the caller's autograd applies head mean / ELU / layer mean).
+ * Backward (two passes over the CSR; the pattern must be SYMMETRIC, as the normalised
+ * bipartite adjacency is: row j lists the rows that aggregate j): given dout, writes
+ * dh [n, heads*o_dim] (lddh), d_self and d_neigh [n, heads] (contiguous); stats is a scratch of
+ * n_rows * heads * 4 floats (softmax max / sum / g.out per row and head). fp32, any order
+ * (tolerance-level vs the reference's dense autograd). heads*o_dim in {16 .. 256}, o_dim / 4 a
+ * power of two. */
+int gnnrec_gat_train_forward_f32(const int64_t* row_ptr, const int32_t* col, int64_t n_rows,
+                                 const float* hfeat, int64_t ldh, const float* s_self,
+                                 const float* s_neigh, int64_t ld_s, int32_t heads, int32_t o_dim,
+                                 float slope, float drop_p, uint32_t seed, float* out, int64_t ldo,
+                                 gnnrec_stream_t stream);
+int gnnrec_gat_train_backward_f32(const int64_t* row_ptr, const int32_t* col, int64_t n_rows,
+                                  const float* hfeat, int64_t ldh, const float* s_self,
+                                  const float* s_neigh, int64_t ld_s, int32_t heads, int32_t o_dim,
+                                  float slope, float drop_p, uint32_t seed, const float* out,
+                                  int64_t ldo, const float* dout, int64_t lddo, float* stats,
+                                  float* dh, int64_t lddh, float* d_self, float* d_neigh,
+                                  gnnrec_stream_t stream);
+
 /* Dense projections of the GAT layer (gat.py:113-118 W_h x and the attention halves, one
  * fused weight; and the head-averaged last layer's W_h applied after the aggregation,
  * gat.py:149): y[r, :p] = x[r, :k] @ B[k, p], B row-major [k][p], on the matrix cores

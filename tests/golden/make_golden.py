@@ -335,6 +335,34 @@ def make_gat_heavy(gb, GAT):
           f"{int((deg > 2048).sum())} rows > 2048")
 
 
+def make_gat_grad(gb, GAT):
+    """GAT training gradients (gat.py:76-151 dense masked softmax, 258-297) for the native
+    backward (csrc/gat_train.hip): the gat_d64_h4 graph and model seed, dropout 0 (the
+    reference's F.dropout draws cannot be reproduced natively), train() mode, loss =
+    sum(user_out * Ru) + sum(item_out * Ri) with seeded Ru, Ri; every parameter's gradient."""
+    import torch
+    gu, gi = interactions(41, 60, 80, 500, min_deg=True)
+    _, _, gt = ref_graph(gb, gu, gi, 60, 80)
+    torch.manual_seed(42)
+    m = GAT(60, 80, embedding_dim=64, n_layers=3, n_heads=4, dropout=0.0, alpha=0.2,
+            init_scale=0.1)
+    m.train()
+    ue, ie = m(gt)
+    rng = np.random.default_rng(43)
+    Ru = torch.from_numpy(rng.standard_normal(ue.shape).astype(np.float32))
+    Ri = torch.from_numpy(rng.standard_normal(ie.shape).astype(np.float32))
+    loss = (ue * Ru).sum() + (ie * Ri).sum()
+    loss.backward()
+    arrs = dict(users=gu, items=gi, n_users=60, n_items=80, Ru=Ru.numpy(), Ri=Ri.numpy(),
+                loss=np.float64(loss.item()), user_out=ue.detach().numpy(),
+                item_out=ie.detach().numpy())
+    for name, prm in m.named_parameters():
+        arrs["grad." + name] = prm.grad.detach().numpy()
+        arrs["param." + name] = prm.detach().numpy()
+    np.savez(OUT / "gat_grad_d64_h4.npz", **arrs)
+    print(f"gat_grad: loss {loss.item():.6f}, {len(list(m.parameters()))} parameter gradients")
+
+
 def make_emb_stats():
     """The over-smoothing statistics Evaluator.evaluate adds (evaluator.py:116-121 ->
     training/metrics.py:229-315) on a table with a zero row and two identical rows."""
@@ -353,7 +381,7 @@ def main():
     import torch
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="", help="comma list: long_rows, edge_paths, emb_stats, "
-                                               "ml1m_models, gat_heavy")
+                                               "ml1m_models, gat_heavy, gat_grad")
     only = set(filter(None, ap.parse_args().only.split(",")))
     gb, LightGCN, NGCF, GAT, GSL, BCL, OBG = _import_reference()
     torch.set_num_threads(1)
@@ -370,6 +398,8 @@ def main():
             make_ml1m_models(gb, NGCF, GSL, OBG)
         if "gat_heavy" in only:
             make_gat_heavy(gb, GAT)
+        if "gat_grad" in only:
+            make_gat_grad(gb, GAT)
         return
     meta = dict(torch=torch.__version__, numpy=np.__version__)
     import scipy
@@ -556,6 +586,7 @@ def main():
     make_emb_stats()
     make_ml1m_models(gb, NGCF, GSL, OBG)
     make_gat_heavy(gb, GAT)
+    make_gat_grad(gb, GAT)
 
     with open(OUT / "VERSIONS.txt", "w") as f:
         for k, v in meta.items():
