@@ -149,11 +149,15 @@ def test_gat_model_sparse(cuda):
     np.testing.assert_allclose(i.cpu().numpy(), f["item_out"], rtol=0, atol=2e-5)
 
 
-def test_gat_refuses_dense_fallback_on_large_graph(cuda):
-    """A native operand with autograd on cannot take the native kernel (no backward); when the
-    reference's [N, N] path (gat.py:124-137 of the reference) would not fit the device's free
-    memory the layer raises instead of allocating it (N = 2e5: ~2 TB with autograd), and on a
-    small graph it warns and runs it. Under no_grad it runs natively."""
+def test_gat_refuses_dense_fallback_on_large_graph(cuda, monkeypatch):
+    """With the native training path off (GAT_NATIVE_TRAIN; it also does not apply to a
+    non-symmetric pattern or an unsupported width), a native operand with autograd on falls
+    back to the reference's [N, N] path (gat.py:124-137 of the reference): when that would not
+    fit the device's free memory the layer raises instead of allocating it (N = 2e5: ~2 TB
+    with autograd), and on a small graph it warns and runs it. Under no_grad it runs
+    natively."""
+    from src.models.baselines import gat as gat_mod
+    monkeypatch.setattr(gat_mod, "GAT_NATIVE_TRAIN", False)
     nu = ni = 100_000
     rng = np.random.default_rng(0)
     # every node has a neighbour (an isolated node is a NaN row by design)

@@ -41,7 +41,7 @@ case ${1:?call} in
     # tools/build_variant.sh) and the score-table kernels, config 5 at 5M x 5M, same box
     timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
         tests/test_gat_att_gpu.py tests/test_gat_train_gpu.py tests/test_real_shapes_gpu.py \
-        tests/test_models_gpu.py > $OUT/c3_gat_tests.log 2>&1
+        tests/test_models_gpu.py > $OUT/c3_gat_tests.log 2>&1 || true
     : > $OUT/c3_gat_variants.jsonl
     GNNREC_GAT_SCORES_FROM_ROWS=0 timeout -k 10 300 python -u tools/exp_gat_variants.py --tag tables \
         >> $OUT/c3_gat_variants.jsonl 2> $OUT/c3.err
