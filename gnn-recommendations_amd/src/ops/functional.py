@@ -713,6 +713,10 @@ def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh:
 # contiguous eighth of that list.
 GAT_SEGMENT_ORDER = os.environ.get("GNNREC_GAT_SEGMENT_ORDER", "column")
 GAT_XCD_ORDER = os.environ.get("GNNREC_GAT_XCD_ORDER", "1") != "0"
+# "panel": the heaviest rows (>= GAT_PANEL_MIN_EDGES edges per GAT_PANEL-column panel on
+# average) are cut at panel boundaries (CsrGraph.heavy_plan_panels)
+GAT_PANEL = int(os.environ.get("GNNREC_GAT_PANEL", "8192"))
+GAT_PANEL_MIN_EDGES = int(os.environ.get("GNNREC_GAT_PANEL_MIN_EDGES", "64"))
 
 
 def gat_att_supported(o_dim: int) -> bool:
@@ -750,8 +754,13 @@ def gat_aggregate_att(adj: CsrGraph, h: torch.Tensor, hself: torch.Tensor, att: 
         out = torch.empty((adj.n_rows, width), dtype=torch.float32, device=h.device)
     plan = None
     if heavy_threshold > 0:
-        plan = (adj.heavy_plan_by_column(heavy_threshold, GAT_SEGMENT)
-                if GAT_SEGMENT_ORDER == "column" else adj.heavy_plan(heavy_threshold, GAT_SEGMENT))
+        if GAT_SEGMENT_ORDER == "panel":
+            plan = adj.heavy_plan_panels(heavy_threshold, GAT_SEGMENT, GAT_PANEL,
+                                         GAT_PANEL_MIN_EDGES)
+        elif GAT_SEGMENT_ORDER == "column":
+            plan = adj.heavy_plan_by_column(heavy_threshold, GAT_SEGMENT)
+        else:
+            plan = adj.heavy_plan(heavy_threshold, GAT_SEGMENT)
     common = (ptr(h), h.stride(0), head_stride, ptr(hself), hself.stride(0), ptr(att),
               int(heads), int(o_dim), float(slope), int(mean_heads), int(apply_elu), ptr(out),
               out.stride(0) if out is not None else width, int(epi), ptr(self_rows),

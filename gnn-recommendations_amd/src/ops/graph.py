@@ -717,6 +717,74 @@ class CsrGraph:
                     seg_end=base["seg_end"][order].contiguous(), seg_pos=pos.contiguous())
         return self._plans[key]
 
+    def heavy_plan_panels(self, threshold: int, seg_len: int, panel: int, min_per_panel: int):
+        """heavy_plan_by_column with the heaviest rows cut at column-panel boundaries: a heavy
+        row with at least `min_per_panel` edges per `panel`-column panel on average gets one
+        segment per (panel, seg_len edges) run instead of equal-length segments, so the
+        segments of every such row over one panel start in that panel and — sorted by first
+        column — run together while that panel's gathered lines sit in L2 (cached). The other
+        heavy rows keep heavy_plan's equal-length cut. Same output layout as
+        heavy_plan_by_column."""
+        key = ("heavy_pan", threshold, seg_len, panel, min_per_panel)
+        if key not in self._plans:
+            base = self.heavy_plan(threshold, seg_len)
+            if base is None:
+                self._plans[key] = None
+                return None
+            rp, col = self.row_ptr, self.col
+            dev = rp.device
+            heavy = base["heavy_rows"]
+            deg = rp[heavy + 1] - rp[heavy]
+            n_panels = max(1, -(-self.shape[1] // panel))
+            cut = deg >= min_per_panel * n_panels
+            # equal-length segments of the other heavy rows (heavy_plan's, row by row)
+            keep_seg = ~cut[torch.repeat_interleave(torch.arange(heavy.numel(), device=dev),
+                                                    base["heavy_seg_ptr"][1:] -
+                                                    base["heavy_seg_ptr"][:-1])]
+            segs = [(base["seg_row"][keep_seg], base["seg_beg"][keep_seg],
+                     base["seg_end"][keep_seg])]
+            rows = heavy[cut]
+            if rows.numel():
+                beg, end = rp[rows], rp[rows + 1]
+                lens = end - beg
+                total = int(lens.sum())
+                start = torch.zeros(rows.numel() + 1, dtype=torch.int64, device=dev)
+                start[1:] = torch.cumsum(lens, 0)
+                e = torch.repeat_interleave(beg - start[:-1], lens, output_size=total) + \
+                    torch.arange(total, device=dev)                   # edge ids, row by row
+                rid = torch.repeat_interleave(rows, lens, output_size=total)
+                pan = col[e].to(torch.int64) // panel
+                first = torch.ones(total, dtype=torch.bool, device=dev)
+                first[1:] = (rid[1:] != rid[:-1]) | (pan[1:] != pan[:-1])
+                run = torch.cumsum(first.to(torch.int64), 0) - 1
+                run_start = torch.nonzero(first).flatten()
+                brk = first | ((torch.arange(total, device=dev) - run_start[run]) % seg_len == 0)
+                bpos = torch.nonzero(brk).flatten()
+                nxt = torch.empty_like(bpos)
+                nxt[:-1] = bpos[1:]
+                nxt[-1] = total
+                segs.append((rid[bpos], e[bpos], e[nxt - 1] + 1))
+                del e, rid, pan, first, run, run_start, brk
+            seg_row = torch.cat([t[0] for t in segs])
+            seg_beg = torch.cat([t[1] for t in segs])
+            seg_end = torch.cat([t[2] for t in segs])
+            # row-grouped numbering for the merge (heavy rows ascending, segments by position)
+            grp = torch.sort(seg_beg, stable=True).indices          # CSR order = row order
+            seg_row, seg_beg, seg_end = seg_row[grp], seg_beg[grp], seg_end[grp]
+            counts = torch.zeros(heavy.numel(), dtype=torch.int64, device=dev)
+            counts.index_add_(0, torch.searchsorted(heavy, seg_row),
+                              torch.ones_like(seg_row))
+            seg_ptr = torch.zeros(heavy.numel() + 1, dtype=torch.int64, device=dev)
+            seg_ptr[1:] = torch.cumsum(counts, 0)
+            order = torch.sort(col[seg_beg].to(torch.int64), stable=True).indices
+            pos = torch.empty_like(order)
+            pos[order] = torch.arange(order.numel(), device=dev)
+            self._plans[key] = dict(
+                heavy_rows=heavy, heavy_seg_ptr=seg_ptr, seg_row=seg_row[order].contiguous(),
+                seg_beg=seg_beg[order].contiguous(), seg_end=seg_end[order].contiguous(),
+                seg_pos=pos.contiguous(), n_cut_rows=int(cut.sum()))
+        return self._plans[key]
+
     def __repr__(self) -> str:  # keep it short: the tensors are huge
         return (f"CsrGraph(shape={self.shape}, nnz={self.nnz}, device={self.device}, "
                 f"symmetric={self.symmetric}, shard={self.shard_info})")

@@ -190,3 +190,34 @@ def test_att_segment_order_and_xcd_blocks_keep_the_bits(cuda, monkeypatch, share
         np.testing.assert_array_equal(v.cpu().numpy().view(np.uint32), base, err_msg=str(k))
     np.testing.assert_allclose(outs["column", True].cpu().numpy(),
                                _oracle(g, feat, att, heads, o, shared), rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("shared", [False, True])
+def test_att_panel_cut_segments_vs_oracle(cuda, monkeypatch, shared):
+    """Heavy rows cut at column-panel boundaries (heavy_plan_panels: every such row's
+    segments start in one panel, then sorted by first column) give the oracle's aggregation;
+    every heavy edge is in exactly one segment."""
+    monkeypatch.setattr(F, "GAT_SEGMENT_ORDER", "panel")
+    monkeypatch.setattr(F, "GAT_PANEL", 16)
+    monkeypatch.setattr(F, "GAT_PANEL_MIN_EDGES", 2)
+    monkeypatch.setattr(F, "GAT_SEGMENT", 9)
+    g, gd = _graph(cuda, seed=23, nu=500, ni=400, n=40000)
+    n, heads, o = g.shape[0], 4, (64 if shared else 16)
+    torch.manual_seed(2)
+    feat = torch.randn(n, o if shared else heads * o, device=cuda) * 0.3
+    att = torch.randn(2, heads, o, device=cuda) * 0.4
+    z = F.gat_aggregate_att(gd, feat, feat, att, heads, o, 0.2, shared_rows=shared,
+                            heavy_threshold=100)
+    plan = gd.heavy_plan_panels(100, 9, 16, 2)
+    assert plan["n_cut_rows"] > 0
+    beg, end = plan["seg_beg"].cpu().numpy(), plan["seg_end"].cpu().numpy()
+    rp = g.row_ptr.numpy()
+    heavy = plan["heavy_rows"].cpu().numpy()
+    assert (end - beg).sum() == (rp[heavy + 1] - rp[heavy]).sum()
+    covered = np.zeros(g.nnz, np.int64)
+    for b, e in zip(beg, end):
+        covered[b:e] += 1
+    hv = np.concatenate([np.arange(rp[r], rp[r + 1]) for r in heavy])
+    assert np.all(covered[hv] == 1)
+    np.testing.assert_allclose(z.cpu().numpy(), _oracle(g, feat, att, heads, o, shared),
+                               rtol=1e-4, atol=1e-6)

@@ -1,0 +1,48 @@
+"""Heavy-row segment plans of the GAT kernels (CsrGraph.heavy_plan, heavy_plan_by_column,
+heavy_plan_panels) on the CPU: every heavy edge in exactly one segment, the merge's
+row-grouped numbering (heavy_seg_ptr through seg_pos) lists each row's own segments, the
+execution order is by first column, and panel-cut rows never cross a panel or exceed the
+segment length."""
+import numpy as np
+import pytest
+
+from src.ops import CsrGraph
+
+
+def _zipf_graph(seed=23, nu=500, ni=400, n=40000):
+    rng = np.random.default_rng(seed)
+    u = rng.integers(0, nu, n)
+    i = np.minimum(rng.zipf(1.3, n) - 1, ni - 1)
+    u = np.concatenate([u, np.arange(nu), rng.integers(0, nu, ni)])
+    i = np.concatenate([i, rng.integers(0, ni, nu), np.arange(ni)])
+    return CsrGraph.from_interactions(u, i, nu, ni)
+
+
+@pytest.mark.parametrize("kind,args", [("column", (100, 9)), ("panel", (100, 9, 16, 2)),
+                                       ("panel", (100, 1024, 64, 4)), ("panel", (50, 7, 8, 1))])
+def test_heavy_plans_cover_every_heavy_edge_once(kind, args):
+    g = _zipf_graph()
+    plan = g.heavy_plan_by_column(*args) if kind == "column" else g.heavy_plan_panels(*args)
+    rp, col = g.row_ptr.numpy(), g.col.numpy()
+    heavy = plan["heavy_rows"].numpy()
+    beg, end = plan["seg_beg"].numpy(), plan["seg_end"].numpy()
+    srow, pos, ptr = plan["seg_row"].numpy(), plan["seg_pos"].numpy(), plan["heavy_seg_ptr"].numpy()
+    assert np.all(end > beg)
+    cov = np.zeros(g.nnz, np.int64)
+    for b, e in zip(beg, end):
+        cov[b:e] += 1
+    hv = np.concatenate([np.arange(rp[r], rp[r + 1]) for r in heavy])
+    assert np.all(cov[hv] == 1) and cov.sum() == hv.size
+    for h, r in enumerate(heavy):                      # the merge's numbering
+        js = pos[ptr[h]:ptr[h + 1]]
+        assert np.all(srow[js] == r) and np.all((beg[js] >= rp[r]) & (end[js] <= rp[r + 1]))
+    assert np.all(np.diff(col[beg]) >= 0)              # execution order: first column
+    if kind == "panel":
+        _, seg_len, panel, min_pp = args
+        deg = rp[heavy + 1] - rp[heavy]
+        n_pan = -(-g.shape[1] // panel)
+        cut = set(heavy[deg >= min_pp * n_pan].tolist())
+        assert plan["n_cut_rows"] == len(cut) and len(cut) > 0
+        for b, e, r in zip(beg, end, srow):
+            if r in cut:
+                assert col[b] // panel == col[e - 1] // panel and e - b <= seg_len

@@ -54,6 +54,15 @@ case ${1:?call} in
     GNNREC_GAT_XCD_ORDER=0 GNNREC_LIB=tools/var/gat_ch16w4.so \
         timeout -k 10 300 python -u tools/exp_gat_variants.py --tag ch16w4_colorder_noxcd >> $OUT/c3_gat_variants.jsonl 2>> $OUT/c3.err
     ;;
+  c4)
+    # the chosen ATT build: G1B kernel trace (checked run before it), and the GAT kernels'
+    # L2 hit / miss at 5M x 5M
+    timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c4_g1bkt -o run -- \
+        python3 tools/bench_configs.py --configs 5 --g1b --steps 3 --warmup 1 --no-ref-check \
+        > $OUT/c4_g1bkt.jsonl 2> $OUT/c4_g1bkt.err
+    timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/c4_c5l2 -o run -- \
+        python3 tools/bench_configs.py $C5 --steps 3 --warmup 1 --no-ref-check > $OUT/c4_c5l2.jsonl 2> $OUT/c4_c5l2.err
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
