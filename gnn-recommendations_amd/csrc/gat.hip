@@ -267,7 +267,7 @@ __device__ __forceinline__ void gat_apply16(std::integer_sequence<int, T...>, fl
 // an[h * 16 + gl])
 template <class AN>
 __device__ __forceinline__ float4 an_of(const AN& an, int h, int gl) {
-  if constexpr (std::is_pointer_v<std::decay_t<AN>>) return an[h * 16 + gl];
+  if constexpr (std::is_pointer_v<AN>) return an[h * 16 + gl];   // AN = float4[4]: no decay
   else return an[h];
 }
 

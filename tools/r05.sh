@@ -63,6 +63,22 @@ case ${1:?call} in
     timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/c4_c5l2 -o run -- \
         python3 tools/bench_configs.py $C5 --steps 3 --warmup 1 --no-ref-check > $OUT/c4_c5l2.jsonl 2> $OUT/c4_c5l2.err
     ;;
+  c5)
+    # heavy-row segment plans, same box: equal-length by first column (default) vs panel-cut
+    : > $OUT/c5_gat_panels.jsonl
+    timeout -k 10 300 python -u tools/exp_gat_variants.py --tag column >> $OUT/c5_gat_panels.jsonl 2> $OUT/c5.err
+    for pp in "8192 64" "16384 64" "4096 64" "8192 256" "32768 64"; do
+      set -- $pp
+      GNNREC_GAT_SEGMENT_ORDER=panel GNNREC_GAT_PANEL=$1 GNNREC_GAT_PANEL_MIN_EDGES=$2 \
+          timeout -k 10 300 python -u tools/exp_gat_variants.py --tag panel_$1_$2 \
+          >> $OUT/c5_gat_panels.jsonl 2>> $OUT/c5.err
+    done
+    timeout -k 10 300 python -u tools/exp_gat_variants.py --tag column >> $OUT/c5_gat_panels.jsonl 2>> $OUT/c5.err
+    GNNREC_LIB=tools/var/gat_ch16w4_nolds.so timeout -k 10 300 python -u tools/exp_gat_variants.py \
+        --tag nolds_fixed >> $OUT/c5_gat_panels.jsonl 2>> $OUT/c5.err
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c5_c5kt -o run -- \
+        python3 tools/bench_configs.py $C5 --steps 3 --warmup 1 --no-ref-check > $OUT/c5_c5kt.jsonl 2> $OUT/c5_c5kt.err
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
