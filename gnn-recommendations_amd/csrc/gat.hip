@@ -97,6 +97,10 @@ __device__ __forceinline__ void gat_finish(const GatParams& p, int64_t r, float4
 #define GAT_ATT_CHUNK 16
 #endif
 #define GAT_OCCUPANCY(ATT) __attribute__((amdgpu_waves_per_eu((ATT) ? GAT_ATT_WAVES : 1)))
+#ifndef GAT_SHARED_WAVES
+#define GAT_SHARED_WAVES GAT_ATT_WAVES
+#endif
+#define GAT_SHARED_OCCUPANCY(ATT) __attribute__((amdgpu_waves_per_eu((ATT) ? GAT_SHARED_WAVES : 1)))
 
 constexpr int kSoftBlock = 8;
 constexpr float kLog2e = 1.4426950408889634f;
@@ -263,6 +267,9 @@ __device__ __forceinline__ void gat_apply16(std::integer_sequence<int, T...>, fl
 #ifndef GAT_ATT_LDS
 #define GAT_ATT_LDS 1
 #endif
+#ifndef GAT_SHARED_PIPE
+#define GAT_SHARED_PIPE 0
+#endif
 // an: the 4 heads' neighbour vectors, this lane's float4 of each (registers: an[h]; LDS:
 // an[h * 16 + gl])
 template <class AN>
@@ -322,15 +329,34 @@ __device__ __forceinline__ void gat_shared_rows16(const GatParams& p, int64_t r,
     for (int h = 0; h < 4; ++h) an[h] = ld4(p.att + (4 + h) * 64 + 4 * gl);
   }
 #endif
-  for (int64_t k0 = beg; k0 < end; k0 += 8) {
+  auto load_block = [&](int64_t k0, float4 (&dst)[8]) {
     int64_t k = k0 + gl;
     k = k < end ? k : end - 1;
     const int cm = p.A.col[k];
-    float4 xv[8];
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       const int c = __shfl(cm, t, 16);
-      xv[t] = ld4(p.h + (int64_t)c * p.ldh + 4 * gl);
+      dst[t] = ld4(p.h + (int64_t)c * p.ldh + 4 * gl);
+    }
+  };
+  // ATT + GAT_SHARED_PIPE: the next block's rows are in flight while this block's scores,
+  // reduce-scatter and weighted sums run (the ATT form has twice the VALU work per
+  // neighbour of the score-table form, so without it the loads wait behind the compute)
+  constexpr bool kPipe = ATT && GAT_SHARED_PIPE;
+  float4 xv[8];
+  if constexpr (kPipe) load_block(beg, xv);
+  for (int64_t k0 = beg; k0 < end; k0 += 8) {
+    float4 xn[8];
+    if constexpr (kPipe) {
+      if (k0 + 8 < end) load_block(k0 + 8, xn);
+    } else {
+      load_block(k0, xv);
+    }
+    int cm = 0;
+    if constexpr (!ATT) {
+      int64_t k = k0 + gl;
+      k = k < end ? k : end - 1;
+      cm = p.A.col[k];
     }
     float sna, snb;
     if constexpr (ATT) {
@@ -363,6 +389,10 @@ __device__ __forceinline__ void gat_shared_rows16(const GatParams& p, int64_t r,
     const float pa = gat_exp2(ea - (hi ? mn[2] : mn[0]));
     const float pb = gat_exp2(eb - (hi ? mn[3] : mn[1]));
     gat_apply16(std::make_integer_sequence<int, 8>{}, pa, pb, xv, l, a);
+    if constexpr (kPipe) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) xv[t] = xn[t];
+    }
   }
 }
 
@@ -432,7 +462,7 @@ __device__ __forceinline__ void shared_self_scores(const GatParams& p, int64_t r
 }
 
 template <int O, int H, int CH, bool ATT>
-__global__ __launch_bounds__(kBlock) GAT_OCCUPANCY(ATT) void gat_shared_kernel(GatParams p) {
+__global__ __launch_bounds__(kBlock) GAT_SHARED_OCCUPANCY(ATT) void gat_shared_kernel(GatParams p) {
   constexpr int GROUP = O / 4;
   constexpr int RPW = 64 / GROUP;
   const int lane = threadIdx.x & 63;
@@ -506,7 +536,7 @@ __global__ __launch_bounds__(kBlock) GAT_OCCUPANCY(ATT) void gat_partial_kernel(
 // ONCE for all H heads (gat_partial_kernel<H*O> would load it H times, one head per lane
 // group); the partials have gat_partial_kernel's layout, so gat_merge_kernel<H*O> finishes.
 template <int O, int H, int CH, bool ATT>
-__global__ __launch_bounds__(kBlock) GAT_OCCUPANCY(ATT) void gat_shared_partial_kernel(GatParams p, GatSplit sp) {
+__global__ __launch_bounds__(kBlock) GAT_SHARED_OCCUPANCY(ATT) void gat_shared_partial_kernel(GatParams p, GatSplit sp) {
   constexpr int GROUP = O / 4;
   constexpr int RPW = 64 / GROUP;
   const int lane = threadIdx.x & 63;

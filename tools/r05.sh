@@ -79,6 +79,19 @@ case ${1:?call} in
     timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c5_c5kt -o run -- \
         python3 tools/bench_configs.py $C5 --steps 3 --warmup 1 --no-ref-check > $OUT/c5_c5kt.jsonl 2> $OUT/c5_c5kt.err
     ;;
+  c6)
+    # the shared-row (last GAT layer) kernel: next block's rows in flight (GAT_SHARED_PIPE)
+    # at 3 or 4 waves per SIMD, same box, 5M x 5M; then correctness of the chosen default
+    : > $OUT/c6_gat_pipe.jsonl
+    for v in default pipe3 pipe4 w3 default; do
+      L=tools/var/gat_$v.so; [ $v = default ] && L=gnn-recommendations_amd/lib/libgnnrec.so
+      GNNREC_LIB=$L timeout -k 10 300 python -u tools/exp_gat_variants.py --tag $v \
+          >> $OUT/c6_gat_pipe.jsonl 2>> $OUT/c6.err
+    done
+    GNNREC_LIB=tools/var/gat_pipe3.so timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d $OUT/c6_pipe3kt -o run -- python3 tools/bench_configs.py $C5 --steps 3 --warmup 1 --no-ref-check \
+        > $OUT/c6_pipe3kt.jsonl 2> $OUT/c6_pipe3kt.err
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
