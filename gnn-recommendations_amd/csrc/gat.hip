@@ -96,6 +96,9 @@ __device__ __forceinline__ void gat_finish(const GatParams& p, int64_t r, float4
 #ifndef GAT_ATT_CHUNK
 #define GAT_ATT_CHUNK 16
 #endif
+#ifndef GAT_MAIN_PIPE
+#define GAT_MAIN_PIPE 0
+#endif
 #define GAT_OCCUPANCY(ATT) __attribute__((amdgpu_waves_per_eu((ATT) ? GAT_ATT_WAVES : 1)))
 #ifndef GAT_SHARED_WAVES
 #define GAT_SHARED_WAVES GAT_ATT_WAVES
@@ -187,8 +190,8 @@ __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, in
   // a time and win the occupancy back
   constexpr int CH = ATT ? GAT_ATT_CHUNK : kChunk;
   static_assert(CH % kSoftBlock == 0, "a gather step holds whole softmax blocks");
-  for (int64_t k0 = beg; k0 < end; k0 += CH) {
-    constexpr int PER = (GROUP >= CH) ? 1 : CH / GROUP;
+  constexpr int PER = (GROUP >= CH) ? 1 : CH / GROUP;
+  auto load_chunk = [&](int64_t k0, float4 (&dst)[CH], float (&snd)[CH]) {
     int cm[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
@@ -196,13 +199,25 @@ __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, in
       k = k < end ? k : end - 1;
       cm[q] = p.A.col[k];
     }
-    float4 xv[CH];
-    float sn[CH];
 #pragma unroll
     for (int t = 0; t < CH; ++t) {
       const int c = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
-      xv[t] = ld4(p.h + (int64_t)c * p.ldh + head * p.head_stride + fo);
-      if constexpr (!ATT) sn[t] = p.s_neigh[(int64_t)c * p.ld_sn + head];
+      dst[t] = ld4(p.h + (int64_t)c * p.ldh + head * p.head_stride + fo);
+      if constexpr (!ATT) snd[t] = p.s_neigh[(int64_t)c * p.ld_sn + head];
+    }
+  };
+  // ATT + GAT_MAIN_PIPE: the next chunk's rows are in flight while this chunk is reduced
+  constexpr bool kPipe = ATT && GAT_MAIN_PIPE;
+  float4 xv[CH];
+  float sn[CH];
+  if constexpr (kPipe) load_chunk(beg, xv, sn);
+  for (int64_t k0 = beg; k0 < end; k0 += CH) {
+    float4 xn[CH];
+    float snn[CH];
+    if constexpr (kPipe) {
+      if (k0 + CH < end) load_chunk(k0 + CH, xn, snn);
+    } else {
+      load_chunk(k0, xv, sn);
     }
     if constexpr (ATT) {
 #pragma unroll
@@ -216,6 +231,10 @@ __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, in
       for (int t = 0; t < kSoftBlock; ++t)
         E[t] = gat_logit2(ss, sn[b * kSoftBlock + t], p.slope, k0 + b * kSoftBlock + t < end);
       gat_block(E, xv + b * kSoftBlock, m, l, a);
+    }
+    if constexpr (kPipe) {
+#pragma unroll
+      for (int t = 0; t < CH; ++t) xv[t] = xn[t];
     }
   }
 }

@@ -92,6 +92,15 @@ case ${1:?call} in
         -d $OUT/c6_pipe3kt -o run -- python3 tools/bench_configs.py $C5 --steps 3 --warmup 1 --no-ref-check \
         > $OUT/c6_pipe3kt.jsonl 2> $OUT/c6_pipe3kt.err
     ;;
+  c7)
+    # the head-major kernel with the next chunk in flight (GAT_MAIN_PIPE, 8 + 8 neighbours)
+    : > $OUT/c7_gat_mpipe.jsonl
+    for v in default mpipe8 default mpipe8; do
+      L=tools/var/gat_$v.so; [ $v = default ] && L=gnn-recommendations_amd/lib/libgnnrec.so
+      GNNREC_LIB=$L timeout -k 10 300 python -u tools/exp_gat_variants.py --tag $v \
+          >> $OUT/c7_gat_mpipe.jsonl 2>> $OUT/c7.err
+    done
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
