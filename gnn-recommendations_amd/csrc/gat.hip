@@ -96,6 +96,19 @@ __device__ __forceinline__ void gat_finish(const GatParams& p, int64_t r, float4
 #ifndef GAT_ATT_CHUNK
 #define GAT_ATT_CHUNK 16
 #endif
+// experiment (A/B only): rows of source ids >= GAT_HOT_COLS are gathered non-temporal, so the
+// cold tail of a degree-ordered power-law graph does not evict the hot rows from L2 (0: off)
+#ifndef GAT_HOT_COLS
+#define GAT_HOT_COLS 0
+#endif
+typedef float gat_f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld4_src(const float* p, int c) {
+  if (GAT_HOT_COLS > 0 && c >= GAT_HOT_COLS) {
+    const gat_f4v v = __builtin_nontemporal_load(reinterpret_cast<const gat_f4v*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  return ld4(p);
+}
 #ifndef GAT_MAIN_PIPE
 #define GAT_MAIN_PIPE 0
 #endif
@@ -202,7 +215,7 @@ __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, in
 #pragma unroll
     for (int t = 0; t < CH; ++t) {
       const int c = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
-      dst[t] = ld4(p.h + (int64_t)c * p.ldh + head * p.head_stride + fo);
+      dst[t] = ld4_src(p.h + (int64_t)c * p.ldh + head * p.head_stride + fo, c);
       if constexpr (!ATT) snd[t] = p.s_neigh[(int64_t)c * p.ld_sn + head];
     }
   };
@@ -355,7 +368,7 @@ __device__ __forceinline__ void gat_shared_rows16(const GatParams& p, int64_t r,
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
       const int c = __shfl(cm, t, 16);
-      dst[t] = ld4(p.h + (int64_t)c * p.ldh + 4 * gl);
+      dst[t] = ld4_src(p.h + (int64_t)c * p.ldh + 4 * gl, c);
     }
   };
   // ATT + GAT_SHARED_PIPE: the next block's rows are in flight while this block's scores,

@@ -101,6 +101,16 @@ case ${1:?call} in
           >> $OUT/c7_gat_mpipe.jsonl 2>> $OUT/c7.err
     done
     ;;
+  c8)
+    # cold-tail rows gathered non-temporal (GAT_HOT_COLS: ids below it are the hot rows of the
+    # degree-ordered Zipf graph), same box, 5M x 5M
+    : > $OUT/c8_gat_hot.jsonl
+    for v in default hot16384 hot65536 hot262144 default; do
+      L=tools/var/gat_$v.so; [ $v = default ] && L=gnn-recommendations_amd/lib/libgnnrec.so
+      GNNREC_LIB=$L timeout -k 10 300 python -u tools/exp_gat_variants.py --tag $v \
+          >> $OUT/c8_gat_hot.jsonl 2>> $OUT/c8.err
+    done
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
