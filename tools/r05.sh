@@ -111,6 +111,12 @@ case ${1:?call} in
           >> $OUT/c8_gat_hot.jsonl 2>> $OUT/c8.err
     done
     ;;
+  c9)
+    # heavy-segment plans at full G1B (its heaviest rows are 3x those of 5M x 5M), one process
+    timeout -k 10 900 python -u tools/exp_gat_variants.py --tag g1b --shape 10000000 10000000 1000000000 \
+        --reps 5 --plans column panel:8192:256 panel:16384:256 panel:8192:64 panel:32768:512 column \
+        > $OUT/c9_g1b_plans.jsonl 2> $OUT/c9.err
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
