@@ -117,6 +117,12 @@ case ${1:?call} in
         --reps 5 --plans column panel:8192:256 panel:16384:256 panel:8192:64 panel:32768:512 column \
         > $OUT/c9_g1b_plans.jsonl 2> $OUT/c9.err
     ;;
+  c10)
+    # stall decomposition of the shared-row kernel (2M x 2M slice), scores from rows vs tables
+    S="python3 tools/exp_gat_variants.py --tag st --shape 2000000 2000000 50000000 --reps 3"
+    bash tools/pmc_stalls_kernel.sh $OUT/c10_att gat_shared_kernel -- $S
+    GNNREC_GAT_SCORES_FROM_ROWS=0 bash tools/pmc_stalls_kernel.sh $OUT/c10_tab gat_shared_kernel -- $S
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
