@@ -711,12 +711,14 @@ def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh:
 # Heavy-row segments of the scores-from-rows kernels: "column" runs them sorted by their first
 # column (CsrGraph.heavy_plan_by_column), "row" in row order; GAT_XCD_ORDER gives each XCD a
 # contiguous eighth of that list.
-GAT_SEGMENT_ORDER = os.environ.get("GNNREC_GAT_SEGMENT_ORDER", "column")
+GAT_SEGMENT_ORDER = os.environ.get("GNNREC_GAT_SEGMENT_ORDER", "panel")
 GAT_XCD_ORDER = os.environ.get("GNNREC_GAT_XCD_ORDER", "1") != "0"
-# "panel": the heaviest rows (>= GAT_PANEL_MIN_EDGES edges per GAT_PANEL-column panel on
-# average) are cut at panel boundaries (CsrGraph.heavy_plan_panels)
+# "panel" (the default): the heaviest rows (>= GAT_PANEL_MIN_EDGES edges per GAT_PANEL-column
+# panel on average) are cut at panel boundaries (CsrGraph.heavy_plan_panels), the others as
+# "column"; G1B 179.8 -> 176.7 ms, 5M x 5M 54.0 -> 53.6 ms (profiles/r05/c9_g1b_plans.jsonl,
+# c5_gat_panels.jsonl)
 GAT_PANEL = int(os.environ.get("GNNREC_GAT_PANEL", "8192"))
-GAT_PANEL_MIN_EDGES = int(os.environ.get("GNNREC_GAT_PANEL_MIN_EDGES", "64"))
+GAT_PANEL_MIN_EDGES = int(os.environ.get("GNNREC_GAT_PANEL_MIN_EDGES", "256"))
 
 
 def gat_att_supported(o_dim: int) -> bool:
