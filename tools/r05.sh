@@ -123,6 +123,17 @@ case ${1:?call} in
     bash tools/pmc_stalls_kernel.sh $OUT/c10_att gat_shared_kernel -- $S
     GNNREC_GAT_SCORES_FROM_ROWS=0 bash tools/pmc_stalls_kernel.sh $OUT/c10_tab gat_shared_kernel -- $S
     ;;
+  c11)
+    # the final GAT default (panel-cut heavy rows): GAT GPU tests, config 5 at 5M x 5M and at
+    # G1B, both with the sampled-row check
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+        tests/test_gat_att_gpu.py tests/test_gat_train_gpu.py tests/test_real_shapes_gpu.py \
+        tests/test_models_gpu.py tests/test_fullsize_models_gpu.py > $OUT/c11_gat_tests.log 2>&1
+    timeout -k 10 600 python -u tools/bench_configs.py $C5 --steps 5 > $OUT/c11_config5_g250m.jsonl \
+        2> $OUT/c11_config5_g250m.err
+    timeout -k 10 800 python -u tools/bench_configs.py --configs 5 --g1b --steps 5 \
+        > $OUT/c11_config5_g1b.jsonl 2> $OUT/c11_config5_g1b.err
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
