@@ -1,0 +1,89 @@
+"""Would the column-ordered schedule pay for config 5's heavy rows? Same rows, same x, one
+process: the heavy rows (degree band --lo..--hi) of the power-law graph cut out as their own
+CSR, then (a) the CSR SpMM (workgroup per heavy row), (b) the column-ordered tiled hop
+(gnnrec_spmm_tiled_f32, one pass: every heavy row's accumulator resident in LDS), both at
+d = 64, and (c) the GAT heavy-row aggregation (ATT partials + merge) on the same rows.
+One JSON line per shape.
+
+    python tools/exp_heavy_tiled.py [--shape U I PAIRS] [--lo 2048] [--hi 0]
+"""
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "gnn-recommendations_amd"), str(ROOT), str(ROOT / "tools")]
+from bench_configs import powerlaw_graph  # noqa: E402
+from src.ops import CsrGraph  # noqa: E402
+from src.ops import functional as F  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--shape", type=int, nargs=3, default=[5_000_000, 5_000_000, 250_000_000])
+ap.add_argument("--lo", type=int, default=2048)
+ap.add_argument("--hi", type=int, default=0, help="max degree kept (0: no bound)")
+ap.add_argument("--reps", type=int, default=10)
+ap.add_argument("--rows-per-block", type=int, default=0)
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+g = powerlaw_graph(*a.shape, 0.9, 0, 16, device=dev)
+deg = g.row_ptr[1:] - g.row_ptr[:-1]
+keep = deg > a.lo
+if a.hi > 0:
+    keep &= deg <= a.hi
+rows = torch.nonzero(keep).flatten()
+cnt = deg[rows]
+rp = torch.zeros(rows.numel() + 1, dtype=torch.int64, device=dev)
+rp[1:] = torch.cumsum(cnt, 0)
+nnz = int(rp[-1])
+off = torch.repeat_interleave(g.row_ptr[rows] - rp[:-1], cnt)
+idx = torch.arange(nnz, device=dev, dtype=torch.int64) + off
+sub = CsrGraph(rp, g.col[idx].contiguous(), g.val[idx].contiguous(), (rows.numel(), g.shape[1]))
+del idx, off
+n_cols = g.shape[1]
+torch.manual_seed(0)
+x = F.hop_table(n_cols, 64, device=dev)
+x.copy_(torch.randn(n_cols, 64, device=dev) * 0.1)
+
+
+def timed(fn):
+    fn()
+    torch.cuda.synchronize()
+    ms = []
+    for _ in range(a.reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        torch.cuda.synchronize()
+        ms.append(s.elapsed_time(e))
+    return float(np.median(ms))
+
+
+rec = {"shape": a.shape, "band": [a.lo, a.hi], "heavy_rows": rows.numel(), "heavy_nnz": nnz,
+       "max_degree": int(cnt.max())}
+y_csr = F.hop_table(sub.n_rows, 64, device=dev)
+F.TILED_HOP = False
+rec["csr_ms"] = timed(lambda: F.spmm_into(sub, x, y_csr))
+F.TILED_HOP = True
+cus = torch.cuda.get_device_properties(dev).multi_processor_count
+R = a.rows_per_block or min(F.TILED_MAX_ROWS, -(-sub.n_rows // cus))
+t0 = time.perf_counter()
+plan = sub.tiled_plan(rows_per_block=R)
+torch.cuda.synchronize()
+rec.update(rows_per_block=R, plan_s=time.perf_counter() - t0, plan_chunks=int(plan["n_chunks"]),
+           plan_blocks=int(plan["n_blocks"]))
+y_t = F.hop_table(sub.n_rows, 64, device=dev)
+rec["tiled_ms"] = timed(lambda: F.spmm_tiled_into(sub, x, y_t, plan))
+rec["tiled_vs_csr_max_abs_diff"] = float((y_t - y_csr).abs().max())
+hself = torch.randn(sub.n_rows, 64, device=dev) * 0.1
+att = torch.randn(2, 4, 16, device=dev) * 0.3
+out = torch.empty(sub.n_rows, 64, device=dev)
+rec["gat_heavy_ms"] = timed(lambda: F.gat_aggregate_att(sub, x, hself, att, 4, 16, out=out))
+for k in ("csr_ms", "tiled_ms", "gat_heavy_ms"):
+    rec[k.replace("_ms", "_edges_per_s")] = nnz / (rec[k] * 1e-3)
+print(json.dumps(rec), flush=True)

@@ -134,6 +134,14 @@ case ${1:?call} in
     timeout -k 10 800 python -u tools/bench_configs.py --configs 5 --g1b --steps 5 \
         > $OUT/c11_config5_g1b.jsonl 2> $OUT/c11_config5_g1b.err
     ;;
+  c12)
+    # config 5's heavy rows alone: CSR SpMM vs the column-ordered tiled hop vs the GAT heavy
+    # partials on the same rows (is an LDS-resident schedule worth building for them?)
+    for band in "2048 65536" "2048 0" "0 2048"; do
+      timeout -k 10 300 python -u tools/exp_heavy_tiled.py --lo ${band% *} --hi ${band#* } \
+          >> $OUT/c12_heavy_tiled.jsonl 2>> $OUT/c12_heavy_tiled.err
+    done
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
