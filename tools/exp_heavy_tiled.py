@@ -10,6 +10,7 @@ One JSON line per shape.
 import argparse
 import json
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -50,6 +51,22 @@ x = F.hop_table(n_cols, 64, device=dev)
 x.copy_(torch.randn(n_cols, 64, device=dev) * 0.1)
 
 
+def note(what):
+    print(f"[{time.strftime('%H:%M:%S')}] {what}", file=sys.stderr, flush=True)
+
+
+note(f"sub-operand: {rows.numel()} rows, {nnz} nnz")
+
+
+def heartbeat():   # long plan builds: keep the run's log moving
+    while True:
+        time.sleep(30)
+        note("...")
+
+
+threading.Thread(target=heartbeat, daemon=True).start()
+
+
 def timed(fn):
     fn()
     torch.cuda.synchronize()
@@ -69,6 +86,7 @@ rec = {"shape": a.shape, "band": [a.lo, a.hi], "heavy_rows": rows.numel(), "heav
 y_csr = F.hop_table(sub.n_rows, 64, device=dev)
 F.TILED_HOP = False
 rec["csr_ms"] = timed(lambda: F.spmm_into(sub, x, y_csr))
+note(f"csr {rec['csr_ms']:.3f} ms; planning")
 F.TILED_HOP = True
 cus = torch.cuda.get_device_properties(dev).multi_processor_count
 R = a.rows_per_block or min(F.TILED_MAX_ROWS, -(-sub.n_rows // cus))
@@ -78,7 +96,9 @@ torch.cuda.synchronize()
 rec.update(rows_per_block=R, plan_s=time.perf_counter() - t0, plan_chunks=int(plan["n_chunks"]),
            plan_blocks=int(plan["n_blocks"]))
 y_t = F.hop_table(sub.n_rows, 64, device=dev)
+note(f"plan {rec['plan_s']:.1f} s")
 rec["tiled_ms"] = timed(lambda: F.spmm_tiled_into(sub, x, y_t, plan))
+note(f"tiled {rec['tiled_ms']:.3f} ms")
 rec["tiled_vs_csr_max_abs_diff"] = float((y_t - y_csr).abs().max())
 hself = torch.randn(sub.n_rows, 64, device=dev) * 0.1
 att = torch.randn(2, 4, 16, device=dev) * 0.3

@@ -137,8 +137,8 @@ case ${1:?call} in
   c12)
     # config 5's heavy rows alone: CSR SpMM vs the column-ordered tiled hop vs the GAT heavy
     # partials on the same rows (is an LDS-resident schedule worth building for them?)
-    for band in "2048 65536" "2048 0" "0 2048"; do
-      timeout -k 10 300 python -u tools/exp_heavy_tiled.py --lo ${band% *} --hi ${band#* } \
+    for band in ${BANDS:-2048:65536 2048:0 0:2048}; do
+      timeout -k 10 300 python -u tools/exp_heavy_tiled.py --lo ${band%:*} --hi ${band#*:} \
           >> $OUT/c12_heavy_tiled.jsonl 2>> $OUT/c12_heavy_tiled.err
     done
     ;;
