@@ -585,10 +585,14 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
 // A operand of v_mfma_f32_16x16x4f32 straight from registers: lane (i, g) = (lane & 15,
 // lane >> 4) loads row i's float4 at columns 16 t + 4 g (t < K/16: the 4 lanes of a row read
 // 64 contiguous bytes per instruction), and MFMA step 4 t + q contracts k = 16 t + 4 g + q
-// (a permutation of the k order; GAT is an fp32-tolerance path). B sits in LDS for the launch
-// (row stride PN + 4: the k rows of lanes g and g + 1 land 16 banks apart), NT 16-column output
-// tiles, the o tile goes through a small private LDS tile so whole rows are stored, and the
-// next tile's rows are in flight in registers meanwhile.
+// (a permutation of the k order; GAT is an fp32-tolerance path). B sits in LDS for the launch:
+// for K >= 128 (MFMA-bound) as MFMA fragments — [t][nt][lane][q] = B[16 t + 4 g + q][16 nt + i],
+// a lane's B operands of 4 steps in one ds_read_b128, double-buffered per t (K = 256: 1.79 ->
+// 1.70 ms per 5M rows, same bits, profiles/r05/c13_rows_gemm.jsonl); for K = 64 (HBM-bound) as
+// rows [K][PN + 4] read per MFMA, which keeps the instances within 128 VGPRs (the fragment form
+// took P = 72 from 0.72 to 0.84 ms). NT 16-column output tiles, the o tile goes through a small
+// private LDS tile so whole rows are stored, and the next tile's rows are in flight in
+// registers meanwhile.
 struct RowsGemmEpi {   // optional epilogue of gnnrec_rows_gemm_f32 (GAT's last layer)
   int apply_elu;
   int epi;             // GNNREC_EPI_ACC_* flags, as gnnrec_gat_aggregate_f32
@@ -608,19 +612,26 @@ __global__ __launch_bounds__(64 * NW) void rows_gemm_kernel(int64_t n_rows, cons
   constexpr int LDB = PN + 4;
   constexpr int LDO = PN + 4;
   constexpr int T = K / 16;            // float4 per lane per tile
+  constexpr bool kFrag = K >= 128;     // B as fragments [T][NT][64][4] (else rows [K][LDB])
   static_assert(K % 16 == 0 && NT >= 1, "rows_gemm: K % 16 == 0");
-  // dynamic LDS (rows_gemm_lds): B [K][LDB] then NW o tiles [16][LDO]
+  // dynamic LDS (rows_gemm_lds): B, then NW o tiles [16][LDO]
   extern __shared__ __attribute__((aligned(16))) float rg_lds[];
   float* b_lds = rg_lds;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int i16 = lane & 15, g = lane >> 4;
   for (int e = threadIdx.x; e < K * PN; e += 64 * NW) {
-    const int k = e / PN, j = e % PN;
-    b_lds[k * LDB + j] = j < P ? B[(int64_t)k * P + j] : 0.f;
+    if constexpr (kFrag) {
+      const int q = e & 3, l = (e >> 2) & 63, tn = e >> 8;
+      const int k = 16 * (tn / NT) + 4 * (l >> 4) + q, j = 16 * (tn % NT) + (l & 15);
+      b_lds[e] = j < P ? B[(int64_t)k * P + j] : 0.f;
+    } else {
+      const int k = e / PN, j = e % PN;
+      b_lds[k * LDB + j] = j < P ? B[(int64_t)k * P + j] : 0.f;
+    }
   }
   __syncthreads();
-  float* ot = rg_lds + K * LDB + wave * 16 * LDO;
+  float* ot = rg_lds + K * (kFrag ? PN : LDB) + wave * 16 * LDO;
   const int64_t n_tiles = ceil_div(n_rows, 16);
   const int64_t stride = (int64_t)gridDim.x * NW;
   float4 pa[T], pn[T];
@@ -635,6 +646,7 @@ __global__ __launch_bounds__(64 * NW) void rows_gemm_kernel(int64_t n_rows, cons
   int64_t tile = (int64_t)blockIdx.x * NW + wave;
   load(tile, pa);
   const int P4 = P / 4;
+  const float4* bl = reinterpret_cast<const float4*>(b_lds) + lane;
   const float* brow = b_lds + (4 * g) * LDB + i16;
   for (; tile < n_tiles; tile += stride) {
     load(tile + stride, pn);
@@ -643,15 +655,43 @@ __global__ __launch_bounds__(64 * NW) void rows_gemm_kernel(int64_t n_rows, cons
     for (int nt = 0; nt < NT; ++nt) c[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
     // fully unrolled (a rolled k loop made the compiler rotate the accumulators through
     // partially overlapping AGPR ranges, v_mfma a[10:13], ..., a[12:15]: wrong on gfx950)
+    if constexpr (kFrag) {
+      // the B fragments of step group t + 1 are read while group t's MFMAs run
+      float4 bc[NT], bn[NT];
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
-      const float av[4] = {pa[t].x, pa[t].y, pa[t].z, pa[t].w};
+      for (int nt = 0; nt < NT; ++nt) bc[nt] = bl[nt * 64];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int t = 0; t < T; ++t) {
+        if (t + 1 < T) {
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-          c[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-              av[q], brow[(16 * t + q) * LDB + 16 * nt], c[nt], 0, 0, 0);
+          for (int nt = 0; nt < NT; ++nt) bn[nt] = bl[((t + 1) * NT + nt) * 64];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const float av[4] = {pa[t].x, pa[t].y, pa[t].z, pa[t].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) {
+            const float bq = q == 0 ? bc[nt].x : q == 1 ? bc[nt].y : q == 2 ? bc[nt].z : bc[nt].w;
+            c[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[q], bq, c[nt], 0, 0, 0);
+          }
+        if (t + 1 < T) {
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) bc[nt] = bn[nt];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const float av[4] = {pa[t].x, pa[t].y, pa[t].z, pa[t].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt)
+            c[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                av[q], brow[(16 * t + q) * LDB + 16 * nt], c[nt], 0, 0, 0);
+      }
     }
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
@@ -873,7 +913,7 @@ namespace {
 template <int K, int NT, int NW>
 constexpr size_t rows_gemm_lds() {
   constexpr int PN = NT * 16;
-  return sizeof(float) * ((size_t)K * (PN + 4) + (size_t)NW * 16 * (PN + 4));
+  return sizeof(float) * ((size_t)K * (K >= 128 ? PN : PN + 4) + (size_t)NW * 16 * (PN + 4));
 }
 
 // Dynamic LDS past 64 KB needs the kernel attribute, set once per (kernel, device); a

@@ -142,6 +142,31 @@ case ${1:?call} in
           >> $OUT/c12_heavy_tiled.jsonl 2>> $OUT/c12_heavy_tiled.err
     done
     ;;
+  c13)
+    # rows_gemm with the B operand as LDS fragments (ds_read_b128 per 4 MFMA steps): its tests,
+    # then the GEMMs alone and config 5 at 5M x 5M, same box, against the round's base build
+    timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
+        tests/test_kernels_gpu.py -k "rows_gemm" tests/test_gat_att_gpu.py > $OUT/c13_tests.log 2>&1
+    : > $OUT/c13_rows_gemm.jsonl; : > $OUT/c13_gat.jsonl
+    for v in base new base new; do
+      L=tools/ab/base_r05.so; [ $v = new ] && L=gnn-recommendations_amd/lib/libgnnrec.so
+      GNNREC_LIB=$L timeout -k 10 120 python -u tools/exp_rows_gemm.py --tag $v >> $OUT/c13_rows_gemm.jsonl 2>> $OUT/c13.err
+      GNNREC_LIB=$L timeout -k 10 300 python -u tools/exp_gat_variants.py --tag $v >> $OUT/c13_gat.jsonl 2>> $OUT/c13.err
+    done
+    ;;
+  c14)
+    # rows_gemm final (fragments for K >= 128 only): tests + timing; the NGCF transform with
+    # its waves started apart (GNNREC_TRANSFORM_STAGGER), same box
+    timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
+        tests/test_kernels_gpu.py tests/test_gat_att_gpu.py > $OUT/c14_tests.log 2>&1
+    timeout -k 10 120 python -u tools/exp_rows_gemm.py --tag final > $OUT/c14_rows_gemm.jsonl 2> $OUT/c14.err
+    : > $OUT/c14_transform.jsonl
+    for v in default 8 20 40 100 default 20 40; do
+      L=tools/ab/tr_stagger$v.so; [ $v = default ] && L=gnn-recommendations_amd/lib/libgnnrec.so
+      GNNREC_LIB=$L timeout -k 10 120 python -u tools/exp_transform.py | sed "s/^{/{\"variant\": \"$v\", /" \
+          >> $OUT/c14_transform.jsonl 2>> $OUT/c14.err
+    done
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
