@@ -401,18 +401,36 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
   const int64_t stride = (int64_t)gridDim.x * NW;
   // A operands: lane (i16, k4) loads row i16's float4 at columns 16t + 4 k4 (t < 4)
   float4 pn[4], px[4];
+  // MODE 0: rows past the end (the last tile's tail, the prefetch past the last tile) load the
+  // last row instead — no row is ever stored from them — and the unconditional loads keep the
+  // prefetch in flight: behind a branch the compiler waited for them right after issuing them
+  // (config 3's transform 364 -> 356 us, profiles/r05/c15_*). MODE 1 keeps the branch (the
+  // unconditional form ran 5 % slower there).
   auto load = [&](int64_t tile) {
-    const int64_t r = tile * 16 + i16;
-    const bool ok = tile < n_tiles && r < p.A.n_rows;
+    if constexpr (MODE == 0) {
+      const int64_t r = std::min<int64_t>(tile * 16 + i16, p.A.n_rows - 1);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      pn[t] = px[t] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (GNNREC_TRANSFORM_EXP & 4) {
-        pn[t] = make_float4((float)r, 1.f, 2.f, (float)t);
-        px[t] = pn[t];
-      } else if (ok) {
-        pn[t] = *reinterpret_cast<const float4*>(p.x + r * p.ldx + 16 * t + 4 * k4);
-        if (MODE == 0) px[t] = *reinterpret_cast<const float4*>(p.x_self + r * p.ld_self + 16 * t + 4 * k4);
+      for (int t = 0; t < 4; ++t) {
+        if (GNNREC_TRANSFORM_EXP & 4) {
+          pn[t] = make_float4((float)r, 1.f, 2.f, (float)t);
+          px[t] = pn[t];
+        } else {
+          pn[t] = *reinterpret_cast<const float4*>(p.x + r * p.ldx + 16 * t + 4 * k4);
+          px[t] = *reinterpret_cast<const float4*>(p.x_self + r * p.ld_self + 16 * t + 4 * k4);
+        }
+      }
+    } else {
+      const int64_t r = tile * 16 + i16;
+      const bool ok = tile < n_tiles && r < p.A.n_rows;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        pn[t] = px[t] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (GNNREC_TRANSFORM_EXP & 4) {
+          pn[t] = make_float4((float)r, 1.f, 2.f, (float)t);
+          px[t] = pn[t];
+        } else if (ok) {
+          pn[t] = *reinterpret_cast<const float4*>(p.x + r * p.ldx + 16 * t + 4 * k4);
+        }
       }
     }
   };
@@ -635,13 +653,23 @@ __global__ __launch_bounds__(64 * NW) void rows_gemm_kernel(int64_t n_rows, cons
   const int64_t n_tiles = ceil_div(n_rows, 16);
   const int64_t stride = (int64_t)gridDim.x * NW;
   float4 pa[T], pn[T];
+  // K >= 128: rows past the end load the last row (never stored), and the unconditional loads
+  // keep the prefetch in flight (as transform64_kernel's; behind a branch the compiler waited for
+  // them right after issuing them). K = 64 keeps the branch: unconditional, its NT = 2 / 4
+  // instances compile to partially overlapping MFMA accumulators (tests/test_native_host.py).
   auto load = [&](int64_t tile, float4 (&v)[T]) {
-    const int64_t r = tile * 16 + i16;
-    const bool ok = tile < n_tiles && r < n_rows;
-    const float* xr = x + (ok ? r : 0) * ldx + 4 * g;
+    if constexpr (kFrag) {
+      const float* xr = x + std::min<int64_t>(tile * 16 + i16, n_rows - 1) * ldx + 4 * g;
 #pragma unroll
-    for (int t = 0; t < T; ++t)
-      v[t] = ok ? *reinterpret_cast<const float4*>(xr + 16 * t) : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int t = 0; t < T; ++t) v[t] = *reinterpret_cast<const float4*>(xr + 16 * t);
+    } else {
+      const int64_t r = tile * 16 + i16;
+      const bool ok = tile < n_tiles && r < n_rows;
+      const float* xr = x + (ok ? r : 0) * ldx + 4 * g;
+#pragma unroll
+      for (int t = 0; t < T; ++t)
+        v[t] = ok ? *reinterpret_cast<const float4*>(xr + 16 * t) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   };
   int64_t tile = (int64_t)blockIdx.x * NW + wave;
   load(tile, pa);

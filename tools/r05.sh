@@ -167,6 +167,42 @@ case ${1:?call} in
           >> $OUT/c14_transform.jsonl 2>> $OUT/c14.err
     done
     ;;
+  c15)
+    # unconditional prefetch loads in the streaming MFMA kernels (transform64, rows_gemm): the
+    # compiler had waited for the next tile's rows right after issuing them. Tests, then same-box
+    # A/B against the previous source (tools/ab/head_r05.so): kernels alone, config 3 traced
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+        tests/test_kernels_gpu.py tests/test_gat_att_gpu.py tests/test_models_gpu.py \
+        tests/test_fullsize_models_gpu.py > $OUT/c15_tests.log 2>&1
+    : > $OUT/c15_transform.jsonl; : > $OUT/c15_rows_gemm.jsonl; : > $OUT/c15_config3.jsonl
+    for v in head new head new; do
+      L=tools/ab/head_r05.so; [ $v = new ] && L=gnn-recommendations_amd/lib/libgnnrec.so
+      GNNREC_LIB=$L timeout -k 10 120 python -u tools/exp_transform.py | sed "s/^{/{\"variant\": \"$v\", /" \
+          >> $OUT/c15_transform.jsonl 2>> $OUT/c15.err
+      GNNREC_LIB=$L timeout -k 10 120 python -u tools/exp_rows_gemm.py --tag $v >> $OUT/c15_rows_gemm.jsonl 2>> $OUT/c15.err
+      GNNREC_LIB=$L timeout -k 10 300 python -u tools/bench_configs.py --configs 3 --steps 10 --no-ref-check \
+          | sed "s/^{/{\"variant\": \"$v\", /" >> $OUT/c15_config3.jsonl 2>> $OUT/c15.err
+    done
+    for v in head new; do
+      L=tools/ab/head_r05.so; [ $v = new ] && L=gnn-recommendations_amd/lib/libgnnrec.so
+      GNNREC_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c15_c3kt_$v -o run -- \
+          python3 tools/bench_configs.py --configs 3 --steps 5 --warmup 1 --no-ref-check > $OUT/c15_c3kt_$v.jsonl 2>> $OUT/c15.err
+    done
+    ;;
+  c16)
+    # the kept form (unconditional prefetch for the NGCF transform and rows_gemm K >= 128 only):
+    # tests, then the kernels alone against the previous source
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+        tests/test_kernels_gpu.py tests/test_models_gpu.py tests/test_fullsize_models_gpu.py \
+        tests/test_gat_att_gpu.py > $OUT/c16_tests.log 2>&1
+    : > $OUT/c16_transform.jsonl; : > $OUT/c16_rows_gemm.jsonl
+    for v in head new head new; do
+      L=tools/ab/head_r05.so; [ $v = new ] && L=gnn-recommendations_amd/lib/libgnnrec.so
+      GNNREC_LIB=$L timeout -k 10 120 python -u tools/exp_transform.py | sed "s/^{/{\"variant\": \"$v\", /" \
+          >> $OUT/c16_transform.jsonl 2>> $OUT/c16.err
+      GNNREC_LIB=$L timeout -k 10 120 python -u tools/exp_rows_gemm.py --tag $v >> $OUT/c16_rows_gemm.jsonl 2>> $OUT/c16.err
+    done
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
