@@ -51,6 +51,16 @@ struct GatParams {
   int64_t ld_hself;
 };
 
+// Softmax normalisation a / l of one head's features: one correctly rounded reciprocal, then
+// products — an IEEE division per feature cost ~10 instructions each, 160 per row in the
+// shared-row kernel (4 heads x 4 features per lane). Within an ulp of a / l (fp32 tolerance,
+// as the reference's own softmax); every kernel normalises through here, so the head-major,
+// shared-row and heavy-row paths keep equal bits. l = 0 (an empty row): 0 * inf = NaN, as 0 / 0.
+__device__ __forceinline__ float4 gat_norm(const float4& a, float l) {
+  const float r = 1.f / l;
+  return make_float4(a.x * r, a.y * r, a.z * r, a.w * r);
+}
+
 // Softmax normalisation + head mean + ELU + store + layer-mean epilogue of one row.
 template <int GROUP>
 __device__ __forceinline__ void gat_finish(const GatParams& p, int64_t r, float4 o, int gl) {
@@ -266,7 +276,7 @@ __global__ __launch_bounds__(kBlock) GAT_OCCUPANCY(ATT) void gat_kernel(GatParam
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
   gat_accumulate<GROUP, ATT, HL>(p, r, beg, end, gl, m, l, a);
   // softmax normalisation (l = 0 for an empty row -> 0/0 = NaN, like the reference)
-  gat_finish<GROUP>(p, r, make_float4(a.x / l, a.y / l, a.z / l, a.w / l), gl);
+  gat_finish<GROUP>(p, r, gat_norm(a, l), gl);
 }
 
 template <int T>
@@ -516,7 +526,7 @@ __global__ __launch_bounds__(kBlock) GAT_SHARED_OCCUPANCY(ATT) void gat_shared_k
 #pragma unroll
   for (int h = 0; h < H; ++h)
     st4(p.out + r * p.ldo + h * O + 4 * gl,
-        make_float4(a[h].x / l[h], a[h].y / l[h], a[h].z / l[h], a[h].w / l[h]));
+        gat_norm(a[h], l[h]));
 }
 
 // Heavy rows, pass 1: one row group per segment -> partial (acc[F], m[H], l[H]).
@@ -647,7 +657,7 @@ __global__ __launch_bounds__(kBlock) void gat_merge_kernel(GatParams p, GatSplit
     a = make_float4(__builtin_fmaf(t.x, w, a.x), __builtin_fmaf(t.y, w, a.y),
                     __builtin_fmaf(t.z, w, a.z), __builtin_fmaf(t.w, w, a.w));
   }
-  gat_finish<GROUP>(p, sp.heavy_rows[h], make_float4(a.x / L, a.y / L, a.z / L, a.w / L), gl);
+  gat_finish<GROUP>(p, sp.heavy_rows[h], gat_norm(a, L), gl);
 }
 
 }  // namespace gnnrec

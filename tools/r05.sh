@@ -203,6 +203,20 @@ case ${1:?call} in
       GNNREC_LIB=$L timeout -k 10 120 python -u tools/exp_rows_gemm.py --tag $v >> $OUT/c16_rows_gemm.jsonl 2>> $OUT/c16.err
     done
     ;;
+  c17)
+    # GAT softmax normalisation by one reciprocal per head (gat_norm): GAT tests, then config 5
+    # at 5M x 5M against the previous build, same box, and the checked run
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+        tests/test_gat_att_gpu.py tests/test_gat_train_gpu.py tests/test_real_shapes_gpu.py \
+        tests/test_models_gpu.py tests/test_fullsize_models_gpu.py > $OUT/c17_tests.log 2>&1
+    : > $OUT/c17_gat.jsonl
+    for v in base new base new; do
+      L=tools/ab/pre_norm.so; [ $v = new ] && L=gnn-recommendations_amd/lib/libgnnrec.so
+      GNNREC_LIB=$L timeout -k 10 300 python -u tools/exp_gat_variants.py --tag $v >> $OUT/c17_gat.jsonl 2>> $OUT/c17.err
+    done
+    timeout -k 10 600 python -u tools/bench_configs.py $C5 --steps 5 > $OUT/c17_config5_g250m.jsonl \
+        2> $OUT/c17_config5_g250m.err
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
