@@ -33,6 +33,12 @@ TILED_PLANNER = "device"
 _DEVICE_PLAN_ERRORS = {1: ValueError}
 # slots of one step (a panel of a block) the device planner's scratch is sized for first
 TILED_PLAN_STEP_CAP = 32768
+# longest row tiled_plan() accepts: a row's slots are merged into streams by one lane, so a
+# power-law operand's hub rows make planning serial (config 5's 5M x 5M rows of degree
+# 2 049-65 536: 24 s; with its 1.48M-degree row: not done in 5 minutes,
+# profiles/r05/c12_heavy_tiled.jsonl). The SpMM itself never plans rows past
+# functional.TILED_MAX_DEGREE = 4 096 (they take the CSR kernel).
+TILED_PLAN_MAX_DEGREE = 65536
 # factored plans (gnnrec_tiled_plan_factor, DESIGN.md §3.1c "plan values"): a device graph's
 # plan carries 1-byte column classes instead of fp32 values whenever every value is
 # fl(dis_r * dis_c) with dis from the row counts and at most TILED_MAX_CLASSES distinct dis
@@ -434,6 +440,11 @@ class CsrGraph:
         order)."""
         key = ("tiled", int(rows_per_block), int(panel), int(sub_panel))
         if key not in self._plans:
+            if self.max_degree() > TILED_PLAN_MAX_DEGREE:
+                raise ValueError(
+                    f"tiled_plan: a row of {self.max_degree()} neighbours (> "
+                    f"TILED_PLAN_MAX_DEGREE = {TILED_PLAN_MAX_DEGREE}); rows that long are "
+                    "planned serially — the SpMM runs such operands on the CSR kernel")
             import time
             cuda = self.device.type == "cuda"
 

@@ -46,3 +46,15 @@ def test_heavy_plans_cover_every_heavy_edge_once(kind, args):
         for b, e, r in zip(beg, end, srow):
             if r in cut:
                 assert col[b] // panel == col[e - 1] // panel and e - b <= seg_len
+
+
+def test_tiled_plan_refuses_hub_rows(monkeypatch):
+    """CsrGraph.tiled_plan refuses rows past TILED_PLAN_MAX_DEGREE instead of planning them
+    serially (the SpMM never plans them: functional.TILED_MAX_DEGREE sends them to CSR)."""
+    from src.ops import graph
+    g = _zipf_graph()
+    monkeypatch.setattr(graph, "TILED_PLAN_MAX_DEGREE", g.max_degree() - 1)
+    with pytest.raises(ValueError, match="TILED_PLAN_MAX_DEGREE"):
+        g.tiled_plan(rows_per_block=100, planner="host")
+    monkeypatch.setattr(graph, "TILED_PLAN_MAX_DEGREE", g.max_degree())
+    assert g.tiled_plan(rows_per_block=100, planner="host")["n_chunks"] > 0
