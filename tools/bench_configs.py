@@ -112,12 +112,13 @@ def config5_model(shape, device):
 
 
 def _close(got, ref, rtol=1e-4, atol=1e-6) -> dict:
-    """Elementwise rtol 1e-4 (+ atol 1e-6), and the north star's bar: embeddings within 1e-4
+    """The governing check, elementwise |diff| <= atol + rtol |ref| (`within_tolerance`, with
+    its atol / rtol in the record), and the north star's bar beside it: embeddings within 1e-4
     (absolute, fp32)."""
     err = (got - ref).abs()
     mx = float(err.max())
-    return {"max_abs_diff": mx, "max_abs_ref": float(ref.abs().max()),
-            "within_rtol_1e-4": bool((err <= atol + rtol * ref.abs()).all()),
+    return {"max_abs_diff": mx, "max_abs_ref": float(ref.abs().max()), "atol": atol,
+            "rtol": rtol, "within_tolerance": bool((err <= atol + rtol * ref.abs()).all()),
             "within_north_star_1e-4": mx <= 1e-4}
 
 
@@ -144,7 +145,7 @@ def verify_config3(g, m, table, device) -> dict:
         res[f"layer{k + 1}"] = _close(table[:, (k + 1) * d:(k + 2) * d], ref)
         del x, n, o, ref
     del A
-    res["all_within_rtol_1e-4"] = all(v["within_rtol_1e-4"] for k, v in res.items()
+    res["all_within_tolerance"] = all(v["within_tolerance"] for k, v in res.items()
                                       if k.startswith("layer"))
     return res
 
@@ -185,7 +186,9 @@ def verify_config5(g, m, mine, device) -> dict:
     ref = acc / float(len(m.layers) + 1)
     res = {"reference": "torch fp32 on the device: per-head edge softmax (scatter amax/exp/"
                         "index_add) over the CSR pattern, ELU, layer mean"}
-    res.update(_close(mine, ref))
+    # atol 1e-5 + rtol 1e-4: the tolerance of the sampled-row oracle check (oracle/gat_sample.py)
+    # — both sides are fp32 softmax chains in different orders, over three layers
+    res.update(_close(mine, ref, atol=1e-5))
     return res
 
 

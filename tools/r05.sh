@@ -217,6 +217,18 @@ case ${1:?call} in
     timeout -k 10 600 python -u tools/bench_configs.py $C5 --steps 5 > $OUT/c17_config5_g250m.jsonl \
         2> $OUT/c17_config5_g250m.err
     ;;
+  c18)
+    # shared-row GAT kernel: 16 column indices per load serve two 8-neighbour blocks; GAT
+    # tests, then config 5 at 5M x 5M against the previous build, same box
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+        tests/test_gat_att_gpu.py tests/test_real_shapes_gpu.py tests/test_models_gpu.py \
+        > $OUT/c18_tests.log 2>&1
+    : > $OUT/c18_gat.jsonl
+    for v in base new base new; do
+      L=tools/ab/pre_shcol.so; [ $v = new ] && L=gnn-recommendations_amd/lib/libgnnrec.so
+      GNNREC_LIB=$L timeout -k 10 300 python -u tools/exp_gat_variants.py --tag $v >> $OUT/c18_gat.jsonl 2>> $OUT/c18.err
+    done
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
