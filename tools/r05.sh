@@ -229,6 +229,15 @@ case ${1:?call} in
       GNNREC_LIB=$L timeout -k 10 300 python -u tools/exp_gat_variants.py --tag $v >> $OUT/c18_gat.jsonl 2>> $OUT/c18.err
     done
     ;;
+  c19)
+    # final-tree GAT evidence: G1B kernel trace (checked run is final2), and the GAT kernels'
+    # L2 hit / miss at 5M x 5M
+    timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c19_g1bkt -o run -- \
+        python3 tools/bench_configs.py --configs 5 --g1b --steps 3 --warmup 1 --no-ref-check \
+        > $OUT/c19_g1bkt.jsonl 2> $OUT/c19_g1bkt.err
+    timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/c19_c5l2 -o run -- \
+        python3 tools/bench_configs.py $C5 --steps 3 --warmup 1 --no-ref-check > $OUT/c19_c5l2.jsonl 2> $OUT/c19_c5l2.err
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
