@@ -106,19 +106,9 @@ __device__ __forceinline__ void gat_finish(const GatParams& p, int64_t r, float4
 #ifndef GAT_ATT_CHUNK
 #define GAT_ATT_CHUNK 16
 #endif
-// experiment (A/B only): rows of source ids >= GAT_HOT_COLS are gathered non-temporal, so the
-// cold tail of a degree-ordered power-law graph does not evict the hot rows from L2 (0: off)
-#ifndef GAT_HOT_COLS
-#define GAT_HOT_COLS 0
-#endif
-typedef float gat_f4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 ld4_src(const float* p, int c) {
-  if (GAT_HOT_COLS > 0 && c >= GAT_HOT_COLS) {
-    const gat_f4v v = __builtin_nontemporal_load(reinterpret_cast<const gat_f4v*>(p));
-    return make_float4(v.x, v.y, v.z, v.w);
-  }
-  return ld4(p);
-}
+// a neighbour row's float4 (plain policy: non-temporal cold-row gathers were measured slower in
+// every form)
+__device__ __forceinline__ float4 ld4_src(const float* p, int) { return ld4(p); }
 #ifndef GAT_MAIN_PIPE
 #define GAT_MAIN_PIPE 0
 #endif

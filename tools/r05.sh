@@ -238,6 +238,17 @@ case ${1:?call} in
     timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/c19_c5l2 -o run -- \
         python3 tools/bench_configs.py $C5 --steps 3 --warmup 1 --no-ref-check > $OUT/c19_c5l2.jsonl 2> $OUT/c19_c5l2.err
     ;;
+  c20)
+    # cold-row gathers non-temporal when a whole wave's neighbours are cold (wave-uniform, one
+    # load instruction), hot = degree rank < H on either side of the 5M x 5M graph; H = 1 (almost
+    # all nt) and H = inf (branches only) bracket it. Same box, config 5 at 5M x 5M
+    : > $OUT/c20_gat_hot.jsonl
+    for v in default inf 1 4096 16384 65536 default 16384; do
+      L=tools/ab/gat_hotu$v.so; [ $v = default ] && L=gnn-recommendations_amd/lib/libgnnrec.so
+      GNNREC_LIB=$L timeout -k 10 300 python -u tools/exp_gat_variants.py --tag hot_$v \
+          >> $OUT/c20_gat_hot.jsonl 2>> $OUT/c20.err
+    done
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
