@@ -109,6 +109,9 @@ __device__ __forceinline__ void gat_finish(const GatParams& p, int64_t r, float4
 // a neighbour row's float4 (plain policy: non-temporal cold-row gathers were measured slower in
 // every form)
 __device__ __forceinline__ float4 ld4_src(const float* p, int) { return ld4(p); }
+#ifndef GAT_LOAD_FENCE
+#define GAT_LOAD_FENCE 0
+#endif
 #ifndef GAT_MAIN_PIPE
 #define GAT_MAIN_PIPE 0
 #endif
@@ -177,6 +180,36 @@ __device__ __forceinline__ void gat_block(const float (&E)[kSoftBlock], const fl
   m = mn;
 }
 
+// Row c of a table: base + c * ld floats as ONE v_mad_u64_u32 (c >= 0, ld * 4 < 2^32): the
+// int64 product took 5 VALU instructions per gathered row (sign extension, two 32-bit
+// multiplies, a 64-bit multiply-add, an add) before its pointer add
+__device__ __forceinline__ const float* row_at(const float* base, int c, uint32_t ld_bytes) {
+  return reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) +
+                                        (uint64_t)(uint32_t)c * ld_bytes);
+}
+
+// Lane T of each 16-lane DPP row to every lane of the row (row_newbcast): a neighbour's column
+// index to its row group without an LDS permute (__shfl compiles to ds_bpermute, and the 16
+// of them sat between the index load and the row gathers, each behind an LDS wait)
+template <int T>
+__device__ __forceinline__ int row_bcast_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, 0x150 + T, 0xF, 0xF, true);
+}
+template <int... T>
+__device__ __forceinline__ void bcast_cols16(std::integer_sequence<int, T...>, int cm,
+                                             int (&c)[sizeof...(T)]) {
+  ((c[T] = row_bcast_i<T % 16>(cm)), ...);
+}
+// rows cm@lane T (T < 16) of a 16-lane row group: one float4 per lane each. The index moves by
+// __shfl here: the DPP form held the 8 indices in registers and pushed the 128-VGPR shared-row
+// kernels from 2 to 10 spilled registers
+template <int... T>
+__device__ __forceinline__ void gather_rows16(std::integer_sequence<int, T...>, int cm,
+                                              const float* base, uint32_t ld_bytes,
+                                              float4 (&dst)[sizeof...(T)]) {
+  ((dst[T] = ld4(row_at(base, __shfl(cm, T, 16), ld_bytes))), ...);
+}
+
 // Online-softmax accumulation of neighbours [beg, end) of row r (head of this lane); m is in
 // the base-2 logit domain.
 // HL: lanes per head (o_dim / 4) as a compile-time constant for the ATT kernels (0: runtime)
@@ -212,10 +245,19 @@ __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, in
       k = k < end ? k : end - 1;
       cm[q] = p.A.col[k];
     }
+    int cs[CH];
+    if constexpr (GROUP == 16 && PER == 1) {
+      bcast_cols16(std::make_integer_sequence<int, CH>{}, cm[0], cs);
+    } else {
+#pragma unroll
+      for (int t = 0; t < CH; ++t) cs[t] = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
+    }
+    const float* hb = p.h + head * p.head_stride + fo;
+    const uint32_t ldb = (uint32_t)(p.ldh * 4);
 #pragma unroll
     for (int t = 0; t < CH; ++t) {
-      const int c = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
-      dst[t] = ld4_src(p.h + (int64_t)c * p.ldh + head * p.head_stride + fo, c);
+      const int c = cs[t];
+      dst[t] = ld4_src(row_at(hb, c, ldb), c);
       if constexpr (!ATT) snd[t] = p.s_neigh[(int64_t)c * p.ld_sn + head];
     }
   };
@@ -232,6 +274,9 @@ __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, in
     } else {
       load_chunk(k0, xv, sn);
     }
+#if GAT_LOAD_FENCE
+    __builtin_amdgcn_sched_barrier(0);   // experiment: every gather of the chunk issued first
+#endif
     if constexpr (ATT) {
 #pragma unroll
       for (int t = 0; t < CH; ++t) sn[t] = group_sum<(HL > 0 ? HL : 1)>(dot4(xv[t], an));
@@ -365,11 +410,7 @@ __device__ __forceinline__ void gat_shared_rows16(const GatParams& p, int64_t r,
     int64_t k = k0 + gl;
     k = k < end ? k : end - 1;
     const int cm = p.A.col[k];
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int c = __shfl(cm, t, 16);
-      dst[t] = ld4_src(p.h + (int64_t)c * p.ldh + 4 * gl, c);
-    }
+    gather_rows16(std::make_integer_sequence<int, 8>{}, cm, p.h + 4 * gl, (uint32_t)(p.ldh * 4), dst);
   };
   // ATT + GAT_SHARED_PIPE: the next block's rows are in flight while this block's scores,
   // reduce-scatter and weighted sums run (the ATT form has twice the VALU work per
@@ -458,7 +499,7 @@ __device__ __forceinline__ void gat_shared_range(const GatParams& p, int64_t r, 
 #pragma unroll
     for (int t = 0; t < CH; ++t) {
       const int c = __shfl(cm[t / GROUP < PER ? t / GROUP : 0], t % GROUP, GROUP);
-      xv[t] = ld4(p.h + (int64_t)c * p.ldh + 4 * gl);
+      xv[t] = ld4(row_at(p.h + 4 * gl, c, (uint32_t)(p.ldh * 4)));
       if constexpr (H == 4) {
         const float4 s4 = ld4(p.s_neigh + (int64_t)c * p.ld_sn);
         sn[t][0] = s4.x; sn[t][1] = s4.y; sn[t][2] = s4.z; sn[t][3] = s4.w;
@@ -691,8 +732,10 @@ int gat_check_common(int64_t n_rows, int32_t heads, int32_t o_dim, const float* 
   const int F = heads * o_dim;
   const int width = mean_heads ? o_dim : F;
   GNNREC_REQUIRE(head_stride >= 0 && !(head_stride & 3), "gat: head_stride must be >= 0 and %% 4 == 0");
-  GNNREC_REQUIRE(hfeat && aligned16(hfeat) && !(ldh & 3) && ldh >= (heads - 1) * head_stride + o_dim,
-                 "gat: hfeat must be 16-B aligned, ld %% 4 == 0, ld >= (heads-1)*head_stride + o_dim");
+  GNNREC_REQUIRE(hfeat && aligned16(hfeat) && !(ldh & 3) && ldh >= (heads - 1) * head_stride + o_dim &&
+                     ldh < ((int64_t)1 << 30),
+                 "gat: hfeat must be 16-B aligned, ld %% 4 == 0, (heads-1)*head_stride + o_dim <= ld "
+                 "< 2^30 (row offsets are formed as 32-bit ld bytes x column)");
   GNNREC_REQUIRE((epi & GNNREC_EPI_NO_Y) || (out && aligned16(out) && !(ldo & 3) && ldo >= width),
                  "gat: bad out");
   GNNREC_REQUIRE(!(epi & GNNREC_EPI_ACC_INIT) || (self && aligned16(self) && !(ld_self & 3) && ld_self >= width),
@@ -882,8 +925,8 @@ extern "C" int gnnrec_gat_heavy_f32(const int32_t* col, const int64_t* seg_row,
   if (n_heavy == 0) return GNNREC_OK;
   GNNREC_REQUIRE(col && seg_row && seg_beg && seg_end && heavy_rows && heavy_seg_ptr && work &&
                      hfeat && s_self && s_neigh && aligned16(work) && aligned16(hfeat) && !(ldh & 3) &&
-                     head_stride >= 0 && !(head_stride & 3),
-                 "gat_heavy: null or misaligned operand");
+                     ldh < ((int64_t)1 << 30) && head_stride >= 0 && !(head_stride & 3),
+                 "gat_heavy: null or misaligned operand (or ld >= 2^30)");
   GNNREC_REQUIRE(ld_ss >= heads && ld_sn >= heads, "gat_heavy: score row strides must be >= heads");
   GatParams p{Csr{nullptr, col, nullptr, 0}, hfeat, ldh, head_stride, s_self, s_neigh, ld_ss, ld_sn, heads, o_dim, slope,
               mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, 0,
@@ -910,8 +953,8 @@ extern "C" int gnnrec_gat_heavy_att_f32(const int32_t* col, const int64_t* seg_r
   if (n_heavy == 0) return GNNREC_OK;
   GNNREC_REQUIRE(col && seg_row && seg_beg && seg_end && heavy_rows && heavy_seg_ptr && work &&
                      hfeat && aligned16(work) && aligned16(hfeat) && !(ldh & 3) &&
-                     head_stride >= 0 && !(head_stride & 3),
-                 "gat_heavy_att: null or misaligned operand");
+                     ldh < ((int64_t)1 << 30) && head_stride >= 0 && !(head_stride & 3),
+                 "gat_heavy_att: null or misaligned operand (or ld >= 2^30)");
   if (int st = gat_check_att(att, hself, ld_hself, ldh, o_dim)) return st;
   GatParams p{Csr{nullptr, col, nullptr, 0}, hfeat, ldh, head_stride, nullptr, nullptr, 0, 0, heads, o_dim, slope,
               mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, 0,

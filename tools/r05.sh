@@ -249,6 +249,31 @@ case ${1:?call} in
           >> $OUT/c20_gat_hot.jsonl 2>> $OUT/c20.err
     done
     ;;
+  c21)
+    # GAT column indices broadcast by DPP row_newbcast instead of __shfl (ds_bpermute): GAT
+    # tests, then config 5 at 5M x 5M against the previous build, same box
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+        tests/test_gat_att_gpu.py tests/test_gat_train_gpu.py tests/test_real_shapes_gpu.py \
+        tests/test_models_gpu.py > $OUT/c21_tests.log 2>&1
+    : > $OUT/c21_gat.jsonl
+    for v in base new base new; do
+      L=tools/ab/pre_dpp.so; [ $v = new ] && L=gnn-recommendations_amd/lib/libgnnrec.so
+      GNNREC_LIB=$L timeout -k 10 300 python -u tools/exp_gat_variants.py --tag $v >> $OUT/c21_gat.jsonl 2>> $OUT/c21.err
+    done
+    ;;
+  c22)
+    # GAT gathers: single-instruction row addressing (row_at) everywhere, DPP index broadcast in
+    # the head-major kernels only; tests, then config 5 at 5M x 5M against the build before
+    # c21, same box
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+        tests/test_gat_att_gpu.py tests/test_gat_train_gpu.py tests/test_real_shapes_gpu.py \
+        tests/test_models_gpu.py tests/test_fullsize_models_gpu.py > $OUT/c22_tests.log 2>&1
+    : > $OUT/c22_gat.jsonl
+    for v in base new base new; do
+      L=tools/ab/pre_dpp.so; [ $v = new ] && L=gnn-recommendations_amd/lib/libgnnrec.so
+      GNNREC_LIB=$L timeout -k 10 300 python -u tools/exp_gat_variants.py --tag $v >> $OUT/c22_gat.jsonl 2>> $OUT/c22.err
+    done
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
