@@ -109,9 +109,6 @@ __device__ __forceinline__ void gat_finish(const GatParams& p, int64_t r, float4
 // a neighbour row's float4 (plain policy: non-temporal cold-row gathers were measured slower in
 // every form)
 __device__ __forceinline__ float4 ld4_src(const float* p, int) { return ld4(p); }
-#ifndef GAT_LOAD_FENCE
-#define GAT_LOAD_FENCE 0
-#endif
 #ifndef GAT_MAIN_PIPE
 #define GAT_MAIN_PIPE 0
 #endif
@@ -274,9 +271,6 @@ __device__ __forceinline__ void gat_accumulate(const GatParams& p, int64_t r, in
     } else {
       load_chunk(k0, xv, sn);
     }
-#if GAT_LOAD_FENCE
-    __builtin_amdgcn_sched_barrier(0);   // experiment: every gather of the chunk issued first
-#endif
     if constexpr (ATT) {
 #pragma unroll
       for (int t = 0; t < CH; ++t) sn[t] = group_sum<(HL > 0 ? HL : 1)>(dot4(xv[t], an));
