@@ -274,6 +274,18 @@ case ${1:?call} in
       GNNREC_LIB=$L timeout -k 10 300 python -u tools/exp_gat_variants.py --tag $v >> $OUT/c22_gat.jsonl 2>> $OUT/c22.err
     done
     ;;
+  c23)
+    # shared-row GAT kernel: block max by DPP instead of __shfl_xor; GAT tests, then config 5
+    # at 5M x 5M against the previous build, same box
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+        tests/test_gat_att_gpu.py tests/test_real_shapes_gpu.py tests/test_models_gpu.py \
+        > $OUT/c23_tests.log 2>&1
+    : > $OUT/c23_gat.jsonl
+    for v in base new base new; do
+      L=tools/ab/pre_dppmax.so; [ $v = new ] && L=gnn-recommendations_amd/lib/libgnnrec.so
+      GNNREC_LIB=$L timeout -k 10 300 python -u tools/exp_gat_variants.py --tag $v >> $OUT/c23_gat.jsonl 2>> $OUT/c23.err
+    done
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
