@@ -286,6 +286,25 @@ case ${1:?call} in
       GNNREC_LIB=$L timeout -k 10 300 python -u tools/exp_gat_variants.py --tag $v >> $OUT/c23_gat.jsonl 2>> $OUT/c23.err
     done
     ;;
+  c24)
+    # the final GAT build at full size: config 5 at 5M x 5M and at G1B, both checked
+    timeout -k 10 600 python -u tools/bench_configs.py $C5 --steps 5 > $OUT/c24_config5_g250m.jsonl \
+        2> $OUT/c24_config5_g250m.err
+    timeout -k 10 900 python -u tools/bench_configs.py --configs 5 --g1b --steps 5 \
+        > $OUT/c24_config5_g1b.jsonl 2> $OUT/c24_config5_g1b.err
+    ;;
+  c25)
+    # head-major GAT kernels with the chunk's scores pinned before its first block (all 16
+    # gathers issued together instead of 8 + 8 behind the first block's work), same box
+    GNNREC_LIB=tools/ab/gat_pin.so timeout -k 10 600 python -u -m pytest -x -v --timeout 300 \
+        --timeout-method thread -m gpu tests/test_gat_att_gpu.py tests/test_real_shapes_gpu.py \
+        tests/test_models_gpu.py > $OUT/c25_tests.log 2>&1
+    : > $OUT/c25_gat.jsonl
+    for v in base pin base pin; do
+      L=gnn-recommendations_amd/lib/libgnnrec.so; [ $v = pin ] && L=tools/ab/gat_pin.so
+      GNNREC_LIB=$L timeout -k 10 300 python -u tools/exp_gat_variants.py --tag $v >> $OUT/c25_gat.jsonl 2>> $OUT/c25.err
+    done
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
