@@ -365,7 +365,8 @@ int gnnrec_dense_transform_f32(int64_t n_rows, const float* n, int64_t ldn, floa
  *   o[r, h, :] = sum_j a_j * hfeat[j, h, :]
  * (single pass, online max/sum rescaling per block of 8 neighbours in base 2, fp32).
  * hfeat[j, h, :] starts at
- * hfeat + j*ldh + h*head_stride: head_stride = o_dim for the head-major [N, heads*o_dim]
+ * hfeat + j*ldh + h*head_stride (ldh < 2^30: the kernels form a row's offset as one 32-bit x
+ * 32-bit multiply of j and ldh*4): head_stride = o_dim for the head-major [N, heads*o_dim]
  * table of the per-head W_h x; head_stride = 0 lets every head aggregate the same row (the
  * layer input x, with W_h applied by the caller afterwards: sum_j a_j W_h x_j =
  * W_h sum_j a_j x_j — the head-averaged last layer then gathers o_dim instead of heads*o_dim
