@@ -316,3 +316,18 @@ def test_vendor_comparator_library_loads():
     deps = subprocess.run(["ldd", str(ROOT / "gnn-recommendations_amd" / "lib" / "libgnnrec.so")],
                           capture_output=True, text=True).stdout
     assert "rocsparse" not in deps
+
+
+def test_gat_entry_points_refuse_row_strides_past_2_30():
+    """The GAT kernels form a gathered row's offset as a 32-bit x 32-bit multiply of its
+    column and ldh * 4 bytes (csrc/gat.hip row_at), so every GAT entry point refuses
+    ldh >= 2^30 before any device work (no GPU needed to reach the check)."""
+    L = _lib.lib()
+    a = 1 << 12                                     # 16-B aligned stand-in addresses
+    big = 1 << 30
+    st = L.gnnrec_gat_aggregate_att_f32(a, a, 10, a, big, 16, a, 64, a, 4, 16, 0.2, 0, 0, a, 64,
+                                        0, None, 64, None, 64, 1.0, 0, None)
+    assert st == -1 and "2^30" in L.gnnrec_last_error().decode()
+    st = L.gnnrec_gat_heavy_att_f32(a, a, a, a, 1, a, a, 1, a, a, big, 16, a, 64, a, 4, 16, 0.2,
+                                    0, 0, a, 64, 0, None, 64, None, 64, 1.0, None, 0, None)
+    assert st == -1 and "2^30" in L.gnnrec_last_error().decode()
