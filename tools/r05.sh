@@ -305,6 +305,11 @@ case ${1:?call} in
       GNNREC_LIB=$L timeout -k 10 300 python -u tools/exp_gat_variants.py --tag $v >> $OUT/c25_gat.jsonl 2>> $OUT/c25.err
     done
     ;;
+  c26)
+    # where the BPR training steps (configs 6 and 9) spend their time: kernel trace
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c26_trainkt -o run -- \
+        python3 tools/bench_configs.py --configs 6 9 --steps 5 --warmup 2 > $OUT/c26_trainkt.jsonl 2> $OUT/c26_trainkt.err
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
