@@ -25,6 +25,9 @@ ap.add_argument("--reps", type=int, default=10)
 ap.add_argument("--plans", nargs="*", default=[],
                 help="heavy-segment plans timed in this one process (same graph): 'column', "
                      "'row' or 'panel:<columns>:<min edges per panel>'")
+ap.add_argument("--splits", nargs="*", default=[],
+                help="heavy-row threshold / segment length pairs timed in this one process: "
+                     "'<threshold>:<segment>' (default plan order)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 g = powerlaw_graph(*a.shape, 0.9, 0, 16, device=dev)
@@ -50,12 +53,16 @@ def run(tag):
     print(json.dumps({"tag": tag, "lib": os.environ.get("GNNREC_LIB", "default"),
                       "env": {k: v for k, v in os.environ.items() if k.startswith("GNNREC_GAT")},
                       "plan": [F.GAT_SEGMENT_ORDER, F.GAT_PANEL, F.GAT_PANEL_MIN_EDGES],
+                      "split": [F.GAT_HEAVY_THRESHOLD, F.GAT_SEGMENT],
                       "shape": a.shape, "nnz": g.nnz, "ms_median": float(np.median(ms)),
                       "ms": ms, "abs_sum": sig, "time": time.strftime("%H:%M:%S")}), flush=True)
 
 
-if not a.plans:
+if not a.plans and not a.splits:
     run(a.tag)
+for spec in a.splits:
+    F.GAT_HEAVY_THRESHOLD, F.GAT_SEGMENT = (int(v) for v in spec.split(":"))
+    run(f"{a.tag}_split{spec}")
 for spec in a.plans:
     parts = spec.split(":")
     F.GAT_SEGMENT_ORDER = parts[0]

@@ -310,6 +310,12 @@ case ${1:?call} in
     timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c26_trainkt -o run -- \
         python3 tools/bench_configs.py --configs 6 9 --steps 5 --warmup 2 > $OUT/c26_trainkt.jsonl 2> $OUT/c26_trainkt.err
     ;;
+  c27)
+    # heavy-row threshold / segment length at G1B, one process, same graph
+    timeout -k 10 1000 python -u tools/exp_gat_variants.py --tag g1b --shape 10000000 10000000 1000000000 \
+        --reps 5 --splits 2048:1024 1024:512 1024:1024 4096:1024 4096:2048 2048:512 2048:2048 2048:1024 \
+        > $OUT/c27_g1b_splits.jsonl 2> $OUT/c27.err
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
