@@ -316,6 +316,26 @@ case ${1:?call} in
         --reps 5 --splits 2048:1024 1024:512 1024:1024 4096:1024 4096:2048 2048:512 2048:2048 2048:1024 \
         > $OUT/c27_g1b_splits.jsonl 2> $OUT/c27.err
     ;;
+  c28)
+    # NGCF + GAS transform software-pipelined per wave (GNNREC_TRANSFORM_PIPE=1, 8 waves per
+    # workgroup): its tests, then the transform alone and config 3 against the shipped build
+    GNNREC_LIB=tools/ab/tr_pipe8.so timeout -k 10 600 python -u -m pytest -x -v --timeout 300 \
+        --timeout-method thread -m gpu tests/test_kernels_gpu.py -k "ngcf or transform or gas" \
+        > $OUT/c28_tests.log 2>&1
+    GNNREC_LIB=tools/ab/tr_pipe8.so timeout -k 10 600 python -u -m pytest -x -v --timeout 300 \
+        --timeout-method thread -m gpu tests/test_fullsize_models_gpu.py -k config3 >> $OUT/c28_tests.log 2>&1
+    : > $OUT/c28_transform.jsonl; : > $OUT/c28_config3.jsonl
+    for v in base pipe base pipe; do
+      L=gnn-recommendations_amd/lib/libgnnrec.so; [ $v = pipe ] && L=tools/ab/tr_pipe8.so
+      GNNREC_LIB=$L timeout -k 10 120 python -u tools/exp_transform.py | sed "s/^{/{\"variant\": \"$v\", /" \
+          >> $OUT/c28_transform.jsonl 2>> $OUT/c28.err
+      GNNREC_LIB=$L timeout -k 10 300 python -u tools/bench_configs.py --configs 3 --steps 10 --no-ref-check \
+          | sed "s/^{/{\"variant\": \"$v\", /" >> $OUT/c28_config3.jsonl 2>> $OUT/c28.err
+    done
+    GNNREC_LIB=tools/ab/tr_pipe8.so timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d $OUT/c28_c3kt_pipe -o run -- python3 tools/bench_configs.py --configs 3 --steps 5 --warmup 1 \
+        --no-ref-check > $OUT/c28_c3kt_pipe.jsonl 2>> $OUT/c28.err
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
