@@ -306,11 +306,6 @@ __global__ __launch_bounds__(64 * NW) void spmm_mfma_kernel(DenseParams p) {
 #define GNNREC_TRANSFORM_PREFETCH 1
 #endif
 constexpr bool kTransformPrefetch = GNNREC_TRANSFORM_PREFETCH != 0;
-// experiment (A/B only): the NGCF + 8x8-GAS instance software-pipelined per wave — tile i's GAS
-// product and row stores run inside tile i+1's MFMA half-groups instead of after them
-#ifndef GNNREC_TRANSFORM_PIPE
-#define GNNREC_TRANSFORM_PIPE 0
-#endif
 #ifndef GNNREC_TRANSFORM_GAS_DPP
 #define GNNREC_TRANSFORM_GAS_DPP 0
 #endif
@@ -442,115 +437,6 @@ __global__ __launch_bounds__(64 * NW) void transform64_kernel(DenseParams p) {
   // output rows: lane covers rows 4 it + (lane >> 4), columns 4 (lane & 15) .. +3, it = 0..3
   const int lr = lane >> 4, lc = 4 * (lane & 15);
   int64_t tile = (int64_t)blockIdx.x * NW + wave;
-  if constexpr (MODE == 0 && GASV && GNNREC_TRANSFORM_PIPE != 0 && !gas_dpp) {
-    // o tile of tile `pt` in ot: its GAS (step s of 16: block 2 k4 + s / 8, input column s % 8)
-    // and its whole-row stores
-    float ov[16], z[16];
-    auto gas_read = [&]() {
-      const float* orow = ot + i16 * LDO + 16 * k4;
-#pragma unroll
-      for (int t4 = 0; t4 < 4; ++t4) {
-        const float4 v = *reinterpret_cast<const float4*>(orow + 4 * t4);
-        ov[4 * t4] = v.x; ov[4 * t4 + 1] = v.y; ov[4 * t4 + 2] = v.z; ov[4 * t4 + 3] = v.w;
-      }
-#pragma unroll
-      for (int e = 0; e < 16; ++e) z[e] = 0.f;
-    };
-    auto gas_step = [&](int s) {
-      const int hh = s >> 3, c = s & 7;
-      const float* W = wv_lds + (16 * k4 + kVbs * hh) * kVbs + c * kVbs;
-      const float4 w0 = *reinterpret_cast<const float4*>(W);
-      const float4 w1 = *reinterpret_cast<const float4*>(W + 4);
-      const float wc[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-      const float x = ov[kVbs * hh + c];
-#pragma unroll
-      for (int e = 0; e < kVbs; ++e) {
-        z[kVbs * hh + e] = __builtin_fmaf(x, wc[e], z[kVbs * hh + e]);
-        asm volatile("" : "+v"(z[kVbs * hh + e]));   // keep the step in its half-group
-      }
-    };
-    auto gas_write_store = [&](int64_t pt) {
-      float* wrow = ot + i16 * LDO;
-#pragma unroll
-      for (int t = 0; t < 16; ++t) wrow[inv_lds[16 * k4 + t]] = z[t];
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        const int row = 4 * it + lr;
-        const int64_t r = pt * 16 + row;
-        const float4 o = *reinterpret_cast<const float4*>(ot + row * LDO + lc);
-        if (r < p.A.n_rows && p.y) *reinterpret_cast<float4*>(p.y + r * p.ldy + lc) = o;
-      }
-    };
-    bool pend = false;
-    int64_t pt = 0;
-    const float4* bl = reinterpret_cast<const float4*>(b_lds) + lane;
-    load(tile);
-    for (; tile < n_tiles; tile += stride) {
-      float an[4][4], ax[4][4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        an[t][0] = pn[t].x; an[t][1] = pn[t].y; an[t][2] = pn[t].z; an[t][3] = pn[t].w;
-        ax[t][0] = px[t].x * pn[t].x; ax[t][1] = px[t].y * pn[t].y;
-        ax[t][2] = px[t].z * pn[t].z; ax[t][3] = px[t].w * pn[t].w;
-      }
-      load(tile + stride);
-      gas_read();   // unconditional (the first tile's is discarded): one basic block per half-group
-
-      floatx4 c1[4], c2[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) c1[nt] = c2[nt] = floatx4{0.f, 0.f, 0.f, 0.f};
-      float4 bc[4], bn[4];
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt) bc[nt] = bl[nt * 64];
-#pragma unroll
-      for (int h = 0; h < 8; ++h) {
-        const int t = h / 2, part = h % 2;
-        if (h + 1 < 8) {
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt)
-            bn[nt] = bl[((((h + 1) % 2) * 4 + (h + 1) / 2) * 4 + nt) * 64];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float a = part == 0 ? an[t][q] : ax[t][q];
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) {
-            const float bq = q == 0 ? bc[nt].x : q == 1 ? bc[nt].y : q == 2 ? bc[nt].z : bc[nt].w;
-            if (part == 0)
-              c1[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bq, c1[nt], 0, 0, 0);
-            else
-              c2[nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bq, c2[nt], 0, 0, 0);
-          }
-        }
-        gas_step(2 * h);       // the previous tile's GAS in this half-group's MFMA shadow
-        gas_step(2 * h + 1);
-        if (h + 1 < 8) {
-#pragma unroll
-          for (int nt = 0; nt < 4; ++nt) bc[nt] = bn[nt];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (pend) gas_write_store(pt);
-#pragma unroll
-      for (int nt = 0; nt < 4; ++nt)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float v = (c1[nt][q] + bias1[nt]) + (c2[nt][q] + bias2[nt]);
-          v = v > 0.f ? v : v * p.slope;
-          ot[(4 * k4 + q) * LDO + 16 * nt + i16] = v;
-        }
-      pend = true;
-      pt = tile;
-    }
-    if (pend) {
-      gas_read();
-#pragma unroll
-      for (int st = 0; st < 16; ++st) gas_step(st);
-      gas_write_store(pt);
-    }
-    return;
-  }
   if (kTransformPrefetch) load(tile);
   for (; tile < n_tiles; tile += stride) {
     if (!kTransformPrefetch) load(tile);
