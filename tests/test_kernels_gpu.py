@@ -172,8 +172,9 @@ def test_ngcf_layers_vs_reference(cuda, fused):
 
 @pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("d", [32, 64, 128])
-def test_ngcf_gas_vs_oracle(cuda, d, fused):
-    g, (rp, col, val) = random_graph(700, 900, 9000, d, cuda)
+@pytest.mark.parametrize("n_items", [900, 905])    # 905: a 5-row tail tile (rows past the end
+def test_ngcf_gas_vs_oracle(cuda, d, fused, n_items):   # are loaded clamped, never stored)
+    g, (rp, col, val) = random_graph(700, n_items, 9000, d, cuda)
     rng = np.random.default_rng(d)
     x = rng.standard_normal((g.shape[0], d)).astype(np.float32) * 0.1
     W1, W2 = (rng.standard_normal((2, d, d)) / np.sqrt(d)).astype(np.float32)
