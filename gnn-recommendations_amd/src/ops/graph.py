@@ -502,14 +502,18 @@ class CsrGraph:
             node_cols = (n == m and info is None) or (info is not None and info.world == 1
                                                       and m >= n)
             if node_cols and self.row_ptr.numel() == n + 1 and self.nnz > 0:
-                deg = (self.row_ptr[1:] - self.row_ptr[:-1]).cpu().numpy().astype(np.float32)
-                dis = inv_sqrt_degrees(deg, "symmetric")
-                table = np.unique(dis)
+                # dis per DISTINCT degree on the host (numpy float32 power, as before), spread to
+                # the rows on the operand's device: the rows' degrees never leave it
+                dev = self.device
+                udeg, inv = torch.unique(self.row_ptr[1:] - self.row_ptr[:-1], sorted=True,
+                                         return_inverse=True)
+                dis_u = inv_sqrt_degrees(udeg.cpu().numpy().astype(np.float32), "symmetric")
+                table = np.unique(dis_u)
                 if table.size <= _lib.TILED_MAX_CLASSES:
-                    cls = np.zeros(m, np.uint8)
-                    cls[:n] = np.searchsorted(table, dis)
-                    dev = self.device
-                    out = (torch.from_numpy(dis).to(dev), torch.from_numpy(cls).to(dev),
+                    cls_u = torch.from_numpy(np.searchsorted(table, dis_u).astype(np.uint8)).to(dev)
+                    cls = torch.zeros(m, dtype=torch.uint8, device=dev)
+                    cls[:n] = cls_u[inv]
+                    out = (torch.from_numpy(dis_u).to(dev)[inv].contiguous(), cls,
                            torch.from_numpy(table).to(dev))
             self._plans["degree_factors"] = out
         return self._plans["degree_factors"]

@@ -331,3 +331,22 @@ def test_gat_entry_points_refuse_row_strides_past_2_30():
     st = L.gnnrec_gat_heavy_att_f32(a, a, a, a, 1, a, a, 1, a, a, big, 16, a, 64, a, 4, 16, 0.2,
                                     0, 0, a, 64, 0, None, 64, None, 64, 1.0, None, 0, None)
     assert st == -1 and "2^30" in L.gnnrec_last_error().decode()
+
+
+def test_degree_factors_match_the_per_row_restatement():
+    """CsrGraph.degree_factors (dis per distinct degree, spread to rows on the operand's
+    device) equals the per-row numpy computation bit for bit, isolated rows included."""
+    from src.ops.graph import inv_sqrt_degrees
+    rng = np.random.default_rng(3)
+    g = CsrGraph.from_interactions(rng.integers(0, 500, 3000), rng.integers(0, 300, 3000),
+                                   700, 400)
+    rowf, cls, table = g.degree_factors()
+    deg = (g.row_ptr[1:] - g.row_ptr[:-1]).numpy().astype(np.float32)
+    assert (deg == 0).any()
+    dis = inv_sqrt_degrees(deg, "symmetric")
+    ref_table = np.unique(dis)
+    ref_cls = np.zeros(g.shape[1], np.uint8)
+    ref_cls[:g.shape[0]] = np.searchsorted(ref_table, dis)
+    np.testing.assert_array_equal(rowf.numpy().view(np.uint32), dis.view(np.uint32))
+    np.testing.assert_array_equal(cls.numpy(), ref_cls)
+    np.testing.assert_array_equal(table.numpy(), ref_table)
