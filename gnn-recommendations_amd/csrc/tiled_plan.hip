@@ -37,6 +37,11 @@ constexpr uint32_t kPRowMask = (1u << kPRowBits) - 1;
 constexpr int kPMaxRows = GNNREC_TILED_MAX_ROWS + 1;
 constexpr int kPKeys = 2048;                      // >= rows per block, a power of two
 constexpr int kPNMax = (1 << 21) - 1;             // run length field of a sort key
+// a run (one row's slots in one step) is kept in 16 bits in LDS: 23 040 B of LDS per
+// workgroup, 7 workgroups per CU, so G100M's 1 791 blocks are planned in one round (6 per CU
+// and 32-bit lengths left 255 blocks for a second round). Longer runs fail the plan (error 3).
+constexpr int kPLenMax = 32767;
+static_assert(kPLenMax <= kPNMax, "run length within the key field");
 constexpr int kPMaxPanel = 1 << 20;
 constexpr uint64_t kPPad = ~0ull;
 static_assert(kPV == 64, "one lane per slot stream");
@@ -137,7 +142,8 @@ __device__ void bitonic64(uint32_t* s, int n, int lane) {
 }
 
 __global__ __launch_bounds__(64) void tiled_plan_kernel(PlanArgs a, int emit) {
-  __shared__ int32_t s_pos[kPMaxRows], s_end[kPMaxRows], s_len[kPMaxRows];
+  __shared__ int32_t s_pos[kPMaxRows], s_end[kPMaxRows];
+  __shared__ int16_t s_len[kPMaxRows];
   __shared__ uint32_t s_key[kPKeys];
   __shared__ uint8_t s_asg[kPKeys];
   const int lane = threadIdx.x;
@@ -188,8 +194,8 @@ __global__ __launch_bounds__(64) void tiled_plan_kernel(PlanArgs a, int emit) {
         if (i < nr) {
           const int32_t k = s_pos[i], e = s_end[i];
           while (k + n < e && col[k + n] / a.panel == pm) ++n;
-          s_len[i] = n;
-          too_long |= n > kPNMax;
+          s_len[i] = (int16_t)min(n, kPLenMax);
+          too_long |= n > kPLenMax;
         }
         const uint64_t m = __ballot(n > 0);
         if (n > 0)

@@ -29,7 +29,8 @@ from . import _lib
 # arrays either way)
 TILED_PLANNER = "device"
 # gnnrec_tiled_plan_device error words: 1 negative column (the host planner's EINVAL),
-# 2 scratch too small, 3 a run longer than 2^21, 4 count / emit disagree
+# 2 scratch too small, 3 a run (one row's slots in one step) longer than 32 767, 4 count / emit
+# disagree
 _DEVICE_PLAN_ERRORS = {1: ValueError}
 # slots of one step (a panel of a block) the device planner's scratch is sized for first
 TILED_PLAN_STEP_CAP = 32768
@@ -37,8 +38,9 @@ TILED_PLAN_STEP_CAP = 32768
 # power-law operand's hub rows make planning serial (config 5's 5M x 5M rows of degree
 # 2 049-65 536: 24 s; with its 1.48M-degree row: not done in 5 minutes,
 # profiles/r05/c12_heavy_tiled.jsonl). The SpMM itself never plans rows past
-# functional.TILED_MAX_DEGREE = 4 096 (they take the CSR kernel).
-TILED_PLAN_MAX_DEGREE = 65536
+# functional.TILED_MAX_DEGREE = 4 096 (they take the CSR kernel). 32 767 also bounds a run
+# (one row's slots in one step), which the device planner keeps in 16 bits.
+TILED_PLAN_MAX_DEGREE = 32767
 # factored plans (gnnrec_tiled_plan_factor, DESIGN.md §3.1c "plan values"): a device graph's
 # plan carries 1-byte column classes instead of fp32 values whenever every value is
 # fl(dis_r * dis_c) with dis from the row counts and at most TILED_MAX_CLASSES distinct dis
@@ -638,8 +640,8 @@ class CsrGraph:
         n, W = self.n_rows, _lib.TILED_WAVES
         per_wg = 8 * L.gnnrec_tiled_plan_device_scratch_words(cap, 1)
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
-        # one 64-lane workgroup per block (LDS: up to 6 per CU), scratch at most ~4 GB
-        wg = max(1, min(nb, 6 * cus, (4 << 30) // max(per_wg, 1)))
+        # one 64-lane workgroup per block (23 KB of LDS: 7 per CU), scratch at most ~4 GB
+        wg = max(1, min(nb, 7 * cus, (4 << 30) // max(per_wg, 1)))
         scratch = torch.empty(max(1, L.gnnrec_tiled_plan_device_scratch_words(cap, wg)),
                               dtype=torch.int64, device=dev)
         chunks = torch.zeros(max(1, nb * W), dtype=torch.int64, device=dev)

@@ -200,7 +200,8 @@ int gnnrec_tiled_plan_free(void* plan);
  * the largest row_ptr[min(n_rows, (b+1) R)] - row_ptr[b R]; a smaller bound that a step
  * exceeds fails the pass with error 2, to be retried with a larger one); err: one device
  * int32, zeroed by the caller, non-zero after a failed pass (1 negative column, 2 scratch
- * too small, 3 a run longer than 2^21, 4 count / emit mismatch). */
+ * too small, 3 a run — one row's slots in one step — longer than 32 767, 4 count / emit
+ * mismatch). */
 int64_t gnnrec_tiled_plan_device_scratch_words(int64_t max_block_nnz, int32_t workgroups);
 int gnnrec_tiled_plan_device(const int64_t* row_ptr, const int32_t* col, const float* val,
                              int64_t n_rows, int32_t rows_per_block, int32_t panel,

@@ -336,6 +336,17 @@ case ${1:?call} in
         -d $OUT/c28_c3kt_pipe -o run -- python3 tools/bench_configs.py --configs 3 --steps 5 --warmup 1 \
         --no-ref-check > $OUT/c28_c3kt_pipe.jsonl 2>> $OUT/c28.err
     ;;
+  c30)
+    # device planner with 16-bit run lengths in LDS (7 workgroups per CU: one round of blocks):
+    # the planner tests (device == host plan, bit for bit), the tiled hop tests, then the bench
+    # (operand prep phases) and a planner kernel trace
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+        tests/test_tiled_plan_gpu.py tests/test_long_rows_gpu.py tests/test_kernels_gpu.py \
+        tests/test_offsets_gpu.py > $OUT/c30_tests.log 2>&1
+    timeout -k 10 600 python bench.py --no-cpu-baseline --no-vendor > $OUT/c30_bench.json 2> $OUT/c30_bench.err
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c30_kt -o run -- \
+        python3 bench.py --no-cpu-baseline --no-vendor --steps 5 > $OUT/c30_kt.json 2> $OUT/c30_kt.err
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
