@@ -347,6 +347,13 @@ case ${1:?call} in
     timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c30_kt -o run -- \
         python3 bench.py --no-cpu-baseline --no-vendor --steps 5 > $OUT/c30_kt.json 2> $OUT/c30_kt.err
     ;;
+  c31)
+    # the N = 2 bench path on the final tree, rehearsed on one GPU with gloo (host-staged
+    # exchange, not RCCL): layouts, exchange candidates, the default self-check and its labels
+    timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+        --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --dist-backend gloo \
+        --steps 3 --warmup 1 --no-cpu-baseline --no-vendor > $OUT/c31_n2_gloo.json 2> $OUT/c31_n2_gloo.err
+    ;;
   *) echo "unknown call $1" >&2; exit 2 ;;
 esac
 echo done
