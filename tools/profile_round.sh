@@ -49,7 +49,7 @@ for step in $STEPS; do
       python tools/pmc_summarize.py "$(find $OUT/pmc_fetch -name "*counter_collection.csv" -print -quit)" \
           "$(find $OUT/pmc_write -name "*counter_collection.csv" -print -quit)" $OUT/pmc_summary.json \
           ${KERNEL:-tiled_hop_kernel} $OUT/pmc_fetch_bench.json
-      python tools/pmc_l2.py "$(find $OUT/pmc_l2 -name "*counter_collection.csv" -print -quit)" \
+      python tools/pmc_table.py --l2 "$(find $OUT/pmc_l2 -name "*counter_collection.csv" -print -quit)" \
           > $OUT/l2_hit.txt ;;
     configs)
       timeout -k 10 900 python -u tools/bench_configs.py --configs ${CONFIGS:-2 3 4 5 6 9} \
