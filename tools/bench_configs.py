@@ -122,6 +122,31 @@ def _close(got, ref, rtol=1e-4, atol=1e-6) -> dict:
             "within_north_star_1e-4": mx <= 1e-4}
 
 
+def gat_cost(n_rows, nnz, ms) -> dict:
+    """Config 5's forward against the HBM roofline and the request model.
+    Compulsory bytes per forward (GAT d=64, 4 heads, K=3, layer mean fused into the epilogues):
+    per layer the CSR (8 B row_ptr per row, 4 B col per edge); layers 1-2 the projection (x in,
+    h out: 256 + 256 B per row), one read of the gathered h table (256), y out (256), the layer
+    mean accumulator (written at layer 1, read + written at 2: 256 / 512); layer 3 one read of
+    the gathered x table (256), the per-head aggregates z out and back into the head-mean GEMM
+    (1 024 + 1 024), the accumulator read and the mean out (256 + 256). The request model: a
+    neighbour's 256-B row is two 128-B lines per layer, priced at the random-miss cost of
+    §3.1c (15.4 ps per line, the 65 G lines/s probe rate) with no L2 hits."""
+    per_row = 3 * 8 + (256 + 256 + 256 + 256 + 256) + (256 + 256 + 256 + 256 + 512) \
+        + (256 + 1024 + 1024 + 256 + 256)
+    algo = n_rows * per_row + 3 * 4 * nnz
+    lines = 3 * 2 * nnz
+    gbps = algo / (ms * 1e-3) / 1e9
+    return {"roofline": {"bound": "hbm", "algorithmic_bytes": algo, "achieved": gbps,
+                         "peak": 8000.0, "unit": "GB/s", "frac": gbps / 8000.0,
+                         "bytes_model": "per row 5 656 B (3 layers' tables, projections, "
+                                        "aggregates, mean accumulator) + 12 B per edge"},
+            "request_model": {"gathered_lines": lines, "G_lines_per_s": lines / (ms * 1e-3) / 1e9,
+                              "all_miss_ms": lines * 15.4e-9, "frac": lines * 15.4e-9 / ms,
+                              "what": "2 x 128-B lines per neighbour per layer at 15.4 ps each "
+                                      "(no L2 hits) / the measured forward"}}
+
+
 def torch_csr(g, device):
     """The operand as a torch CSR tensor on the device (ATen's ROCm sparse path)."""
     return torch.sparse_csr_tensor(g.row_ptr.to(device), g.col.to(device).long(),
@@ -443,6 +468,7 @@ def main(argv=None):
                    "ms": t, "edges_per_s": 3 * g.nnz / (t * 1e-3), "graph_build_s": build_s,
                    "shard_nnz_max": int(rank_max(dg.shard.nnz, world, device)),
                    "exchange": dg.exchange_mode if world > 1 else None}
+            rec.update(gat_cost(shape[0] + shape[1], g.nnz, t))
             if a.verify:
                 del x0p
                 g1 = g.to(device)

@@ -293,6 +293,13 @@ case ${1:?call} in
     timeout -k 10 900 python -u tools/bench_configs.py --configs 5 --g1b --steps 5 \
         > $OUT/c24_config5_g1b.jsonl 2> $OUT/c24_config5_g1b.err
     ;;
+  c32)
+    # config 5 records with the roofline and request-model fields (5M x 5M and G1B, checked)
+    timeout -k 10 600 python -u tools/bench_configs.py $C5 --steps 5 > $OUT/c32_config5_g250m.jsonl \
+        2> $OUT/c32_config5_g250m.err
+    timeout -k 10 900 python -u tools/bench_configs.py --configs 5 --g1b --steps 5 \
+        > $OUT/c32_config5_g1b.jsonl 2> $OUT/c32_config5_g1b.err
+    ;;
   c25)
     # head-major GAT kernels with the chunk's scores pinned before its first block (all 16
     # gathers issued together instead of 8 + 8 behind the first block's work), same box
