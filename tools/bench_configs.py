@@ -122,6 +122,17 @@ def _close(got, ref, rtol=1e-4, atol=1e-6) -> dict:
             "within_north_star_1e-4": mx <= 1e-4}
 
 
+def hop_roofline(n_rows, nnz, d, ms, K=3, extra_per_row=0, what="") -> dict:
+    """K hops at SURVEY §8(d)'s bytes (bench.hop_bytes_alg: CSR, x read once, y written once)
+    plus extra_per_row bytes per layer (config 3: the transform's n and x rows in, its output
+    row out), against 8 TB/s: the same model as the headline's roofline."""
+    algo = K * (bench.hop_bytes_alg(nnz, n_rows, n_rows, d) + extra_per_row * n_rows)
+    gbps = algo / (ms * 1e-3) / 1e9
+    return {"roofline": {"bound": "hbm", "algorithmic_bytes": algo, "achieved": gbps,
+                         "peak": 8000.0, "unit": "GB/s", "frac": gbps / 8000.0,
+                         "bytes_model": "K x SURVEY 8(d) B_hop" + what}}
+
+
 def gat_cost(n_rows, nnz, ms) -> dict:
     """Config 5's forward against the HBM roofline and the request model.
     Compulsory bytes per forward (GAT d=64, 4 heads, K=3, layer mean fused into the epilogues):
@@ -300,7 +311,7 @@ def main(argv=None):
             t, _ = timed(lambda: m(g), a.steps * 10, a.warmup, 1, device)
             emit({"config": 2, "workload": "ML-1M-shaped LightGCN K=3 d=64 forward",
                   "nnz": g.nnz, "n_nodes": g.shape[0], "ms": t,
-                  "edges_per_s": 3 * g.nnz / (t * 1e-3)})
+                  "edges_per_s": 3 * g.nnz / (t * 1e-3), **hop_roofline(g.shape[0], g.nnz, 64, t)})
         g100 = None
         if 3 in a.configs or 4 in a.configs or 9 in a.configs or (6 in a.configs and world == 1):
             g100 = bench.build_graph(1_000_000, 1_000_000, 100_000_000, 0, threads)
@@ -313,7 +324,9 @@ def main(argv=None):
                    "transform per layer)", "nnz": g100.nnz, "ms": t,
                    "edges_per_s": 3 * g100.nnz / (t * 1e-3),
                    "mfma_flops_per_s": 3 * 2 * 2_000_000 * 128 * 64 / (t * 1e-3),
-                   "exchange": dg.exchange_mode if world > 1 else None}
+                   "exchange": dg.exchange_mode if world > 1 else None,
+                   **hop_roofline(2_000_000, g100.nnz, 64, t, extra_per_row=3 * 256,
+                                  what=" + 768 B per row per layer (transform: n, x in; out)")}
             if a.verify:
                 g1 = g100.to(device)
                 u, i = m(g1)
@@ -334,7 +347,8 @@ def main(argv=None):
                             a.steps, a.warmup, world, device)
             rec = {"config": 4, "workload": "G100M LightGCN K=3 d=128, dst-row shards",
                    "nnz": g100.nnz, "ms": t, "edges_per_s": 3 * g100.nnz / (t * 1e-3),
-                   "exchange": dg.exchange_mode if world > 1 else None}
+                   "exchange": dg.exchange_mode if world > 1 else None,
+                   **hop_roofline(2_000_000, g100.nnz, 128, t)}
             if a.verify:
                 g1 = g100.to(device)
                 u, i = m(g1)

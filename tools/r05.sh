@@ -300,6 +300,11 @@ case ${1:?call} in
     timeout -k 10 900 python -u tools/bench_configs.py --configs 5 --g1b --steps 5 \
         > $OUT/c32_config5_g1b.jsonl 2> $OUT/c32_config5_g1b.err
     ;;
+  c33)
+    # configs 2-4 records with the roofline field (SURVEY 8(d) bytes, as the headline's)
+    timeout -k 10 900 python -u tools/bench_configs.py --configs 2 3 4 --steps 10 \
+        > $OUT/c33_configs_2_3_4.jsonl 2> $OUT/c33_configs_2_3_4.err
+    ;;
   c25)
     # head-major GAT kernels with the chunk's scores pinned before its first block (all 16
     # gathers issued together instead of 8 + 8 behind the first block's work), same box
