@@ -9,6 +9,15 @@
 // Row mapping and load pipelining: see gather.h.
 #include "gather.h"
 
+// 1: the vec kernel loads a step's indices one step ahead (gather_row_pipe); 0: as round 4.
+#ifndef GNNREC_VEC_PIPE
+#define GNNREC_VEC_PIPE 0
+#endif
+// LDS steps (4 neighbours each) the heavy-row consumer keeps in flight ahead of its chain
+#ifndef GNNREC_HEAVY_AHEAD
+#define GNNREC_HEAVY_AHEAD 4
+#endif
+
 namespace gnnrec {
 
 // MASKED: skip the neighbours whose input row is all-zero (xmask). ACTIVE: rows with
@@ -38,7 +47,10 @@ __global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
 #pragma unroll
     for (int q = 0; q < VEC; ++q) a.v[q] = 0.f;
   } else {
-    a = gather_row_v<VEC, GROUP, CH, false, MASKED>(A.col, A.val, beg, end, x, ldx, gl, xmask);
+    if constexpr (!MASKED && GNNREC_VEC_PIPE && GROUP >= CH)
+      a = gather_row_pipe<VEC, GROUP, CH>(A.col, A.val, beg, end, x, ldx, gl);
+    else
+      a = gather_row_v<VEC, GROUP, CH, false, MASKED>(A.col, A.val, beg, end, x, ldx, gl, xmask);
   }
   if (!(epi & GNNREC_EPI_NO_Y)) stv<VEC>(y + r * ldy + VEC * gl, a);
   acc_epilogue_v<VEC>(epi, a, self + r * ld_self + VEC * gl, acc + r * ld_acc + VEC * gl, acc_div);
@@ -205,17 +217,25 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
     const float* vb = vbuf + (c & 1) * kHeavyMaxChunk;
     const int m = (int)min<int64_t>(chk, end - (beg + c * chk));
     const int steps = m >> 2;
-    // two register sets: the reads of step q+1 are in flight while step q's chain runs
-    Step s0, s1;
-    if (steps > 0) fetch(xb, vb, 0, s0);
+    // P register sets: the LDS reads of steps q+1 .. q+P-1 are in flight while step q's chain
+    // runs (one set ahead left each step waiting on an LDS latency; clamped indices read
+    // inside the buffer and are never applied)
+    constexpr int P = GNNREC_HEAVY_AHEAD;
+    Step s[P];
+    const int last = steps > 0 ? steps - 1 : 0;
+#pragma unroll
+    for (int i = 0; i < P; ++i) fetch(xb, vb, 4 * min(i, last), s[i]);
     int q = 0;
-    for (; q + 2 <= steps; q += 2) {
-      fetch(xb, vb, 4 * (q + 1), s1);
-      apply(s0);
-      fetch(xb, vb, 4 * min(q + 2, steps - 1), s0);
-      apply(s1);
+    for (; q + P <= steps; q += P) {
+#pragma unroll
+      for (int i = 0; i < P; ++i) {
+        apply(s[i]);
+        fetch(xb, vb, 4 * min(q + i + P, last), s[i]);
+      }
     }
-    if (q < steps) apply(s0);
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+      if (q + i < steps) apply(s[i]);
     for (int j = steps * 4; j < m; ++j) {
       const float v = vb[j];
 #pragma unroll

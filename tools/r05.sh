@@ -305,6 +305,24 @@ case ${1:?call} in
     timeout -k 10 900 python -u tools/bench_configs.py --configs 2 3 4 --steps 10 \
         > $OUT/c33_configs_2_3_4.jsonl 2> $OUT/c33_configs_2_3_4.err
     ;;
+  c34)
+    # config 2 (ML-1M LightGCN) kernel trace: GPU time per forward against the 0.256 ms wall
+    cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/c34_kt -o run -- \
+        python3 tools/bench_configs.py --configs 2 --steps 10 > $OUT/c34_config2.jsonl 2> $OUT/c34.err
+    ;;
+  c35)
+    # CSR hop: indices one step ahead (vec kernel), 4 LDS steps ahead (heavy-row consumer).
+    # The CSR / heavy-row / long-row GPU tests on the new build, then the same-box A/B
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+        tests/test_kernels_gpu.py tests/test_long_rows_gpu.py tests/test_offsets_gpu.py \
+        tests/test_real_shapes_gpu.py > $OUT/c35_tests.log 2>&1
+    for lib in tools/ab/base.so default tools/ab/nopipe.so tools/ab/ahead8.so default tools/ab/base.so; do
+      if [ $lib = default ]; then unset GNNREC_LIB; else export GNNREC_LIB=$lib; fi
+      timeout -k 10 300 python -u tools/exp_csr_hop.py --tag c35 --g100m \
+          >> $OUT/c35_csr_hop.jsonl 2>> $OUT/c35.err
+    done
+    ;;
   c25)
     # head-major GAT kernels with the chunk's scores pinned before its first block (all 16
     # gathers issued together instead of 8 + 8 behind the first block's work), same box
