@@ -9,10 +9,6 @@
 // Row mapping and load pipelining: see gather.h.
 #include "gather.h"
 
-// 1: the vec kernel loads a step's indices one step ahead (gather_row_pipe); 0: as round 4.
-#ifndef GNNREC_VEC_PIPE
-#define GNNREC_VEC_PIPE 0
-#endif
 // LDS steps (4 neighbours each) the heavy-row consumer keeps in flight ahead of its chain
 #ifndef GNNREC_HEAVY_AHEAD
 #define GNNREC_HEAVY_AHEAD 4
@@ -47,10 +43,7 @@ __global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
 #pragma unroll
     for (int q = 0; q < VEC; ++q) a.v[q] = 0.f;
   } else {
-    if constexpr (!MASKED && GNNREC_VEC_PIPE && GROUP >= CH)
-      a = gather_row_pipe<VEC, GROUP, CH>(A.col, A.val, beg, end, x, ldx, gl);
-    else
-      a = gather_row_v<VEC, GROUP, CH, false, MASKED>(A.col, A.val, beg, end, x, ldx, gl, xmask);
+    a = gather_row_v<VEC, GROUP, CH, false, MASKED>(A.col, A.val, beg, end, x, ldx, gl, xmask);
   }
   if (!(epi & GNNREC_EPI_NO_Y)) stv<VEC>(y + r * ldy + VEC * gl, a);
   acc_epilogue_v<VEC>(epi, a, self + r * ld_self + VEC * gl, acc + r * ld_acc + VEC * gl, acc_div);
@@ -220,7 +213,9 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
     // P register sets: the LDS reads of steps q+1 .. q+P-1 are in flight while step q's chain
     // runs (one set ahead left each step waiting on an LDS latency; clamped indices read
     // inside the buffer and are never applied)
-    constexpr int P = GNNREC_HEAVY_AHEAD;
+    // (F = 1 with a compile-time d only: the wider and runtime-d instances hold more registers
+    // per step and spilled with 4 sets, so they keep 2)
+    constexpr int P = (F == 1 && DC != 0) ? GNNREC_HEAVY_AHEAD : 2;
     Step s[P];
     const int last = steps > 0 ? steps - 1 : 0;
 #pragma unroll

@@ -323,6 +323,17 @@ case ${1:?call} in
           >> $OUT/c35_csr_hop.jsonl 2>> $OUT/c35.err
     done
     ;;
+  c36)
+    # the kept form (4 LDS steps ahead for the F = 1 heavy instances only, no index prefetch):
+    # CSR / heavy / long-row GPU tests, then alternating same-box timings against round 4's
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+        tests/test_kernels_gpu.py tests/test_long_rows_gpu.py tests/test_offsets_gpu.py \
+        tests/test_real_shapes_gpu.py tests/test_models_gpu.py > $OUT/c36_tests.log 2>&1
+    for lib in tools/ab/base.so default tools/ab/base.so default; do
+      if [ $lib = default ]; then unset GNNREC_LIB; else export GNNREC_LIB=$lib; fi
+      timeout -k 10 300 python -u tools/exp_csr_hop.py --tag c36 >> $OUT/c36_csr_hop.jsonl 2>> $OUT/c36.err
+    done
+    ;;
   c25)
     # head-major GAT kernels with the chunk's scores pinned before its first block (all 16
     # gathers issued together instead of 8 + 8 behind the first block's work), same box
