@@ -91,8 +91,9 @@ constexpr int kHeavyMinD = 16;
 constexpr int kHeavyMaxChunk = kHeavyBufFloats / kHeavyMinD;          // vals per buffer
 constexpr int kHeavyPieces = (kHeavyBufFloats / 4 + kHeavyLoaders - 1) / kHeavyLoaders;  // 10
 constexpr int kHeavyVals = (kHeavyMaxChunk + kHeavyLoaders - 1) / kHeavyLoaders;         // 3
+constexpr int kHeavyPad = 64;   // floats past the value buffers: the consumer's read-ahead
 constexpr size_t kHeavyLds = 2 * kHeavyBufFloats * sizeof(float) +
-                             2 * kHeavyMaxChunk * sizeof(float);
+                             2 * kHeavyMaxChunk * sizeof(float) + kHeavyPad * sizeof(float);
 
 // Neighbours per chunk (a multiple of 4) for a row width d: chk + 2 <= 16384 / d.
 __host__ __device__ constexpr int heavy_chunk(int d) { return ((kHeavyBufFloats / d - 2) / 4) * 4; }
@@ -211,21 +212,25 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
     const int m = (int)min<int64_t>(chk, end - (beg + c * chk));
     const int steps = m >> 2;
     // P register sets: the LDS reads of steps q+1 .. q+P-1 are in flight while step q's chain
-    // runs (one set ahead left each step waiting on an LDS latency; clamped indices read
-    // inside the buffer and are never applied)
+    // runs (one set ahead left each step waiting on an LDS latency)
     // (F = 1 with a compile-time d only: the wider and runtime-d instances hold more registers
     // per step and spilled with 4 sets, so they keep 2)
     constexpr int P = (F == 1 && DC != 0) ? GNNREC_HEAVY_AHEAD : 2;
     Step s[P];
-    const int last = steps > 0 ? steps - 1 : 0;
+    // the read-ahead is not clamped to the chunk: reads past it stay inside the allocation
+    // (the next buffer, the value buffers, kHeavyPad) and are never applied, so a step costs
+    // no index arithmetic (the clamped form was 6 % slower on config 2)
 #pragma unroll
-    for (int i = 0; i < P; ++i) fetch(xb, vb, 4 * min(i, last), s[i]);
+    for (int i = 0; i < P; ++i) fetch(xb, vb, 4 * i, s[i]);
     int q = 0;
     for (; q + P <= steps; q += P) {
 #pragma unroll
       for (int i = 0; i < P; ++i) {
         apply(s[i]);
-        fetch(xb, vb, 4 * min(q + i + P, last), s[i]);
+        fetch(xb, vb, 4 * (q + i + P), s[i]);
+        // keep each fetch P steps ahead of its use (unpinned, the compiler regrouped the
+        // fetches of P steps and then waited on them)
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
 #pragma unroll

@@ -334,6 +334,18 @@ case ${1:?call} in
       timeout -k 10 300 python -u tools/exp_csr_hop.py --tag c36 >> $OUT/c36_csr_hop.jsonl 2>> $OUT/c36.err
     done
     ;;
+  c37)
+    # heavy-row consumer variants (B: unclamped read-ahead + a scheduling barrier per step so
+    # each LDS fetch stays 4 steps ahead; C: 72 KB buffers, 284 neighbours per round at
+    # d = 64; D: both): the CSR / heavy / long-row tests on D, then alternating timings
+    GNNREC_LIB=tools/ab/D.so timeout -k 10 600 python -u -m pytest -x -v --timeout 300 \
+        --timeout-method thread -m gpu tests/test_kernels_gpu.py tests/test_long_rows_gpu.py \
+        tests/test_offsets_gpu.py tests/test_real_shapes_gpu.py > $OUT/c37_tests.log 2>&1
+    for lib in default tools/ab/B.so tools/ab/C.so tools/ab/D.so default tools/ab/B.so tools/ab/C.so tools/ab/D.so; do
+      if [ $lib = default ]; then unset GNNREC_LIB; else export GNNREC_LIB=$lib; fi
+      timeout -k 10 300 python -u tools/exp_csr_hop.py --tag c37 >> $OUT/c37_csr_hop.jsonl 2>> $OUT/c37.err
+    done
+    ;;
   c25)
     # head-major GAT kernels with the chunk's scores pinned before its first block (all 16
     # gathers issued together instead of 8 + 8 behind the first block's work), same box
