@@ -1,7 +1,8 @@
 """The CSR hop kernels (spmm_vec_kernel + spmm_heavy_kernel) for one libgnnrec build
 (GNNREC_LIB): config 2 (ML-1M-shaped LightGCN K=3 d=64, the model's forward and the
 propagation at several heavy-row thresholds) and, with --g100m, the G100M K=3 propagation on
-the CSR path (tiled hop off). ms per call and an output hash (bit-identity across builds).
+the CSR path (tiled hop off), with --powerlaw the power-law 2M x 2M propagation (rows up to
+400K neighbours: the heavy-row kernel). ms per call and an output hash (bit-identity across builds).
 
     GNNREC_LIB=tools/ab/base.so python tools/exp_csr_hop.py --tag base [--g100m]
 """
@@ -24,6 +25,8 @@ from src.ops import functional as F  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--tag", required=True)
 ap.add_argument("--g100m", action="store_true")
+ap.add_argument("--powerlaw", action="store_true",
+                help="also the power-law 2M x 2M graph (50M pairs, Zipf 0.9) at d = 64 and 128")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 lib = os.environ.get("GNNREC_LIB", "default")
@@ -69,3 +72,12 @@ with torch.no_grad():
         F.TILED_HOP = False
         t, (out, _) = ms_of(lambda: F.lightgcn_forward(g100, x, 3), 2)
         emit(case="g100m_csr_propagate", ms=t, sha=sha(out))
+    if a.powerlaw:
+        sys.path.insert(0, str(ROOT / "tools"))
+        from bench_configs import powerlaw_graph
+        gp = powerlaw_graph(2_000_000, 2_000_000, 50_000_000, 0.9, 0).to(dev)
+        for d in (64, 128):
+            x = torch.randn(4_000_000, d, device=dev, generator=torch.Generator(device=dev).manual_seed(d))
+            t, (out, _) = ms_of(lambda: F.lightgcn_forward(gp, x, 3), 2)
+            emit(case=f"powerlaw2m_propagate_d{d}", ms=t, sha=sha(out))
+            del x, out

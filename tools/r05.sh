@@ -346,6 +346,14 @@ case ${1:?call} in
       timeout -k 10 300 python -u tools/exp_csr_hop.py --tag c37 >> $OUT/c37_csr_hop.jsonl 2>> $OUT/c37.err
     done
     ;;
+  c38)
+    # the heavy-row change on the power-law 2M x 2M LightGCN (d = 64 and 128) and config 2,
+    # against round 4's spmm.hip (tools/ab/r4.so), alternating
+    for lib in tools/ab/r4.so default tools/ab/r4.so default; do
+      if [ $lib = default ]; then unset GNNREC_LIB; else export GNNREC_LIB=$lib; fi
+      timeout -k 10 300 python -u tools/exp_csr_hop.py --tag c38 --powerlaw >> $OUT/c38_csr_hop.jsonl 2>> $OUT/c38.err
+    done
+    ;;
   c25)
     # head-major GAT kernels with the chunk's scores pinned before its first block (all 16
     # gathers issued together instead of 8 + 8 behind the first block's work), same box
