@@ -211,31 +211,43 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
     const float* vb = vbuf + (c & 1) * kHeavyMaxChunk;
     const int m = (int)min<int64_t>(chk, end - (beg + c * chk));
     const int steps = m >> 2;
-    // P register sets: the LDS reads of steps q+1 .. q+P-1 are in flight while step q's chain
-    // runs (one set ahead left each step waiting on an LDS latency)
-    // (F = 1 with a compile-time d only: the wider and runtime-d instances hold more registers
-    // per step and spilled with 4 sets, so they keep 2)
-    constexpr int P = (F == 1 && DC != 0) ? GNNREC_HEAVY_AHEAD : 2;
-    Step s[P];
-    // the read-ahead is not clamped to the chunk: reads past it stay inside the allocation
-    // (the next buffer, the value buffers, kHeavyPad) and are never applied, so a step costs
-    // no index arithmetic (the clamped form was 6 % slower on config 2)
+    if constexpr (F == 1 && DC != 0) {
+      // d = 32 / 64: P register sets, the LDS reads of steps q+1 .. q+P-1 in flight while step
+      // q's chain runs. The read-ahead is not clamped to the chunk: reads past it stay inside
+      // the allocation (the next buffer, the value buffers, kHeavyPad) and are never applied,
+      // so a step costs no index arithmetic; a scheduling barrier per step keeps each fetch P
+      // steps ahead of its use (unpinned, the compiler regrouped the fetches of P steps and
+      // then waited on them). The wider and runtime-d instances spilled with it, and the
+      // d = 128 one ran slower in this form: they keep two sets below.
+      constexpr int P = GNNREC_HEAVY_AHEAD;
+      Step s[P];
 #pragma unroll
-    for (int i = 0; i < P; ++i) fetch(xb, vb, 4 * i, s[i]);
-    int q = 0;
-    for (; q + P <= steps; q += P) {
+      for (int i = 0; i < P; ++i) fetch(xb, vb, 4 * i, s[i]);
+      int q = 0;
+      for (; q + P <= steps; q += P) {
 #pragma unroll
-      for (int i = 0; i < P; ++i) {
-        apply(s[i]);
-        fetch(xb, vb, 4 * (q + i + P), s[i]);
-        // keep each fetch P steps ahead of its use (unpinned, the compiler regrouped the
-        // fetches of P steps and then waited on them)
-        __builtin_amdgcn_sched_barrier(0);
+        for (int i = 0; i < P; ++i) {
+          apply(s[i]);
+          fetch(xb, vb, 4 * (q + i + P), s[i]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
-    }
 #pragma unroll
-    for (int i = 0; i < P; ++i)
-      if (q + i < steps) apply(s[i]);
+      for (int i = 0; i < P; ++i)
+        if (q + i < steps) apply(s[i]);
+    } else {
+      // two register sets: the reads of step q+1 are in flight while step q's chain runs
+      Step s0, s1;
+      if (steps > 0) fetch(xb, vb, 0, s0);
+      int q = 0;
+      for (; q + 2 <= steps; q += 2) {
+        fetch(xb, vb, 4 * (q + 1), s1);
+        apply(s0);
+        fetch(xb, vb, 4 * min(q + 2, steps - 1), s0);
+        apply(s1);
+      }
+      if (q < steps) apply(s0);
+    }
     for (int j = steps * 4; j < m; ++j) {
       const float v = vb[j];
 #pragma unroll

@@ -354,6 +354,17 @@ case ${1:?call} in
       timeout -k 10 300 python -u tools/exp_csr_hop.py --tag c38 --powerlaw >> $OUT/c38_csr_hop.jsonl 2>> $OUT/c38.err
     done
     ;;
+  c39)
+    # the new consumer for the d = 32 / 64 instances only (d = 128 and runtime d back to round
+    # 4's form): CSR / heavy / long-row tests, then alternating timings against round 4
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
+        tests/test_kernels_gpu.py tests/test_long_rows_gpu.py tests/test_offsets_gpu.py \
+        tests/test_real_shapes_gpu.py tests/test_models_gpu.py > $OUT/c39_tests.log 2>&1
+    for lib in tools/ab/r4.so default tools/ab/r4.so default; do
+      if [ $lib = default ]; then unset GNNREC_LIB; else export GNNREC_LIB=$lib; fi
+      timeout -k 10 300 python -u tools/exp_csr_hop.py --tag c39 --powerlaw >> $OUT/c39_csr_hop.jsonl 2>> $OUT/c39.err
+    done
+    ;;
   c25)
     # head-major GAT kernels with the chunk's scores pinned before its first block (all 16
     # gathers issued together instead of 8 + 8 behind the first block's work), same box
