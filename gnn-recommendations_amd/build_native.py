@@ -84,7 +84,11 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs),
              "-lpthread"])
         os.replace(tmp, LIB)
-    build_vendor(force=force, verbose=verbose)
+    try:
+        build_vendor(force=force, verbose=verbose)
+    except Exception as e:  # the comparator is bench-only; the product library is built
+        print(f"build_native: rocSPARSE comparator not built ({e}); bench.py records it as "
+              "unavailable", file=sys.stderr)
     return LIB
 
 

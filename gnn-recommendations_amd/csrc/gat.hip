@@ -742,12 +742,15 @@ int gat_check_common(int64_t n_rows, int32_t heads, int32_t o_dim, const float* 
 
 // ATT form: scores from the rows (o_dim <= 64: a head's dot spans at most a 16-lane DPP row)
 int gat_check_att(const float* att, const float* hself, int64_t ld_hself, int64_t ldh,
-                  int32_t o_dim) {
+                  int32_t o_dim, int32_t heads, int64_t head_stride) {
   GNNREC_REQUIRE(att && aligned16(att), "gat_att: att must be a 16-B aligned [2][heads][o_dim] array");
   GNNREC_REQUIRE(hself && aligned16(hself) && !(ld_hself & 3),
                  "gat_att: hself must be 16-B aligned with ld %% 4 == 0");
   GNNREC_REQUIRE(o_dim <= 64 && ((o_dim / 4) & (o_dim / 4 - 1)) == 0,
                  "gat_att: o_dim must be 4, 8, 16, 32 or 64 (got %d)", (int)o_dim);
+  // the kernels read hself[r * ld_hself + h * head_stride + o] for h < heads, o < o_dim
+  GNNREC_REQUIRE(ld_hself >= (int64_t)(heads - 1) * head_stride + o_dim,
+                 "gat_att: ld_hself %lld < (heads - 1) * head_stride + o_dim", (long long)ld_hself);
   (void)ldh;
   return GNNREC_OK;
 }
@@ -896,7 +899,7 @@ extern "C" int gnnrec_gat_aggregate_att_f32(const int64_t* row_ptr, const int32_
     return st;
   if (n_rows == 0) return GNNREC_OK;
   GNNREC_REQUIRE(row_ptr && col, "gat_att: null operand");
-  if (int st = gat_check_att(att, hself, ld_hself, ldh, o_dim)) return st;
+  if (int st = gat_check_att(att, hself, ld_hself, ldh, o_dim, heads, head_stride)) return st;
   GatParams p{Csr{row_ptr, col, nullptr, n_rows}, hfeat, ldh, head_stride, nullptr, nullptr, 0, 0, heads, o_dim, slope,
               mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, max_row_len,
               att, hself, ld_hself};
@@ -949,7 +952,7 @@ extern "C" int gnnrec_gat_heavy_att_f32(const int32_t* col, const int64_t* seg_r
                      hfeat && aligned16(work) && aligned16(hfeat) && !(ldh & 3) &&
                      ldh < ((int64_t)1 << 30) && head_stride >= 0 && !(head_stride & 3),
                  "gat_heavy_att: null or misaligned operand (or ld >= 2^30)");
-  if (int st = gat_check_att(att, hself, ld_hself, ldh, o_dim)) return st;
+  if (int st = gat_check_att(att, hself, ld_hself, ldh, o_dim, heads, head_stride)) return st;
   GatParams p{Csr{nullptr, col, nullptr, 0}, hfeat, ldh, head_stride, nullptr, nullptr, 0, 0, heads, o_dim, slope,
               mean_heads, apply_elu, out, ldo, epi, self, ld_self, acc, ld_acc, acc_div, 0,
               att, hself, ld_hself};

@@ -192,6 +192,67 @@ __device__ __forceinline__ VecF<VEC> gather_row_v(const int32_t* __restrict__ co
   return a;
 }
 
+// Latency form of the same chain, for operands too small to fill the chip with rows (ML-1M:
+// 9.4K row-parallel rows, one wave each): the next step's (col, val) are loaded before this
+// step's row gathers, so a step waits for one memory latency (the gathers) instead of two
+// (indices, then rows), and a step carries CH (>= the throughput form's) gathers. Same fmaf
+// order, same bits. PER == 1 only (GROUP >= CH: lanes gl < CH hold the step's indices).
+template <int VEC, int GROUP, bool TAIL, int CH>
+__device__ __forceinline__ void gather_apply_v(int cm, float vm, int64_t k0, int64_t end,
+                                               const float* __restrict__ x, int64_t ldx, int gl,
+                                               VecF<VEC>& a) {
+  VecF<VEC> xv[CH];
+#pragma unroll
+  for (int t = 0; t < CH; ++t) {
+    const int c = __shfl(cm, t, GROUP);
+    xv[t] = ldv<VEC>(x + (int64_t)c * ldx + VEC * gl);
+  }
+#pragma unroll
+  for (int t = 0; t < CH; ++t) {
+    const float v = __shfl(vm, t, GROUP);
+    const bool ok = !TAIL || (k0 + t) < end;
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) {
+      const float n = __builtin_fmaf(v, xv[t].v[q], a.v[q]);
+      a.v[q] = ok ? n : a.v[q];
+    }
+  }
+}
+
+template <int VEC, int GROUP, int CH>
+__device__ __forceinline__ VecF<VEC> gather_row_pipe(const int32_t* __restrict__ col,
+                                                     const float* __restrict__ val, int64_t beg,
+                                                     int64_t end, const float* __restrict__ x,
+                                                     int64_t ldx, int gl) {
+  static_assert(GROUP >= CH, "one index per lane per step");
+  VecF<VEC> a;
+#pragma unroll
+  for (int q = 0; q < VEC; ++q) a.v[q] = 0.f;
+  if (beg >= end) return a;
+  // step k0's index of lane gl (lanes past CH repeat k0's), clamped into the row: always a
+  // valid entry, so the loads need no branch (a branch made the compiler wait on them)
+  auto load_cv = [&](int64_t k0, int& c, float& v) {
+    int64_t k = gl < CH ? k0 + gl : k0;
+    k = k < end ? k : end - 1;
+    c = col[k];
+    v = val[k];
+  };
+  int cm;
+  float vm;
+  load_cv(beg, cm, vm);
+  int64_t k0 = beg;
+  for (; k0 + CH <= end; k0 += CH) {
+    int cn;
+    float vn;
+    load_cv(k0 + CH, cn, vn);
+    gather_apply_v<VEC, GROUP, false, CH>(cm, vm, k0, end, x, ldx, gl, a);
+    cm = cn;
+    vm = vn;
+  }
+  if (k0 < end) gather_apply_v<VEC, GROUP, true, CH>(cm, vm, k0, end, x, ldx, gl, a);
+  return a;
+}
+
 template <int VEC>
 __device__ __forceinline__ void acc_epilogue_v(int epi, const VecF<VEC>& y, const float* self_row,
                                                float* acc_row, float acc_div) {
@@ -211,6 +272,16 @@ template <int D> struct SpmmCfg { static constexpr int VEC = 4, CH = 16; };
 template <> struct SpmmCfg<32> { static constexpr int VEC = 2, CH = 16; };
 template <> struct SpmmCfg<64> { static constexpr int VEC = 1, CH = 8; };   // wave per row
 template <> struct SpmmCfg<128> { static constexpr int VEC = 2, CH = 16; };  // wave per row
+
+// Latency form (gather_row_pipe) per d: the same lane mapping, CH gathers per step.
+#ifndef GNNREC_LAT_CH
+#define GNNREC_LAT_CH 8
+#endif
+template <int D> struct SpmmLatCfg {
+  static constexpr bool OK = (D == 32 || D == 64 || D == 128);
+  static constexpr int GROUP = D / SpmmCfg<D>::VEC;
+  static constexpr int CH = GNNREC_LAT_CH < GROUP ? GNNREC_LAT_CH : GROUP;
+};
 
 // ---- GAS (block-diagonal orthogonal transform + column shuffle) -----------------------
 // y[r, j] = sum_{c<bs} z[r, bs*b + c] * W_b[c, e],  perm[j] = bs*b + e  (sequential fmaf in c).

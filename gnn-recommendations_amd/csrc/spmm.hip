@@ -7,6 +7,8 @@
 // starting from +0.0f. That order is reproduced exactly here, so results are bit-identical.
 //
 // Row mapping and load pipelining: see gather.h.
+#include <mutex>
+
 #include "gather.h"
 
 // LDS steps (4 neighbours each) the heavy-row consumer keeps in flight ahead of its chain
@@ -19,7 +21,8 @@ namespace gnnrec {
 // MASKED: skip the neighbours whose input row is all-zero (xmask). ACTIVE: rows with
 // y_active[r] == 0 are not computed (written as +0 with the epilogue applied) — for rows
 // whose value nobody reads, or that no non-zero input row reaches.
-template <int D, bool MASKED = false, bool ACTIVE = false>
+// LAT: the latency form of the chain (gather_row_pipe; small operands, see gather.h).
+template <int D, bool MASKED = false, bool ACTIVE = false, bool LAT = false>
 __global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
     Csr A, const float* __restrict__ x, int64_t ldx, float* __restrict__ y, int64_t ldy,
     int epi, const float* __restrict__ self, int64_t ld_self, float* __restrict__ acc,
@@ -42,6 +45,8 @@ __global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
     // only +-0 terms to +0
 #pragma unroll
     for (int q = 0; q < VEC; ++q) a.v[q] = 0.f;
+  } else if constexpr (LAT && !MASKED) {
+    a = gather_row_pipe<VEC, GROUP, SpmmLatCfg<D>::CH>(A.col, A.val, beg, end, x, ldx, gl);
   } else {
     a = gather_row_v<VEC, GROUP, CH, false, MASKED>(A.col, A.val, beg, end, x, ldx, gl, xmask);
   }
@@ -107,12 +112,37 @@ struct HeavyStage {       // one chunk's gathered rows + vals in flight in regis
   float v[kHeavyVals];
 };
 
-// F: features per consumer lane (d <= 64 F); DC: d as a compile-time constant (0 = runtime d).
+// Which chunk slot (j = neighbour, part = float4 of its row) loader piece p fills. The plain
+// order (j = p / q4) gives a 32-lane store group two neighbours x all 16 parts at d = 64, and
+// the feature-major park then lands those 32 dwords on 8 banks (4-way: every ds_write_b32 at
+// twice its cycles, 40 of them per loader thread per round). Swizzled, a 64-piece block holds
+// rpb = 64 / q4 neighbours with j fastest, so a group spans 8 parts x 4 neighbours = 16 banks
+// at d = 64 (2-way: free for ds_write_b32) and 32 banks at d = 32. A wave's load instruction
+// still covers the same rpb whole rows. Needs q4 | 64 (d = 16, 32, 64, 128, 256).
+#ifndef GNNREC_HEAVY_SWIZZLE
+#define GNNREC_HEAVY_SWIZZLE 1
+#endif
+template <int DC>
+__device__ __forceinline__ void heavy_piece(int p, int q4, int& j, int& part) {
+  const bool swz = GNNREC_HEAVY_SWIZZLE && (DC ? (64 % (DC / 4) == 0) : (64 % q4 == 0));
+  if (swz) {
+    const int rpb = 64 / q4;
+    j = (p >> 6) * rpb + (p & 63) % rpb;
+    part = (p & 63) / rpb;
+  } else {
+    j = p / q4;
+    part = p - j * q4;
+  }
+}
+
+// One heavy row r (or a feature slice of it: x / y / self / acc already offset to the slice,
+// d = its width) on the whole workgroup. F: features per consumer lane (d <= 64 F); DC: d as a
+// compile-time constant (0 = runtime d).
 template <int F, int DC>
-__global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
-    Csr A, const int64_t* __restrict__ rows, const float* __restrict__ x, int64_t ldx,
-    float* __restrict__ y, int64_t ldy, int d_rt, int epi, const float* __restrict__ self,
-    int64_t ld_self, float* __restrict__ acc, int64_t ld_acc, float acc_div) {
+__device__ __forceinline__ void heavy_row(
+    const Csr& A, int64_t r, const float* __restrict__ x, int64_t ldx, float* __restrict__ y,
+    int64_t ldy, int d_rt, int epi, const float* __restrict__ self, int64_t ld_self,
+    float* __restrict__ acc, int64_t ld_acc, float acc_div) {
   const int d = DC ? DC : d_rt;
   extern __shared__ float4 heavy_lds4[];
   float* buf = reinterpret_cast<float*>(heavy_lds4);     // [2][kHeavyBufFloats]: [d][S] each
@@ -120,21 +150,20 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
   const int tid = threadIdx.x, lane = tid & 63;
   const bool consumer = tid < 64;
   const int lt = tid - 64;                               // loader thread index
-  const int64_t r = rows[blockIdx.x];
   const int64_t beg = A.row_ptr[r], end = A.row_ptr[r + 1];
   const int q4 = d >> 2;                                 // float4 per neighbour row
   const int chk = heavy_chunk(d);                        // neighbours per chunk
   const int S = chk + 2;                                 // LDS row stride of a feature
-  const int npieces = chk * q4;
   const int64_t n_chunks = (end - beg + chk - 1) / chk;
 
   auto load_cols = [&](int64_t c, HeavyCols& hc) {
     const int64_t k0 = beg + c * chk;
 #pragma unroll
     for (int i = 0; i < kHeavyPieces; ++i) {
-      const int p = lt + i * kHeavyLoaders;
-      const int64_t k = k0 + p / q4;
-      hc.c[i] = (c < n_chunks && p < npieces && k < end) ? A.col[k] : -1;
+      int j, part;
+      heavy_piece<DC>(lt + i * kHeavyLoaders, q4, j, part);
+      const int64_t k = k0 + j;
+      hc.c[i] = (c < n_chunks && j < chk && k < end) ? A.col[k] : -1;
     }
 #pragma unroll
     for (int i = 0; i < kHeavyVals; ++i) {
@@ -146,7 +175,8 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
   auto gather = [&](const HeavyCols& hc, HeavyStage& st) {
 #pragma unroll
     for (int i = 0; i < kHeavyPieces; ++i) {
-      const int p = lt + i * kHeavyLoaders, part = p - (p / q4) * q4;
+      int j, part;
+      heavy_piece<DC>(lt + i * kHeavyLoaders, q4, j, part);
       st.x[i] = hc.c[i] >= 0
                     ? *reinterpret_cast<const float4*>(x + (int64_t)hc.c[i] * ldx + 4 * part)
                     : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -158,9 +188,10 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
     float* dst = buf + b * kHeavyBufFloats;
 #pragma unroll
     for (int i = 0; i < kHeavyPieces; ++i) {
-      const int p = lt + i * kHeavyLoaders;
-      if (p < npieces) {
-        const int j = p / q4, f0 = 4 * (p - j * q4);
+      int j, part;
+      heavy_piece<DC>(lt + i * kHeavyLoaders, q4, j, part);
+      if (j < chk) {
+        const int f0 = 4 * part;
         dst[(f0 + 0) * S + j] = st.x[i].x;
         dst[(f0 + 1) * S + j] = st.x[i].y;
         dst[(f0 + 2) * S + j] = st.x[i].z;
@@ -299,6 +330,33 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
   }
 }
 
+// The heavy-row launch: block b < n_sliced * SLICES runs feature slice b % SLICES (d / SLICES
+// features, instance <SF, SDC>) of row rows[b / SLICES]; the other blocks run whole rows
+// rows[n_sliced ..] (instance <F, DC>). rows is longest first, so the sliced rows are the
+// longest: each slice gathers 1/SLICES of every neighbour row, so its loaders fill a chunk of
+// SLICES x the neighbours per round and the row's chain finishes in fewer rounds. Every slice
+// still applies its features' fmafs in the row's order: the same bits.
+template <int F, int DC, int SLICES, int SF, int SDC>
+__global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
+    Csr A, const int64_t* __restrict__ rows, int64_t n_sliced, const float* __restrict__ x,
+    int64_t ldx, float* __restrict__ y, int64_t ldy, int d_rt, int epi,
+    const float* __restrict__ self, int64_t ld_self, float* __restrict__ acc, int64_t ld_acc,
+    float acc_div) {
+  int64_t b = blockIdx.x;
+  if constexpr (SLICES > 1) {
+    static_assert(DC > 0 && SDC * SLICES == DC, "sliced instance: SDC = DC / SLICES");
+    if (b < n_sliced * SLICES) {
+      const int64_t r = rows[b / SLICES];
+      const int f0 = (int)(b % SLICES) * SDC;
+      heavy_row<SF, SDC>(A, r, x + f0, ldx, y + f0, ldy, SDC, epi, self + f0, ld_self,
+                         acc + f0, ld_acc, acc_div);
+      return;
+    }
+    b -= n_sliced * (SLICES - 1);
+  }
+  heavy_row<F, DC>(A, rows[b], x, ldx, y, ldy, d_rt, epi, self, ld_self, acc, ld_acc, acc_div);
+}
+
 // mask[r] = 1 if row r of x has any element != 0 (NaN counts as non-zero), for the masked hop.
 __global__ __launch_bounds__(kBlock) void row_nonzero_kernel(const float* __restrict__ x,
                                                              int64_t ldx, int64_t n_rows, int d,
@@ -373,16 +431,19 @@ template <int D>
 void launch_spmm_vec4(const Csr& A, const float* x, int64_t ldx, float* y, int64_t ldy, int epi,
                       const float* self, int64_t ld_self, float* acc, int64_t ld_acc,
                       float acc_div, int64_t skip, const uint8_t* xmask, const uint8_t* y_active,
-                      hipStream_t s) {
+                      bool lat, hipStream_t s) {
   constexpr int RPB = (64 / (D / SpmmCfg<D>::VEC)) * (kBlock / 64);
   const int64_t grid = ceil_div(A.n_rows, RPB);
-#define GNNREC_VEC(M, AC)                                                                          \
-  hipLaunchKernelGGL((spmm_vec_kernel<D, M, AC>), dim3((unsigned)grid), dim3(kBlock), 0, s, A, x, \
-                     ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xmask, y_active)
-  if (xmask && y_active) GNNREC_VEC(true, true);
-  else if (xmask) GNNREC_VEC(true, false);
-  else if (y_active) GNNREC_VEC(false, true);
-  else GNNREC_VEC(false, false);
+#define GNNREC_VEC(M, AC, LT)                                                                      \
+  hipLaunchKernelGGL((spmm_vec_kernel<D, M, AC, LT>), dim3((unsigned)grid), dim3(kBlock), 0, s, A, \
+                     x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xmask,       \
+                     y_active)
+  if (xmask && y_active) GNNREC_VEC(true, true, false);
+  else if (xmask) GNNREC_VEC(true, false, false);
+  else if (y_active && lat) GNNREC_VEC(false, true, SpmmLatCfg<D>::OK);
+  else if (y_active) GNNREC_VEC(false, true, false);
+  else if (lat) GNNREC_VEC(false, false, SpmmLatCfg<D>::OK);
+  else GNNREC_VEC(false, false, false);
 #undef GNNREC_VEC
 }
 
@@ -397,17 +458,86 @@ bool vec4_ok(int d, const float* x, int64_t ldx, const float* y, int64_t ldy, in
   return true;
 }
 
+// Rows at most this many: the row-parallel kernel runs the latency form of the chain (gather.h
+// gather_row_pipe) unless a GNNREC_CSR_LIGHT_* flag says otherwise.
+constexpr int64_t kLatencyMaxRows = 65536;
+
+// The side stream a GNNREC_CSR_FORK launch runs its heavy rows on (one per device, created on
+// first use, the device's highest priority so its workgroups are dispatched before the
+// row-parallel kernel's), with the fork / join events. The mutex also keeps one caller's
+// record-wait-launch-record-wait sequence whole.
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+std::mutex g_side_mu;
+SideStream g_side[64];
+
+int side_stream(SideStream** out) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    set_error("spmm: no current device for the heavy-row side stream");
+    return GNNREC_EHIP;
+  }
+  SideStream& ss = g_side[dev];
+  if (!ss.s) {
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+        hipStreamCreateWithPriority(&ss.s, hipStreamNonBlocking, greatest) != hipSuccess ||
+        hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) != hipSuccess) {
+      set_error("spmm: creating the heavy-row side stream failed");
+      return GNNREC_EHIP;
+    }
+  }
+  *out = &ss;
+  return GNNREC_OK;
+}
+
+// Feature slices of a sliced heavy row at d = 64 / 128 / 256 (d = 32 always takes 2).
+#ifndef GNNREC_HEAVY_SLICES
+#define GNNREC_HEAVY_SLICES 4
+#endif
+constexpr int kHeavySlices = GNNREC_HEAVY_SLICES;
+
+int launch_heavy(const Csr& A, const int64_t* heavy_rows, int64_t n_heavy, int64_t n_sliced,
+                 const float* x, int64_t ldx, float* y, int64_t ldy, int d, int epi,
+                 const float* self, int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
+                 hipStream_t s) {
+  const int slices = d == 32 ? 2 : kHeavySlices;
+  const int64_t blocks = n_heavy + n_sliced * (slices - 1);   // a block per slice
+  GNNREC_REQUIRE(blocks < (int64_t)INT32_MAX, "spmm: too many heavy rows");
+  const dim3 grid((unsigned)blocks), block(kHeavyThreads);
+#define GNNREC_HEAVY(F, DC, SL, SF, SDC)                                                          \
+  hipLaunchKernelGGL((spmm_heavy_kernel<F, DC, SL, SF, SDC>), grid, block, kHeavyLds, s, A,      \
+                     heavy_rows, n_sliced, x, ldx, y, ldy, d, epi, self, ld_self, acc, ld_acc,    \
+                     acc_div)
+  switch (d) {
+    case 32: GNNREC_HEAVY(1, 32, 2, 1, 16); break;
+    case 64: GNNREC_HEAVY(1, 64, kHeavySlices, 1, 64 / kHeavySlices); break;
+    case 128: GNNREC_HEAVY(2, 128, kHeavySlices, 1, 128 / kHeavySlices); break;
+    case 256: GNNREC_HEAVY(4, 256, kHeavySlices, 256 / kHeavySlices / 64, 256 / kHeavySlices); break;
+    default:
+      if (d <= 64) GNNREC_HEAVY(1, 0, 1, 1, 0);
+      else if (d <= 128) GNNREC_HEAVY(2, 0, 1, 1, 0);
+      else GNNREC_HEAVY(4, 0, 1, 1, 0);
+  }
+#undef GNNREC_HEAVY
+  return check_launch("spmm_heavy");
+}
+
 }  // namespace
 
-extern "C" int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col,
-                                          const float* val, int64_t n_rows, const float* x,
-                                          int64_t ldx, const uint8_t* x_nonzero,
-                                          const uint8_t* y_active, float* y,
-                                          int64_t ldy, int32_t d, int32_t epi, const float* self,
-                                          int64_t ld_self, float* acc, int64_t ld_acc,
-                                          float acc_div, const int64_t* heavy_rows,
-                                          int64_t n_heavy, int64_t heavy_threshold,
-                                          gnnrec_stream_t stream) {
+extern "C" int gnnrec_spmm_csr_heavy_f32(const int64_t* row_ptr, const int32_t* col,
+                                         const float* val, int64_t n_rows, const float* x,
+                                         int64_t ldx, const uint8_t* x_nonzero,
+                                         const uint8_t* y_active, float* y, int64_t ldy,
+                                         int32_t d, int32_t epi, const float* self,
+                                         int64_t ld_self, float* acc, int64_t ld_acc,
+                                         float acc_div, const int64_t* heavy_rows,
+                                         int64_t n_heavy, int64_t heavy_threshold,
+                                         int64_t n_sliced, int32_t flags,
+                                         gnnrec_stream_t stream) {
   GNNREC_REQUIRE(n_rows >= 0 && d >= 1, "spmm: bad sizes n_rows=%lld d=%d", (long long)n_rows, d);
   if (n_rows == 0) return GNNREC_OK;
   GNNREC_REQUIRE(row_ptr && x, "spmm: null row_ptr/x");
@@ -424,6 +554,12 @@ extern "C" int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t*
     return GNNREC_EUNSUPPORTED;
   }
   GNNREC_REQUIRE(heavy_threshold >= 0 && n_heavy >= 0, "spmm: negative heavy_threshold/n_heavy");
+  GNNREC_REQUIRE(n_sliced >= 0 && n_sliced <= n_heavy, "spmm: n_sliced must be in [0, n_heavy]");
+  GNNREC_REQUIRE((flags & ~(GNNREC_CSR_FORK | GNNREC_CSR_LIGHT_LATENCY |
+                            GNNREC_CSR_LIGHT_THROUGHPUT)) == 0 &&
+                     (flags & (GNNREC_CSR_LIGHT_LATENCY | GNNREC_CSR_LIGHT_THROUGHPUT)) !=
+                         (GNNREC_CSR_LIGHT_LATENCY | GNNREC_CSR_LIGHT_THROUGHPUT),
+                 "spmm: bad flags 0x%x", flags);
   const bool split = heavy_threshold > 0;
   if (split) {
     GNNREC_REQUIRE(n_heavy == 0 || heavy_rows, "spmm: null heavy_rows");
@@ -431,45 +567,68 @@ extern "C" int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t*
                    "spmm: the heavy-row path needs d %% 4 == 0, 16 <= d <= 256 and a 16-B "
                    "aligned x with ldx %% 4 == 0");
   }
+  // feature slices only where the instance has them (d = 32, 64, 128, 256)
+  if (!(d == 32 || d == 64 || d == 128 || d == 256)) n_sliced = 0;
+  const bool heavy = split && n_heavy > 0;
   const Csr A{row_ptr, col, val, n_rows};
   hipStream_t s = as_hip(stream);
   const int64_t skip = split ? heavy_threshold : 0;
-  const uint8_t* xm = x_nonzero;
-  if (vec4_ok(d, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc)) {
-    switch (d) {
-      case 8: launch_spmm_vec4<8>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, s); break;
-      case 16: launch_spmm_vec4<16>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, s); break;
-      case 32: launch_spmm_vec4<32>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, s); break;
-      case 64: launch_spmm_vec4<64>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, s); break;
-      case 128: launch_spmm_vec4<128>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, s); break;
-      default: launch_spmm_vec4<256>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, s); break;
+  const bool lat = (flags & GNNREC_CSR_LIGHT_LATENCY) ||
+                   (!(flags & GNNREC_CSR_LIGHT_THROUGHPUT) && !x_nonzero &&
+                    n_rows <= kLatencyMaxRows);
+  auto light = [&]() -> int {
+    const uint8_t* xm = x_nonzero;
+    if (vec4_ok(d, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc)) {
+      switch (d) {
+        case 8: launch_spmm_vec4<8>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, lat, s); break;
+        case 16: launch_spmm_vec4<16>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, lat, s); break;
+        case 32: launch_spmm_vec4<32>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, lat, s); break;
+        case 64: launch_spmm_vec4<64>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, lat, s); break;
+        case 128: launch_spmm_vec4<128>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, lat, s); break;
+        default: launch_spmm_vec4<256>(A, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xm, y_active, lat, s); break;
+      }
+    } else {
+      const int64_t grid = ceil_div(n_rows, kBlock / 64);
+      hipLaunchKernelGGL(spmm_generic_kernel, dim3((unsigned)grid), dim3(kBlock), 0, s, A, x, ldx,
+                         y, ldy, d, epi, self, ld_self, acc, ld_acc, acc_div, skip);
     }
-  } else {
-    const int64_t grid = ceil_div(n_rows, kBlock / 64);
-    hipLaunchKernelGGL(spmm_generic_kernel, dim3((unsigned)grid), dim3(kBlock), 0, s, A, x, ldx,
-                       y, ldy, d, epi, self, ld_self, acc, ld_acc, acc_div, skip);
+    return check_launch("spmm");
+  };
+  if (!heavy) return light();
+  if (!(flags & GNNREC_CSR_FORK)) {
+    if (int rc = light()) return rc;
+    return launch_heavy(A, heavy_rows, n_heavy, n_sliced, x, ldx, y, ldy, d, epi, self, ld_self,
+                        acc, ld_acc, acc_div, s);
   }
-  if (int rc = check_launch("spmm")) return rc;
-  if (split && n_heavy > 0) {
-    GNNREC_REQUIRE(n_heavy < (int64_t)INT32_MAX, "spmm: too many heavy rows");
-    const dim3 grid((unsigned)n_heavy), block(kHeavyThreads);
-#define GNNREC_HEAVY(F, DC)                                                                      \
-  hipLaunchKernelGGL((spmm_heavy_kernel<F, DC>), grid, block, kHeavyLds, s, A, heavy_rows, x, ldx, \
-                     y, ldy, d, epi, self, ld_self, acc, ld_acc, acc_div)
-    switch (d) {
-      case 32: GNNREC_HEAVY(1, 32); break;
-      case 64: GNNREC_HEAVY(1, 64); break;
-      case 128: GNNREC_HEAVY(2, 128); break;
-      case 256: GNNREC_HEAVY(4, 256); break;
-      default:
-        if (d <= 64) GNNREC_HEAVY(1, 0);
-        else if (d <= 128) GNNREC_HEAVY(2, 0);
-        else GNNREC_HEAVY(4, 0);
-    }
-#undef GNNREC_HEAVY
-    return check_launch("spmm_heavy");
-  }
-  return GNNREC_OK;
+  // Fork / join: the heavy rows (disjoint from the row-parallel kernel's rows) go first, on the
+  // high-priority side stream, so their workgroups — the longest chains — start first and the
+  // row-parallel rows fill the CUs as the shorter heavy rows retire.
+  std::lock_guard<std::mutex> lock(g_side_mu);
+  SideStream* ss = nullptr;
+  if (int rc = side_stream(&ss)) return rc;
+  if (hipEventRecord(ss->fork, s) != hipSuccess || hipStreamWaitEvent(ss->s, ss->fork, 0) != hipSuccess)
+    return check_launch("spmm: fork");
+  int rc = launch_heavy(A, heavy_rows, n_heavy, n_sliced, x, ldx, y, ldy, d, epi, self, ld_self,
+                        acc, ld_acc, acc_div, ss->s);
+  const int rc_light = rc == GNNREC_OK ? light() : rc;
+  // join even after a failed launch, so the caller's stream never runs ahead of the side's
+  if (hipEventRecord(ss->join, ss->s) != hipSuccess || hipStreamWaitEvent(s, ss->join, 0) != hipSuccess)
+    return check_launch("spmm: join");
+  return rc != GNNREC_OK ? rc : rc_light;
+}
+
+extern "C" int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col,
+                                          const float* val, int64_t n_rows, const float* x,
+                                          int64_t ldx, const uint8_t* x_nonzero,
+                                          const uint8_t* y_active, float* y,
+                                          int64_t ldy, int32_t d, int32_t epi, const float* self,
+                                          int64_t ld_self, float* acc, int64_t ld_acc,
+                                          float acc_div, const int64_t* heavy_rows,
+                                          int64_t n_heavy, int64_t heavy_threshold,
+                                          gnnrec_stream_t stream) {
+  return gnnrec_spmm_csr_heavy_f32(row_ptr, col, val, n_rows, x, ldx, x_nonzero, y_active, y, ldy,
+                                   d, epi, self, ld_self, acc, ld_acc, acc_div, heavy_rows,
+                                   n_heavy, heavy_threshold, 0, 0, stream);
 }
 
 extern "C" int gnnrec_row_nonzero_f32(const float* x, int64_t ldx, int64_t n_rows, int32_t d,
@@ -520,12 +679,13 @@ extern "C" int gnnrec_spmm_csr_f32(const int64_t* row_ptr, const int32_t* col, c
                                    ld_self, acc, ld_acc, acc_div, nullptr, 0, 0, stream);
 }
 
-extern "C" int gnnrec_lightgcn_split_f32(const int64_t* row_ptr, const int32_t* col,
+extern "C" int gnnrec_lightgcn_heavy_f32(const int64_t* row_ptr, const int32_t* col,
                                          const float* val, int64_t n_rows, const float* x0,
                                          int32_t d, int32_t n_layers, float* work0, float* work1,
                                          float* layers, float* out, int64_t ld_out,
                                          const int64_t* heavy_rows, int64_t n_heavy,
-                                         int64_t heavy_threshold, gnnrec_stream_t stream) {
+                                         int64_t heavy_threshold, int64_t n_sliced,
+                                         int32_t flags, gnnrec_stream_t stream) {
   GNNREC_REQUIRE(n_layers >= 0 && d >= 1 && n_rows >= 0, "lightgcn: bad sizes");
   GNNREC_REQUIRE(x0 && out && ld_out >= d, "lightgcn: null x0/out");
   GNNREC_REQUIRE(layers || n_layers <= 1 || (work0 && work1), "lightgcn: need work0/work1 or layers");
@@ -545,13 +705,25 @@ extern "C" int gnnrec_lightgcn_split_f32(const int64_t* row_ptr, const int32_t* 
       epi |= GNNREC_EPI_ACC_DIV;
       if (!layers) epi |= GNNREC_EPI_NO_Y;
     }
-    const int rc = gnnrec_spmm_csr_split_f32(row_ptr, col, val, n_rows, in, d, yk, d, d, epi, x0,
-                                             d, out, ld_out, (float)(n_layers + 1), heavy_rows,
-                                             n_heavy, heavy_threshold, stream);
+    const int rc = gnnrec_spmm_csr_heavy_f32(row_ptr, col, val, n_rows, in, d, nullptr, nullptr, yk,
+                                             d, d, epi, x0, d, out, ld_out, (float)(n_layers + 1),
+                                             heavy_rows, n_heavy, heavy_threshold, n_sliced, flags,
+                                             stream);
     if (rc != GNNREC_OK) return rc;
     in = yk;
   }
   return GNNREC_OK;
+}
+
+extern "C" int gnnrec_lightgcn_split_f32(const int64_t* row_ptr, const int32_t* col,
+                                         const float* val, int64_t n_rows, const float* x0,
+                                         int32_t d, int32_t n_layers, float* work0, float* work1,
+                                         float* layers, float* out, int64_t ld_out,
+                                         const int64_t* heavy_rows, int64_t n_heavy,
+                                         int64_t heavy_threshold, gnnrec_stream_t stream) {
+  return gnnrec_lightgcn_heavy_f32(row_ptr, col, val, n_rows, x0, d, n_layers, work0, work1,
+                                   layers, out, ld_out, heavy_rows, n_heavy, heavy_threshold, 0, 0,
+                                   stream);
 }
 
 extern "C" int gnnrec_lightgcn_f32(const int64_t* row_ptr, const int32_t* col, const float* val,

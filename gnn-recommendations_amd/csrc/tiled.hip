@@ -553,8 +553,8 @@ __global__ __launch_bounds__(kTiledWaves * 64) void tiled_hop_kernel(
     f4 sink = {0.f, 0.f, 0.f, 0.f};   // diagnostic builds only (GNNREC_TILED_EXP & 1)
     if (kQuad && b < e && (b & 3)) {
       // a chunk-major plan passed to a quad build: the quads would straddle waves' ranges.
-      // Flag it (the caller checks GNNREC_TILED_SYNC_ERR_WORD after the launch) and leave the
-      // rows untouched instead of computing garbage.
+      // Flag it (the caller checks GNNREC_TILED_SYNC_ERR_WORD after the launch) and skip the
+      // chunks; the block's epilogue still stores, so the launch's rows are undefined.
       if (lane == 0)
         __hip_atomic_fetch_or(sync + GNNREC_TILED_SYNC_ERR_WORD, 1u, __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT);

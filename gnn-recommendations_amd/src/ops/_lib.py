@@ -17,7 +17,7 @@ import torch  # noqa: F401  (load order: torch's HIP runtime first)
 
 _PKG_ROOT = Path(__file__).resolve().parents[2]
 LIB_PATH = Path(os.environ.get("GNNREC_LIB", _PKG_ROOT / "lib" / "libgnnrec.so"))
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 # gnnrec.h epilogue flags
 EPI_ACC_INIT = 1
@@ -25,6 +25,10 @@ EPI_ACC_ADD = 2
 EPI_ACC_DIV = 4
 EPI_NO_Y = 8
 EPI_ACC_X = 16
+# gnnrec.h CSR hop flags (gnnrec_spmm_csr_heavy_f32)
+CSR_FORK = 1
+CSR_LIGHT_LATENCY = 2
+CSR_LIGHT_THROUGHPUT = 4
 # column-ordered hop plan layout (include/gnnrec.h GNNREC_TILED_*)
 TILED_WAVES = 8
 TILED_GROUPS = 8
@@ -58,6 +62,10 @@ _SIGNATURES = {
                                   _p, _i64, _f32, _p, _i64, _i64, _p],
     "gnnrec_spmm_csr_masked_f32": [_p, _p, _p, _i64, _p, _i64, _p, _p, _p, _i64, _i32, _i32,
                                    _p, _i64, _p, _i64, _f32, _p, _i64, _i64, _p],
+    "gnnrec_spmm_csr_heavy_f32": [_p, _p, _p, _i64, _p, _i64, _p, _p, _p, _i64, _i32, _i32,
+                                  _p, _i64, _p, _i64, _f32, _p, _i64, _i64, _i64, _i32, _p],
+    "gnnrec_lightgcn_heavy_f32": [_p, _p, _p, _i64, _p, _i32, _i32, _p, _p, _p, _p, _i64, _p,
+                                  _i64, _i64, _i64, _i32, _p],
     "gnnrec_mark_active_rows": [_p, _p, _i64, _p, _i64, _p, _p],
     "gnnrec_tiled_plan_build": [_p, _p, _p, _i64, _i32, _i32, _i32, _i32, _p, _p, _p],
     "gnnrec_tiled_plan_emit": [_p, _p, _p, _p, _p, _p],

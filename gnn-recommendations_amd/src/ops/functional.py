@@ -45,7 +45,18 @@ def _csr_args(adj: CsrGraph):
 # 0 disables the split. Sweep (tools/exp_heavy.py, profiles/r01/heavy_split_sweep.jsonl):
 # ML-1M-shaped LightGCN K=3 0.90 ms unsplit -> 0.30 ms at 128, power-law 2M x 2M 123 -> 29 ms;
 # uniform graphs (G100M, max degree ~150) have no rows above it.
-SPMM_HEAVY_THRESHOLD = 256
+# Round 6 (config 2, profiles/r06/config2_knobs_sweep_*.jsonl, every output bit-identical):
+# 256 -> 128 moves the rows of 129-256 neighbours off the row-parallel kernel, whose time is its
+# longest rows' chain (27.6 -> 21.4 us per hop, profiles/r06/config2_trace/).
+SPMM_HEAVY_THRESHOLD = 128
+# Heavy rows longer than this run as feature slices (gnnrec_spmm_csr_heavy_f32 n_sliced: four
+# d/4-wide workgroups at d = 64 / 128 / 256, two at d = 32; 0 = none): the longest rows' chains
+# then finish in fewer LDS rounds (config 2: 0.215 -> 0.188 ms per forward at threshold 128).
+# CSR_FLAGS: _lib.CSR_FORK (the heavy rows on a side stream beside the row-parallel kernel:
+# measured slower, the cross-stream join costs ~17 us per hop) and the row-parallel chain's
+# form (CSR_LIGHT_*; 0 = by operand size).
+SPMM_SLICE_LEN = 1024
+CSR_FLAGS = 0
 
 
 # Column-ordered hop (gnnrec_spmm_tiled_f32): the same bits, used for any d
@@ -176,16 +187,24 @@ def hop_table(n_rows: int, d: int, *, device=None, zero: bool = False,
 HOP_TABLE_MAX_EXTRA_FRACTION = 0.25
 
 
+_PLACED_FIT: dict = {}
+
+
 def _placed_tables_fit(n_rows: int, d: int, ld: int, device) -> bool:
+    """Decided once per (device, n_rows, d, ld) and cached, so a layer's tables keep one
+    layout from call to call and the hot path makes no device-memory query."""
     if os.environ.get("GNNREC_HOP_TABLE_LAYOUT", "1") == "0":
         return False
     dev = torch.device(device) if device is not None else None
     if dev is None or dev.type != "cuda" or n_rows == 0:
         return True
-    extra = n_rows * (ld - d) * 4
-    free, _ = torch.cuda.mem_get_info(dev)
-    cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
-    return extra <= HOP_TABLE_MAX_EXTRA_FRACTION * (free + max(0, cached))
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), n_rows, d, ld)
+    if key not in _PLACED_FIT:
+        extra = n_rows * (ld - d) * 4
+        free, _ = torch.cuda.mem_get_info(dev)
+        cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
+        _PLACED_FIT[key] = extra <= HOP_TABLE_MAX_EXTRA_FRACTION * (free + max(0, cached))
+    return _PLACED_FIT[key]
 
 
 def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None,
@@ -205,16 +224,21 @@ def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None,
     return adj.tiled_plan(rows_per_block=R)
 
 
-def _heavy_args(adj: CsrGraph, x: torch.Tensor, heavy_threshold: int):
-    """(heavy_rows ptr, n_heavy, threshold) for the split launch, or the no-split triple."""
+def _heavy_args(adj: CsrGraph, x: torch.Tensor, heavy_threshold: int,
+                slice_len: Optional[int] = None):
+    """(heavy_rows ptr, n_heavy, threshold, n_sliced) for the split launch, or the no-split
+    tuple. n_sliced: how many of the (longest-first) heavy rows are longer than slice_len
+    (None: SPMM_SLICE_LEN; 0: none)."""
     d = x.shape[1]
     if (heavy_threshold <= 0 or d % 4 or d < 16 or d > 256 or x.stride(0) % 4
             or x.data_ptr() % 16):
-        return None, 0, 0
+        return None, 0, 0, 0
     rows = adj.heavy_rows(heavy_threshold)
     if rows is None:
-        return None, 0, 0
-    return ptr(rows), rows.numel(), int(heavy_threshold)
+        return None, 0, 0, 0
+    sl = SPMM_SLICE_LEN if slice_len is None else slice_len
+    n_sliced = adj.heavy_rows_longer(heavy_threshold, sl) if sl > 0 else 0
+    return ptr(rows), rows.numel(), int(heavy_threshold), n_sliced
 
 
 # ---- raw launches (no autograd) ---------------------------------------------------------
@@ -224,7 +248,7 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
               x_mask: Optional[torch.Tensor] = None,
               y_active: Optional[torch.Tensor] = None, meet_us: Optional[int] = None,
               reserve_cus: int = 0, prev: Optional[torch.Tensor] = None) -> None:
-    """y = A x with an optional fused layer-mean epilogue (gnnrec_spmm_csr_masked_f32: rows
+    """y = A x with an optional fused layer-mean epilogue (gnnrec_spmm_csr_heavy_f32: rows
     longer than `heavy_threshold` run on the workgroup-per-row kernel; rows of x whose
     `x_mask` byte is 0 are all-zero and are not gathered — same bits; destination rows whose
     `y_active` byte is 0 are not computed — y is +0 there, or the true value). `meet_us`: the
@@ -252,13 +276,13 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
         spmm_tiled_into(adj, x, y, plan, epi=epi, self_rows=self_rows, acc=acc, acc_div=acc_div,
                         meet_us=meet_us, prev=prev)
         return
-    check(L.gnnrec_spmm_csr_masked_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(x_mask),
-                                       ptr(y_active), ptr(y), y.stride(0) if y is not None else d, d, epi,
-                                       ptr(self_rows),
-                                       self_rows.stride(0) if self_rows is not None else d,
-                                       ptr(acc), acc.stride(0) if acc is not None else d,
-                                       float(acc_div), *_heavy_args(adj, x, ht),
-                                       _lib.stream_of(adj.device)), "gnnrec_spmm_csr_masked_f32")
+    check(L.gnnrec_spmm_csr_heavy_f32(*_csr_args(adj), ptr(x), x.stride(0), ptr(x_mask),
+                                      ptr(y_active), ptr(y), y.stride(0) if y is not None else d, d,
+                                      epi, ptr(self_rows),
+                                      self_rows.stride(0) if self_rows is not None else d,
+                                      ptr(acc), acc.stride(0) if acc is not None else d,
+                                      float(acc_div), *_heavy_args(adj, x, ht), int(CSR_FLAGS),
+                                      _lib.stream_of(adj.device)), "gnnrec_spmm_csr_heavy_f32")
 
 
 def spmm_tiled_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], plan: dict, *,
@@ -513,10 +537,11 @@ def lightgcn_forward(adj: CsrGraph, x0: torch.Tensor, n_layers: int,
         work0 = work1 = torch.empty_like(x0)
     L = _lib.lib()
     ht = SPMM_HEAVY_THRESHOLD if heavy_threshold is None else heavy_threshold
-    check(L.gnnrec_lightgcn_split_f32(*_csr_args(adj), ptr(x0), d, int(n_layers), ptr(work0),
+    check(L.gnnrec_lightgcn_heavy_f32(*_csr_args(adj), ptr(x0), d, int(n_layers), ptr(work0),
                                       ptr(work1), ptr(layers), ptr(out), d,
-                                      *_heavy_args(adj, x0, ht), _lib.stream_of(adj.device)),
-          "gnnrec_lightgcn_split_f32")
+                                      *_heavy_args(adj, x0, ht), int(CSR_FLAGS),
+                                      _lib.stream_of(adj.device)),
+          "gnnrec_lightgcn_heavy_f32")
     return out, layers
 
 
@@ -748,7 +773,8 @@ def gat_aggregate_att(adj: CsrGraph, h: torch.Tensor, hself: torch.Tensor, att: 
     if att.numel() != 2 * heads * o_dim:
         raise ValueError("att must hold [2, heads, o_dim] floats")
     _require_device(adj, h, hself, self_rows, acc)
-    if h.shape[1] < (o_dim if shared_rows else heads * o_dim) or hself.shape[0] < adj.n_rows:
+    row_w = o_dim if shared_rows else heads * o_dim
+    if (h.shape[1] < row_w or hself.shape[1] < row_w or hself.shape[0] < adj.n_rows):
         raise ValueError("h / hself too small for the aggregated rows")
     head_stride = 0 if shared_rows else o_dim
     width = o_dim if mean_heads else heads * o_dim

@@ -420,6 +420,19 @@ class CsrGraph:
             self._plans[key] = rows.contiguous() if rows.numel() else None
         return self._plans[key]
 
+    def heavy_rows_longer(self, threshold: int, length: int) -> int:
+        """How many of heavy_rows(threshold) have more than `length` neighbours (a prefix of
+        that longest-first list; cached): the rows the SpMM runs as feature slices."""
+        key = ("heavy_rows_longer", threshold, length)
+        if key not in self._plans:
+            rows = self.heavy_rows(threshold)
+            if rows is None:
+                self._plans[key] = 0
+            else:
+                deg = self.row_ptr[rows + 1] - self.row_ptr[rows]
+                self._plans[key] = int((deg > length).sum())
+        return self._plans[key]
+
     def max_degree(self) -> int:
         """Longest row (cached; one device read the first time)."""
         if "max_degree" not in self._plans:
@@ -470,6 +483,8 @@ class CsrGraph:
                                          device=self.device))
             t1 = now()
             build_s = {"planner": planner, "plan_s": t1 - t0}
+            if "planner_phases" in plan:
+                build_s["planner_phases"] = plan.pop("planner_phases")
             if (TILED_FACTOR and cuda
                     and int(rows_per_block) <= _lib.TILED_MAX_ROWS_FACTORED):
                 self.degree_factors()
@@ -658,6 +673,10 @@ class CsrGraph:
             raise _DEVICE_PLAN_ERRORS.get(code, RuntimeError)(
                 f"gnnrec_tiled_plan_device ({what}) failed: error {code}")
 
+        import time
+        t_alloc = time.perf_counter()
+        torch.cuda.synchronize(dev)
+        t_count = time.perf_counter()
         _lib.check(L.gnnrec_tiled_plan_device(*args, ptr(chunks), ptr(n_steps), None, None, None,
                                               None, ptr(err), stream),
                    "gnnrec_tiled_plan_device (count)")
@@ -666,19 +685,27 @@ class CsrGraph:
         n_chunks, code = int(wave_ptr[-1]), int(err)
         if code:
             failed("count", code)
+        t_emit_alloc = time.perf_counter()
         total = n_chunks + _lib.TILED_TAIL
         slot = torch.empty(total * _lib.TILED_CHUNK, dtype=torch.int32, device=dev)
         v = torch.empty(total * _lib.TILED_CHUNK, dtype=torch.float32, device=dev)
         hdr = torch.empty(total * _lib.TILED_HDR_WORDS, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize(dev)
+        t_emit = time.perf_counter()
         _lib.check(L.gnnrec_tiled_plan_device(*args, None, None, ptr(wave_ptr), ptr(slot), ptr(v),
                                               ptr(hdr), ptr(err), stream),
                    "gnnrec_tiled_plan_device (emit)")
         code = int(err)
         if code:
             failed("emit", code)
+        t_end = time.perf_counter()
         del scratch
+        # sub-phases of the planner (bench.py's operand_prep_s): scratch allocation, the count
+        # pass (+ cumsum, chunk total read back), the plan arrays' allocation, the emit pass
+        phases = dict(scratch_alloc_s=t_count - t_alloc, count_s=t_emit_alloc - t_count,
+                      arrays_alloc_s=t_emit - t_emit_alloc, emit_s=t_end - t_emit)
         return dict(slot=slot, val=v, hdr=hdr, wave_ptr=wave_ptr, n_steps=n_steps,
-                    n_blocks=nb, n_chunks=n_chunks)
+                    n_blocks=nb, n_chunks=n_chunks, planner_phases=phases)
 
     def heavy_plan(self, threshold: int, seg_len: int):
         """Degree buckets for the skew-tolerant kernels (cached): rows with more than

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define GNNREC_ABI_VERSION 10
+#define GNNREC_ABI_VERSION 11
 
 typedef struct ihipStream_t* gnnrec_stream_t;
 
@@ -133,6 +133,36 @@ int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col, const
                                int64_t ld_acc, float acc_div, const int64_t* heavy_rows,
                                int64_t n_heavy, int64_t heavy_threshold, gnnrec_stream_t stream);
 
+/* The CSR hop with its heavy rows tuned (ABI 11): gnnrec_spmm_csr_masked_f32 /
+ * gnnrec_lightgcn_split_f32 plus
+ *  - n_sliced: the first n_sliced entries of heavy_rows (which must then be sorted longest
+ *    first, as every caller in this package lists them) run as two workgroups of d/2 features
+ *    each (d = 32, 64, 128, 256; ignored for other d): each gathers half of every neighbour
+ *    row, so the longest chains finish in fewer LDS rounds. Same bits.
+ *  - flags: GNNREC_CSR_FORK runs the heavy-row kernel on an internal high-priority side
+ *    stream forked from and joined back into `stream` with events (capture-safe), so the
+ *    row-parallel rows run beside the heavy chains instead of after them (the two write
+ *    disjoint rows). GNNREC_CSR_LIGHT_LATENCY / _THROUGHPUT force the row-parallel chain's
+ *    form (default: the latency form — the next step's indices loaded one step ahead — for
+ *    operands of at most 65536 rows, whose rows cannot fill the chip; see csrc/gather.h).
+ * Replaces the same torch.sparse.mm calls (lightgcn.py:88, ngcf.py:70). */
+#define GNNREC_CSR_FORK 1
+#define GNNREC_CSR_LIGHT_LATENCY 2
+#define GNNREC_CSR_LIGHT_THROUGHPUT 4
+int gnnrec_spmm_csr_heavy_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
+                              int64_t n_rows, const float* x, int64_t ldx,
+                              const uint8_t* x_nonzero, const uint8_t* y_active, float* y,
+                              int64_t ldy, int32_t d, int32_t epi, const float* self,
+                              int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
+                              const int64_t* heavy_rows, int64_t n_heavy, int64_t heavy_threshold,
+                              int64_t n_sliced, int32_t flags, gnnrec_stream_t stream);
+int gnnrec_lightgcn_heavy_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
+                              int64_t n_rows, const float* x0, int32_t d, int32_t n_layers,
+                              float* work0, float* work1, float* layers, float* out,
+                              int64_t ld_out, const int64_t* heavy_rows, int64_t n_heavy,
+                              int64_t heavy_threshold, int64_t n_sliced, int32_t flags,
+                              gnnrec_stream_t stream);
+
 /* Column-ordered ("tiled") hop, the same y and epilogue bits as gnnrec_spmm_csr_f32 for any
  * d that is a multiple of 32. A persistent workgroup per CU owns
  * `rows_per_block` destination rows per pass with their accumulators in LDS and walks their
@@ -175,7 +205,8 @@ int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col, const
 #define GNNREC_TILED_SYNC_WORDS 256
 /* sync[GNNREC_TILED_SYNC_ERR_WORD] != 0 after a gnnrec_spmm_tiled_f32 launch: the plan's wave
  * ranges were not quad-aligned (chunk-major arrays passed to a quad-layout build, see
- * gnnrec_tiled_plan_quad); the affected rows were not written. The launch zeroes the word. */
+ * gnnrec_tiled_plan_quad); the launch's output rows (y, acc) are then UNDEFINED: a flagged wave
+ * skips its chunks, but every block still runs its epilogue. The launch zeroes the word. */
 #define GNNREC_TILED_SYNC_ERR_WORD 1
 #define GNNREC_TILED_HDR_WORDS 4
 #define GNNREC_TILED_MAX_LDX 1024

@@ -140,3 +140,35 @@ def test_config5_g250m_sampled_rows_vs_oracle(cuda):
     bad = [k for k, v in res.items() if isinstance(v, dict) and not v["within_tolerance"]]
     assert res["all_within_tolerance"], bad
     assert res["max_row_degree"] == int(deg.max())
+
+
+@pytest.mark.timeout(400)
+def test_config5_g1b_sampled_rows_vs_oracle(cuda):
+    """Config 5 at the size its timing is quoted: the 10M x 10M power-law
+    graph with 1B Zipf-0.9 pairs + min-degree fill (1,670,276,726 nnz, max degree 4,297,502),
+    operand built on the device exactly as tools/bench_configs.py --g1b does; the timed
+    single-device forward (gat_forward_dist on a world-1 DistributedGraph, heavy-row segments
+    + merge on every layer) at the 16 heaviest rows plus 1024 random rows per degree decile:
+    every head of the first and last layer's aggregation vs oracle.gat_head, every layer's
+    output vs the reference layer on the native input, and the forward's layer mean vs the
+    oracle layers' mean — |diff| <= 1e-5 + 1e-4 |ref| (oracle/gat_sample.py, gat.py:258-297).
+    About 20 s to build and 80 s to check."""
+    from oracle.gat_sample import check_forward, sample_rows
+    from src.ops.distributed import DistributedGraph, gat_forward_dist
+    shape = (10_000_000, 10_000_000)
+    g = bench_configs.powerlaw_graph(*shape, 1_000_000_000, 0.9, 0, 16, device=cuda)
+    assert g.nnz == 1_670_276_726
+    deg = (g.row_ptr[1:] - g.row_ptr[:-1]).cpu().numpy()
+    assert deg.min() >= 1 and int(deg.max()) == 4_297_502
+    m = bench_configs.config5_model(shape, cuda)
+    dg = DistributedGraph(g, 0, 1, cuda)
+    with torch.no_grad():
+        mine = gat_forward_dist(dg, m, dg.pad_table(m._initial_table()))
+    torch.cuda.synchronize()
+    rows = sample_rows(deg, n_heavy=16, per_decile=1024, seed=1)
+    res = check_forward(m, g, mine, rows)
+    print("\n[config5 G1B sampled]", {k: (v["max_abs_diff"] if isinstance(v, dict) else v)
+                                     for k, v in res.items()})
+    bad = [k for k, v in res.items() if isinstance(v, dict) and not v["within_tolerance"]]
+    assert res["all_within_tolerance"], bad
+    assert res["max_row_degree"] == 4_297_502

@@ -124,3 +124,57 @@ def test_tiled_deferred_layer_mean_bit_exact(case, rows_per_block):
         F.spmm_tiled_into(g, bufs[xn], bufs[yn], plan, epi=epi, self_rows=x0, acc=out,
                           acc_div=4.0)
     check_layers(f, [], out)
+
+
+@pytest.mark.parametrize("light", ["throughput", "latency"])
+@pytest.mark.parametrize("fork", [False, True])
+@pytest.mark.parametrize("heavy,slice_len", [(256, 0), (256, 2048), (128, 512), (16, 16)])
+def test_csr_knobs_bit_exact(case, light, fork, heavy, slice_len):
+    """The round-6 CSR hop knobs (gnnrec_spmm_csr_heavy_f32): the row-parallel chain's
+    latency form, the heavy rows forked onto the side stream beside it, and the longest heavy
+    rows as two half-width feature slices — every combination the reference's bits, per hop
+    (spmm_into) and through the fused K-hop launch."""
+    from src.ops import _lib
+    f, g, x0, _, _ = case
+    flags = (_lib.CSR_LIGHT_LATENCY if light == "latency" else _lib.CSR_LIGHT_THROUGHPUT) | \
+        (_lib.CSR_FORK if fork else 0)
+    saved = F.CSR_FLAGS, F.SPMM_SLICE_LEN
+    F.CSR_FLAGS, F.SPMM_SLICE_LEN = flags, slice_len
+    try:
+        if slice_len:
+            assert g.heavy_rows_longer(heavy, slice_len) > 0
+        hops, x = [], x0
+        for _ in range(3):
+            y = torch.empty_like(x0)
+            F.spmm_into(g, x, y, heavy_threshold=heavy)
+            hops.append(y)
+            x = y
+        check_layers(f, hops)
+        out, layers = F.lightgcn_forward(g, x0, 3, return_layers=True, heavy_threshold=heavy)
+        check_layers(f, list(layers), out)
+        out2, _ = F.lightgcn_forward(g, x0, 3, heavy_threshold=heavy)
+        assert torch.equal(out, out2)
+    finally:
+        F.CSR_FLAGS, F.SPMM_SLICE_LEN = saved
+
+
+@pytest.mark.parametrize("d", [32, 128, 256])
+def test_sliced_heavy_rows_other_widths(case, d):
+    """Feature slices at the other sliced instances (d/2 = 16, 64, 128 features per slice),
+    with the fork: the same bits as the unsplit row-parallel kernel (heavy=0), which the d=64
+    case pins to the reference."""
+    from src.ops import _lib
+    _, g, _, _, _ = case
+    x = torch.randn(g.shape[1], d, device=g.device,
+                    generator=torch.Generator(device=g.device).manual_seed(d))
+    ref = torch.empty(g.n_rows, d, device=g.device)
+    F.spmm_into(g, x, ref, heavy_threshold=0)
+    saved = F.CSR_FLAGS, F.SPMM_SLICE_LEN
+    try:
+        for flags, sl in ((0, 1024), (_lib.CSR_FORK, 256), (_lib.CSR_FORK, 0)):
+            F.CSR_FLAGS, F.SPMM_SLICE_LEN = flags, sl
+            y = torch.full_like(ref, float("nan"))
+            F.spmm_into(g, x, y, heavy_threshold=256)
+            assert torch.equal(y, ref), (flags, sl)
+    finally:
+        F.CSR_FLAGS, F.SPMM_SLICE_LEN = saved

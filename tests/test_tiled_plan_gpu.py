@@ -176,8 +176,8 @@ def test_quad_plan_layout_is_padding_plus_permutation(cuda):
 
 def test_chunk_major_plan_on_quad_build_is_flagged(cuda):
     """a raw-ABI caller passing the planner's chunk-major arrays to a quad-layout
-    build gets the error word set (sync[GNNREC_TILED_SYNC_ERR_WORD]) and untouched rows, not
-    silently wrong ones; the Python wrapper refuses such a plan before launching."""
+    build gets the error word set (sync[GNNREC_TILED_SYNC_ERR_WORD]; the launch's rows are then
+    undefined, gnnrec.h), and the Python wrapper refuses such a plan before launching."""
     from src.ops import _lib
     L = _lib.lib()
     if not L.gnnrec_tiled_plan_quad():
