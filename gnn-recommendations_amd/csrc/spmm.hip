@@ -494,17 +494,23 @@ int side_stream(SideStream** out) {
   return GNNREC_OK;
 }
 
-// Feature slices of a sliced heavy row at d = 64 / 128 / 256 (d = 32 always takes 2).
-#ifndef GNNREC_HEAVY_SLICES
-#define GNNREC_HEAVY_SLICES 4
-#endif
-constexpr int kHeavySlices = GNNREC_HEAVY_SLICES;
+// Feature slices of a sliced heavy row: narrow (16 features) at d = 32 and on small operands
+// at d = 64, where the rows' chains are latency-bound and a 64-B slice of a neighbour row
+// costs nothing extra (config 2: 4 slices 0.188 ms vs 2 slices 0.192 ms); otherwise whole
+// 128-B lines (32 features: d = 64 -> 2 slices, 128 -> 4) or 64 features at d = 256, since a
+// half-line slice doubles a bandwidth-bound row's line requests (power-law 2M x 2M, d = 64:
+// 4 slices 21.9 ms vs 19.0 ms unsliced, profiles/r06/).
+int heavy_slices(int d, bool small) {
+  if (d == 32) return 2;
+  if (d == 64) return small ? 4 : 2;
+  return 4;   // d = 128 (32-wide), 256 (64-wide)
+}
 
 int launch_heavy(const Csr& A, const int64_t* heavy_rows, int64_t n_heavy, int64_t n_sliced,
                  const float* x, int64_t ldx, float* y, int64_t ldy, int d, int epi,
                  const float* self, int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
-                 hipStream_t s) {
-  const int slices = d == 32 ? 2 : kHeavySlices;
+                 bool small, hipStream_t s) {
+  const int slices = heavy_slices(d, small);
   const int64_t blocks = n_heavy + n_sliced * (slices - 1);   // a block per slice
   GNNREC_REQUIRE(blocks < (int64_t)INT32_MAX, "spmm: too many heavy rows");
   const dim3 grid((unsigned)blocks), block(kHeavyThreads);
@@ -514,9 +520,12 @@ int launch_heavy(const Csr& A, const int64_t* heavy_rows, int64_t n_heavy, int64
                      acc_div)
   switch (d) {
     case 32: GNNREC_HEAVY(1, 32, 2, 1, 16); break;
-    case 64: GNNREC_HEAVY(1, 64, kHeavySlices, 1, 64 / kHeavySlices); break;
-    case 128: GNNREC_HEAVY(2, 128, kHeavySlices, 1, 128 / kHeavySlices); break;
-    case 256: GNNREC_HEAVY(4, 256, kHeavySlices, 256 / kHeavySlices / 64, 256 / kHeavySlices); break;
+    case 64:
+      if (slices == 4) GNNREC_HEAVY(1, 64, 4, 1, 16);
+      else GNNREC_HEAVY(1, 64, 2, 1, 32);
+      break;
+    case 128: GNNREC_HEAVY(2, 128, 4, 1, 32); break;
+    case 256: GNNREC_HEAVY(4, 256, 4, 1, 64); break;
     default:
       if (d <= 64) GNNREC_HEAVY(1, 0, 1, 1, 0);
       else if (d <= 128) GNNREC_HEAVY(2, 0, 1, 1, 0);
@@ -573,9 +582,10 @@ extern "C" int gnnrec_spmm_csr_heavy_f32(const int64_t* row_ptr, const int32_t* 
   const Csr A{row_ptr, col, val, n_rows};
   hipStream_t s = as_hip(stream);
   const int64_t skip = split ? heavy_threshold : 0;
+  // a small operand (its rows cannot fill the chip): latency-bound chains
+  const bool small = n_rows <= kLatencyMaxRows;
   const bool lat = (flags & GNNREC_CSR_LIGHT_LATENCY) ||
-                   (!(flags & GNNREC_CSR_LIGHT_THROUGHPUT) && !x_nonzero &&
-                    n_rows <= kLatencyMaxRows);
+                   (!(flags & GNNREC_CSR_LIGHT_THROUGHPUT) && !x_nonzero && small);
   auto light = [&]() -> int {
     const uint8_t* xm = x_nonzero;
     if (vec4_ok(d, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc)) {
@@ -598,7 +608,7 @@ extern "C" int gnnrec_spmm_csr_heavy_f32(const int64_t* row_ptr, const int32_t* 
   if (!(flags & GNNREC_CSR_FORK)) {
     if (int rc = light()) return rc;
     return launch_heavy(A, heavy_rows, n_heavy, n_sliced, x, ldx, y, ldy, d, epi, self, ld_self,
-                        acc, ld_acc, acc_div, s);
+                        acc, ld_acc, acc_div, small, s);
   }
   // Fork / join: the heavy rows (disjoint from the row-parallel kernel's rows) go first, on the
   // high-priority side stream, so their workgroups — the longest chains — start first and the
@@ -609,7 +619,7 @@ extern "C" int gnnrec_spmm_csr_heavy_f32(const int64_t* row_ptr, const int32_t* 
   if (hipEventRecord(ss->fork, s) != hipSuccess || hipStreamWaitEvent(ss->s, ss->fork, 0) != hipSuccess)
     return check_launch("spmm: fork");
   int rc = launch_heavy(A, heavy_rows, n_heavy, n_sliced, x, ldx, y, ldy, d, epi, self, ld_self,
-                        acc, ld_acc, acc_div, ss->s);
+                        acc, ld_acc, acc_div, small, ss->s);
   const int rc_light = rc == GNNREC_OK ? light() : rc;
   // join even after a failed launch, so the caller's stream never runs ahead of the side's
   if (hipEventRecord(ss->join, ss->s) != hipSuccess || hipStreamWaitEvent(s, ss->join, 0) != hipSuccess)

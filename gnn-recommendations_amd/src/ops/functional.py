@@ -45,18 +45,34 @@ def _csr_args(adj: CsrGraph):
 # 0 disables the split. Sweep (tools/exp_heavy.py, profiles/r01/heavy_split_sweep.jsonl):
 # ML-1M-shaped LightGCN K=3 0.90 ms unsplit -> 0.30 ms at 128, power-law 2M x 2M 123 -> 29 ms;
 # uniform graphs (G100M, max degree ~150) have no rows above it.
-# Round 6 (config 2, profiles/r06/config2_knobs_sweep_*.jsonl, every output bit-identical):
-# 256 -> 128 moves the rows of 129-256 neighbours off the row-parallel kernel, whose time is its
-# longest rows' chain (27.6 -> 21.4 us per hop, profiles/r06/config2_trace/).
-SPMM_HEAVY_THRESHOLD = 128
-# Heavy rows longer than this run as feature slices (gnnrec_spmm_csr_heavy_f32 n_sliced: four
-# d/4-wide workgroups at d = 64 / 128 / 256, two at d = 32; 0 = none): the longest rows' chains
-# then finish in fewer LDS rounds (config 2: 0.215 -> 0.188 ms per forward at threshold 128).
+# Heavy-row knobs of the CSR hop (gnnrec_spmm_csr_heavy_f32), None = by operand (heavy_knobs):
+# rows longer than SPMM_HEAVY_THRESHOLD run one workgroup per row, and of those the rows longer
+# than SPMM_SLICE_LEN as feature slices (workgroups of d/4 or 32 features, chosen in the kernel
+# by operand size; 0 = none). Round-6 sweeps, every output bit-identical
+# (profiles/r06/config2_knobs_sweep_*.jsonl, powerlaw_knobs_sweep.jsonl):
+#   small operands (<= 65 536 rows, e.g. ML-1M): threshold 128, slices above 1024 — config 2
+#     0.246 -> 0.191 ms per forward (threshold 256 unsliced: 0.215);
+#   large: threshold 256 (d <= 64) / 512 (d >= 128), slices above 1024 / 4096 — power-law
+#     2M x 2M K=3 d=64 18.98 -> 15.6 ms, d=128 36.4 -> 24.6 ms; G100M's CSR path (no row above
+#     ~200) 21.1 ms at 256 against 21.4 at 128.
+SPMM_HEAVY_THRESHOLD = None
+SPMM_SLICE_LEN = None
+SMALL_OPERAND_ROWS = 65536          # gnnrec_spmm_csr_heavy_f32's own small-operand bound
 # CSR_FLAGS: _lib.CSR_FORK (the heavy rows on a side stream beside the row-parallel kernel:
-# measured slower, the cross-stream join costs ~17 us per hop) and the row-parallel chain's
-# form (CSR_LIGHT_*; 0 = by operand size).
-SPMM_SLICE_LEN = 1024
+# measured slower, the cross-stream join costs ~17 us per hop, profiles/r06/config2_trace/)
+# and the row-parallel chain's form (CSR_LIGHT_*; 0 = by operand size).
 CSR_FLAGS = 0
+
+
+def heavy_knobs(n_rows: int, d: int) -> Tuple[int, int]:
+    """(heavy threshold, slice length) for a CSR hop over n_rows destination rows at width d
+    (the module's SPMM_* settings when not None)."""
+    small = n_rows <= SMALL_OPERAND_ROWS
+    ht = SPMM_HEAVY_THRESHOLD if SPMM_HEAVY_THRESHOLD is not None else (
+        128 if small else (256 if d <= 64 else 512))
+    sl = SPMM_SLICE_LEN if SPMM_SLICE_LEN is not None else (
+        1024 if (small or d <= 64) else 4096)
+    return ht, sl
 
 
 # Column-ordered hop (gnnrec_spmm_tiled_f32, DESIGN.md §3.1c): the same bits, used for any d
@@ -228,7 +244,7 @@ def _heavy_args(adj: CsrGraph, x: torch.Tensor, heavy_threshold: int,
                 slice_len: Optional[int] = None):
     """(heavy_rows ptr, n_heavy, threshold, n_sliced) for the split launch, or the no-split
     tuple. n_sliced: how many of the (longest-first) heavy rows are longer than slice_len
-    (None: SPMM_SLICE_LEN; 0: none)."""
+    (None: heavy_knobs; 0: none)."""
     d = x.shape[1]
     if (heavy_threshold <= 0 or d % 4 or d < 16 or d > 256 or x.stride(0) % 4
             or x.data_ptr() % 16):
@@ -236,7 +252,7 @@ def _heavy_args(adj: CsrGraph, x: torch.Tensor, heavy_threshold: int,
     rows = adj.heavy_rows(heavy_threshold)
     if rows is None:
         return None, 0, 0, 0
-    sl = SPMM_SLICE_LEN if slice_len is None else slice_len
+    sl = heavy_knobs(adj.n_rows, d)[1] if slice_len is None else slice_len
     n_sliced = adj.heavy_rows_longer(heavy_threshold, sl) if sl > 0 else 0
     return ptr(rows), rows.numel(), int(heavy_threshold), n_sliced
 
@@ -263,7 +279,7 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
     if x.shape[0] < adj.shape[1]:
         raise ValueError(f"x has {x.shape[0]} rows, operand has {adj.shape[1]} columns")
     L = _lib.lib()
-    ht = SPMM_HEAVY_THRESHOLD if heavy_threshold is None else heavy_threshold
+    ht = heavy_knobs(adj.n_rows, d)[0] if heavy_threshold is None else heavy_threshold
     if y_active is not None and (y_active.dtype != torch.uint8 or y_active.device != x.device
                                  or y_active.numel() < adj.n_rows):
         raise ValueError("y_active must be a uint8 tensor on x's device with a byte per "
@@ -536,7 +552,7 @@ def lightgcn_forward(adj: CsrGraph, x0: torch.Tensor, n_layers: int,
     elif n_layers == 1:
         work0 = work1 = torch.empty_like(x0)
     L = _lib.lib()
-    ht = SPMM_HEAVY_THRESHOLD if heavy_threshold is None else heavy_threshold
+    ht = heavy_knobs(n, d)[0] if heavy_threshold is None else heavy_threshold
     check(L.gnnrec_lightgcn_heavy_f32(*_csr_args(adj), ptr(x0), d, int(n_layers), ptr(work0),
                                       ptr(work1), ptr(layers), ptr(out), d,
                                       *_heavy_args(adj, x0, ht), int(CSR_FLAGS),

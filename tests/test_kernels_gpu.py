@@ -359,7 +359,7 @@ def test_lightgcn_forward_rows_equal_full(cuda, K, d):
         need = torch.zeros(n, dtype=torch.uint8, device=cuda)
         idx = torch.randperm(n, device=cuda)[:n_need]
         need[idx] = 1
-        hr = g.heavy_rows(F.SPMM_HEAVY_THRESHOLD)
+        hr = g.heavy_rows(F.heavy_knobs(n, d)[0])
         if hr is not None and n_need > 1:
             need[hr[:2]] = 1
         out = F.lightgcn_forward_rows(g, x0, K, need)

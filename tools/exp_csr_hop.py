@@ -100,8 +100,10 @@ with torch.no_grad():
         g100 = bench.build_graph(1_000_000, 1_000_000, 100_000_000, 0, 16).to(dev)
         x = torch.randn(2_000_000, 64, device=dev, generator=torch.Generator(device=dev).manual_seed(0))
         F.TILED_HOP = False
-        t, (out, _) = ms_of(lambda: F.lightgcn_forward(g100, x, 3), 2)
-        emit(case="g100m_csr_propagate", ms=t, sha=sha(out))
+        for ht in ((128, 256) if a.sweep else (None,)):
+            t, (out, _) = ms_of(lambda: F.lightgcn_forward(g100, x, 3, heavy_threshold=ht), 2)
+            emit(case="g100m_csr_propagate", heavy_threshold=ht, ms=t, sha=sha(out))
+        F.TILED_HOP = True
     if a.powerlaw:
         sys.path.insert(0, str(ROOT / "tools"))
         from bench_configs import powerlaw_graph
@@ -109,6 +111,9 @@ with torch.no_grad():
         from src.ops import _lib
         knobs = {"r05": (256, 0, _lib.CSR_LIGHT_THROUGHPUT),
                  "r06": (F.SPMM_HEAVY_THRESHOLD, F.SPMM_SLICE_LEN, F.CSR_FLAGS)}
+        if a.sweep:
+            knobs.update({f"ht{ht}_sl{sl}": (ht, sl, 0) for ht in (128, 256, 512)
+                          for sl in (0, 1024, 4096) if not sl or sl >= ht})
         for d in (64, 128):
             x = torch.randn(4_000_000, d, device=dev, generator=torch.Generator(device=dev).manual_seed(d))
             for name, (ht, sl, fl) in knobs.items():
