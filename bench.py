@@ -164,29 +164,36 @@ class Layout:
         log(f"layout F={self.grid.F} x R={self.grid.R}: tables ready, planning")
         # operand re-layout for the column-ordered hop (built once, outside the timed region);
         # the uploads and table fills queued before it are drained first, so plan_s is the
-        # plan's own time
+        # plan's own time. Its pieces are timed in the order tiled_plan_for runs them: the
+        # operand's longest row (a device reduction), the kernel's LDS grant for the block size
+        # (a driver query), then the plan itself (CsrGraph.tiled_plan: device planner and its
+        # sub-phases, degree factors, factor check, quad layout), each synchronised.
+        shard = self.dg.shard
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        plan = F.tiled_plan_for(self.dg.shard, self.x0_pad)
+        shard.max_degree()
+        torch.cuda.synchronize()
+        t_md = time.perf_counter()
+        rpb = F._tiled_rows_per_block(shard.n_rows, device)
+        F._tiled_supported(device, rpb)
+        t_sup = time.perf_counter()
+        plan = F.tiled_plan_for(shard, self.x0_pad)
         self.tiled = plan is not None
         torch.cuda.synchronize()
-        self.plan_s = time.perf_counter() - t1
-        # phase times inside it (CsrGraph.tiled_plan: device planner and its sub-phases,
-        # degree factors, factor check, quad layout), each synchronised, and the rest of
-        # plan_s (tiled_plan_for's own checks: max degree, device properties) as setup_s
-        self.plan_phases = dict(plan["build_s"]) if plan is not None else None
+        t_end = time.perf_counter()
+        self.plan_s = t_end - t1
+        self.plan_phases = None
         if plan is not None:
-            inner = sum(v for k, v in self.plan_phases.items()
-                        if k.endswith("_s") and isinstance(v, float))
-            self.plan_phases["setup_s"] = self.plan_s - inner
+            self.plan_phases = dict(plan["build_s"], max_degree_s=t_md - t1,
+                                    kernel_lds_query_s=t_sup - t_md,
+                                    tiled_plan_call_s=t_end - t_sup)
             # the same build again in this (now warm) process: what the first call's one-time
-            # costs (code-object loads, first allocations of the plan's GBs) add to plan_s
-            key = [k for k, v in self.dg.shard._plans.items() if v is plan]
-            for k in key:
-                del self.dg.shard._plans[k]
+            # costs (first allocations, first use of each kernel) add to plan_s
+            for k in [k for k, v in shard._plans.items() if v is plan]:
+                del shard._plans[k]
             torch.cuda.synchronize()
             t2 = time.perf_counter()
-            plan2 = F.tiled_plan_for(self.dg.shard, self.x0_pad)
+            plan2 = F.tiled_plan_for(shard, self.x0_pad)
             torch.cuda.synchronize()
             self.plan_phases["warm_rebuild_s"] = time.perf_counter() - t2
             self.plan_phases["warm_rebuild_phases"] = plan2["build_s"]

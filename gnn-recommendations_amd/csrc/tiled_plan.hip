@@ -408,10 +408,53 @@ __global__ __launch_bounds__(256) void tiled_plan_tail_kernel(const int64_t* end
   if (i < GNNREC_TILED_TAIL * GNNREC_TILED_HDR_WORDS) hdr[e * GNNREC_TILED_HDR_WORDS + i] = 0u;
 }
 
+// Row statistics of a device CSR in one workgroup: out[0] = the longest row, out[1] = the most
+// edges of any block of `block_rows` consecutive rows (0 when block_rows <= 0). One kernel of
+// this library instead of a chain of torch reductions: in a fresh process every torch kernel's
+// first launch loads its code object, which cost the plan build ≈ 0.2 s (profiles/r06/).
+__global__ __launch_bounds__(1024) void csr_row_stats_kernel(const int64_t* __restrict__ row_ptr,
+                                                             int64_t n_rows, int64_t block_rows,
+                                                             int64_t* __restrict__ out) {
+  __shared__ int64_t red[2][1024 / 64];
+  int64_t mrow = 0, mblk = 0;
+  for (int64_t r = threadIdx.x; r < n_rows; r += blockDim.x)
+    mrow = max(mrow, row_ptr[r + 1] - row_ptr[r]);
+  if (block_rows > 0) {
+    const int64_t nb = (n_rows + block_rows - 1) / block_rows;
+    for (int64_t b = threadIdx.x; b < nb; b += blockDim.x) {
+      const int64_t e = min(n_rows, (b + 1) * block_rows);
+      mblk = max(mblk, row_ptr[e] - row_ptr[b * block_rows]);
+    }
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    mrow = max(mrow, __shfl_xor(mrow, d, 64));
+    mblk = max(mblk, __shfl_xor(mblk, d, 64));
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = mrow;
+    red[1][w] = mblk;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    int64_t m = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) m = max(m, red[threadIdx.x][i]);
+    out[threadIdx.x] = m;
+  }
+}
+
 }  // namespace
 }  // namespace gnnrec
 
 using namespace gnnrec;
+
+extern "C" int gnnrec_csr_row_stats(const int64_t* row_ptr, int64_t n_rows, int64_t block_rows,
+                                    int64_t* out, gnnrec_stream_t stream) {
+  GNNREC_REQUIRE(row_ptr && out && n_rows >= 0, "csr_row_stats: bad args");
+  hipLaunchKernelGGL(csr_row_stats_kernel, dim3(1), dim3(1024), 0, as_hip(stream), row_ptr,
+                     n_rows, block_rows, out);
+  return check_launch("csr_row_stats");
+}
 
 extern "C" int64_t gnnrec_tiled_plan_device_scratch_words(int64_t max_block_nnz,
                                                          int32_t workgroups) {

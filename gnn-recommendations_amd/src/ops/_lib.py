@@ -71,6 +71,7 @@ _SIGNATURES = {
     "gnnrec_tiled_plan_emit": [_p, _p, _p, _p, _p, _p],
     "gnnrec_tiled_plan_free": [_p],
     "gnnrec_tiled_plan_device_scratch_words": [_i64, _i32],
+    "gnnrec_csr_row_stats": [_p, _i64, _i64, _p, _p],
     "gnnrec_tiled_plan_device": [_p, _p, _p, _i64, _i32, _i32, _i32, _i64, _p, _i32, _p, _p, _p,
                                  _p, _p, _p, _p, _p],
     "gnnrec_spmm_tiled_supported": [_i32, _i32],
@@ -117,6 +118,13 @@ _SIGNATURES = {
     "gnnrec_gat_train_backward_f32": [_p, _p, _i64, _p, _i64, _p, _p, _i64, _i32, _i32, _f32,
                                       _f32, C.c_uint32, _p, _i64, _p, _i64, _p, _p, _i64, _p, _p,
                                       _p],
+    "gnnrec_gat_train_forward_split_f32": [_p, _p, _i64, _p, _i64, _p, _p, _i64, _i32, _i32,
+                                           _f32, _f32, C.c_uint32, _p, _i64, _p, _i64, _p, _p,
+                                           _p, _i64, _p, _p, _i64, _p, _p],
+    "gnnrec_gat_train_backward_split_f32": [_p, _p, _i64, _p, _i64, _p, _p, _i64, _i32, _i32,
+                                            _f32, _f32, C.c_uint32, _p, _i64, _p, _i64, _p, _p,
+                                            _i64, _p, _p, _i64, _p, _p, _p, _i64, _p, _p, _i64,
+                                            _p, _p],
     "gnnrec_score_topk_f32": [_p, _i64, _i64, _p, _i64, _i64, _i32, _p, _p, _i32, _p, _p, _p],
     "gnnrec_score_topk_split_f32": [_p, _i64, _i64, _p, _i64, _i64, _i32, _p, _p, _i32, _i32,
                                     _p, _p, _p, _p, _p],

@@ -839,39 +839,68 @@ def gat_train_supported(adj: CsrGraph, heads: int, o_dim: int) -> bool:
             and heads * o_dim in (16, 32, 64, 128, 256) and adj.pattern_symmetric())
 
 
+# GAT training's heavy-row split (gnnrec_gat_train_*_split_f32): rows longer than the threshold
+# are cut into segments of at most GAT_TRAIN_SEGMENT edges (CsrGraph.heavy_plan), their partial
+# sums merged per row. 0 disables it (every row one lane group: a 4e5-neighbour hub then takes
+# the whole step, profiles/r06/gat_train_*).
+GAT_TRAIN_HEAVY_THRESHOLD = 2048
+GAT_TRAIN_SEGMENT = 1024
+
+
+def _gat_train_split_args(adj: CsrGraph, F: int, heads: int, device):
+    """(max_row_len, seg_row, seg_beg, seg_end, n_seg, heavy_rows, heavy_seg_ptr, n_heavy,
+    work) for the split launches, or the no-split tuple; work is returned separately to keep
+    it alive."""
+    plan = (adj.heavy_plan(GAT_TRAIN_HEAVY_THRESHOLD, GAT_TRAIN_SEGMENT)
+            if GAT_TRAIN_HEAVY_THRESHOLD > 0 else None)
+    if plan is None:
+        return (0, None, None, None, 0, None, None, 0, None), None
+    n_seg = plan["seg_row"].numel()
+    work = torch.empty(n_seg * (F + 2 * heads) + 4, dtype=torch.float32, device=device)
+    return (int(GAT_TRAIN_HEAVY_THRESHOLD), ptr(plan["seg_row"]), ptr(plan["seg_beg"]),
+            ptr(plan["seg_end"]), n_seg, ptr(plan["heavy_rows"]), ptr(plan["heavy_seg_ptr"]),
+            plan["heavy_rows"].numel(), ptr(work)), work
+
+
 class _GatTrainAggregate(torch.autograd.Function):
     """out[:, q*o:(q+1)*o] = dropout(softmax_j(LeakyReLU(s_self[r,q] + s_neigh[j,q]))) @ h_q —
     one GATLayer's per-head aggregation (gat.py:113-141) with its backward in two native passes;
-    h, s_self and s_neigh are the differentiable inputs (the projections stay in autograd)."""
+    h, s_self and s_neigh are the differentiable inputs (the projections stay in autograd).
+    Rows above GAT_TRAIN_HEAVY_THRESHOLD run as merged segments in all three passes; the forward
+    keeps the softmax statistics for the backward."""
 
     @staticmethod
     def forward(ctx, h, s_self, s_neigh, adj, heads, o_dim, slope, drop_p, seed):
         h, s_self, s_neigh = h.contiguous(), s_self.contiguous(), s_neigh.contiguous()
         n = adj.n_rows
         out = torch.empty((n, heads * o_dim), dtype=torch.float32, device=h.device)
-        check(_lib.lib().gnnrec_gat_train_forward_f32(
+        stats = torch.empty(n * heads * 4 + 4, dtype=torch.float32, device=h.device)
+        split, work = _gat_train_split_args(adj, heads * o_dim, heads, h.device)
+        check(_lib.lib().gnnrec_gat_train_forward_split_f32(
             ptr(adj.row_ptr), ptr(adj.col), n, ptr(h), h.stride(0), ptr(s_self), ptr(s_neigh),
             s_self.stride(0), int(heads), int(o_dim), float(slope), float(drop_p), int(seed),
-            ptr(out), out.stride(0), _lib.stream_of(adj.device)), "gnnrec_gat_train_forward_f32")
-        ctx.save_for_backward(h, s_self, s_neigh, out)
+            ptr(out), out.stride(0), ptr(stats), *split, _lib.stream_of(adj.device)),
+            "gnnrec_gat_train_forward_split_f32")
+        ctx.save_for_backward(h, s_self, s_neigh, out, stats)
         ctx.cfg = (adj, int(heads), int(o_dim), float(slope), float(drop_p), int(seed))
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        h, s_self, s_neigh, out = ctx.saved_tensors
+        h, s_self, s_neigh, out, stats = ctx.saved_tensors
         adj, heads, o_dim, slope, drop_p, seed = ctx.cfg
         dout = dout.contiguous()
         n = adj.n_rows
         dh = torch.empty_like(h)
         d_self = torch.empty_like(s_self)
         d_neigh = torch.empty_like(s_neigh)
-        stats = torch.empty(n * heads * 4 + 4, dtype=torch.float32, device=h.device)
-        check(_lib.lib().gnnrec_gat_train_backward_f32(
+        split, work = _gat_train_split_args(adj, heads * o_dim, heads, h.device)
+        check(_lib.lib().gnnrec_gat_train_backward_split_f32(
             ptr(adj.row_ptr), ptr(adj.col), n, ptr(h), h.stride(0), ptr(s_self), ptr(s_neigh),
             s_self.stride(0), heads, o_dim, slope, drop_p, seed, ptr(out), out.stride(0),
             ptr(dout), dout.stride(0), ptr(stats), ptr(dh), dh.stride(0), ptr(d_self),
-            ptr(d_neigh), _lib.stream_of(adj.device)), "gnnrec_gat_train_backward_f32")
+            ptr(d_neigh), *split, _lib.stream_of(adj.device)),
+            "gnnrec_gat_train_backward_split_f32")
         return dh, d_self, d_neigh, None, None, None, None, None, None
 
 

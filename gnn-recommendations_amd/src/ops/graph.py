@@ -433,11 +433,31 @@ class CsrGraph:
                 self._plans[key] = int((deg > length).sum())
         return self._plans[key]
 
+    def row_stats(self, block_rows: int = 0) -> Tuple[int, int]:
+        """(longest row, most edges in a block of block_rows consecutive rows): on a device
+        graph one gnnrec_csr_row_stats launch and an 16-B read (no torch kernels, whose first
+        launches in a fresh process cost ~0.1 s each to load), on the host numpy."""
+        if self.n_rows == 0:
+            return 0, 0
+        if self.device.type == "cuda":
+            out = torch.empty(2, dtype=torch.int64, device=self.device)
+            _lib.check(_lib.lib().gnnrec_csr_row_stats(_lib.ptr(self.row_ptr), self.n_rows,
+                                                       int(block_rows), _lib.ptr(out),
+                                                       _lib.stream_of(self.device)),
+                       "gnnrec_csr_row_stats")
+            a, b = out.cpu().tolist()
+            return int(a), int(b)
+        rp = self.row_ptr.numpy()
+        mb = 0
+        if block_rows > 0:
+            starts = np.arange(0, self.n_rows, block_rows)
+            mb = int((rp[np.minimum(starts + block_rows, self.n_rows)] - rp[starts]).max())
+        return int(np.diff(rp).max()), mb
+
     def max_degree(self) -> int:
         """Longest row (cached; one device read the first time)."""
         if "max_degree" not in self._plans:
-            deg = self.row_ptr[1:] - self.row_ptr[:-1]
-            self._plans["max_degree"] = int(deg.max()) if deg.numel() else 0
+            self._plans["max_degree"] = self.row_stats()[0]
         return self._plans["max_degree"]
 
     def tiled_plan(self, rows_per_block: int = 1117, panel: int = 49152,
@@ -635,24 +655,28 @@ class CsrGraph:
         dev = self.device
         if dev.type != "cuda":
             raise ValueError("the device planner needs the graph on a ROCm device")
+        import time
+        t0 = time.perf_counter()
         n, W = self.n_rows, _lib.TILED_WAVES
         nb = -(-n // R)
-        rp = self.row_ptr
-        starts = torch.arange(nb, dtype=torch.int64, device=dev) * R
-        bnnz = rp[torch.clamp(starts + R, max=n)] - rp[starts]
-        max_nnz = int(bnnz.max()) if nb else 0
+        max_nnz = self.row_stats(R)[1] if nb else 0
         if max_nnz >= (1 << 31) - 1:
             raise ValueError("tiled plan: a block holds more than 2^31 edges")
         cap = min(max_nnz, TILED_PLAN_STEP_CAP)
+        prologue = time.perf_counter() - t0
         try:
-            return self._tiled_plan_device_pass(R, panel, sub_panel, nb, cap)
+            plan = self._tiled_plan_device_pass(R, panel, sub_panel, nb, cap)
         except _ScratchTooSmall:
-            return self._tiled_plan_device_pass(R, panel, sub_panel, nb, max_nnz)
+            plan = self._tiled_plan_device_pass(R, panel, sub_panel, nb, max_nnz)
+        plan["planner_phases"]["block_sizes_s"] = prologue
+        return plan
 
     def _tiled_plan_device_pass(self, R, panel, sub_panel, nb, cap) -> dict:
         dev = self.device
         L = _lib.lib()
         n, W = self.n_rows, _lib.TILED_WAVES
+        import time
+        t_alloc = time.perf_counter()
         per_wg = 8 * L.gnnrec_tiled_plan_device_scratch_words(cap, 1)
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         # one 64-lane workgroup per block (23 KB of LDS: 7 per CU), scratch at most ~4 GB
@@ -673,8 +697,6 @@ class CsrGraph:
             raise _DEVICE_PLAN_ERRORS.get(code, RuntimeError)(
                 f"gnnrec_tiled_plan_device ({what}) failed: error {code}")
 
-        import time
-        t_alloc = time.perf_counter()
         torch.cuda.synchronize(dev)
         t_count = time.perf_counter()
         _lib.check(L.gnnrec_tiled_plan_device(*args, ptr(chunks), ptr(n_steps), None, None, None,
@@ -700,8 +722,9 @@ class CsrGraph:
             failed("emit", code)
         t_end = time.perf_counter()
         del scratch
-        # sub-phases of the planner (bench.py's operand_prep_s): scratch allocation, the count
-        # pass (+ cumsum, chunk total read back), the plan arrays' allocation, the emit pass
+        # sub-phases of the planner (bench.py's operand_prep_s): the scratch / count arrays'
+        # allocation, the count pass (+ cumsum, chunk total read back), the plan arrays'
+        # allocation, the emit pass (and, from _tiled_plan_device, the block sizes before them)
         phases = dict(scratch_alloc_s=t_count - t_alloc, count_s=t_emit_alloc - t_count,
                       arrays_alloc_s=t_emit - t_emit_alloc, emit_s=t_end - t_emit)
         return dict(slot=slot, val=v, hdr=hdr, wave_ptr=wave_ptr, n_steps=n_steps,

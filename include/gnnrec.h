@@ -234,6 +234,11 @@ int gnnrec_tiled_plan_free(void* plan);
  * too small, 3 a run — one row's slots in one step — longer than 32 767, 4 count / emit
  * mismatch). */
 int64_t gnnrec_tiled_plan_device_scratch_words(int64_t max_block_nnz, int32_t workgroups);
+/* Row statistics of a device CSR (ABI 11), written to the device int64 out[2]: out[0] = the
+ * longest row, out[1] = the most edges in any block of block_rows consecutive rows (the
+ * planner's max_block_nnz; 0 when block_rows <= 0). One single-workgroup kernel. */
+int gnnrec_csr_row_stats(const int64_t* row_ptr, int64_t n_rows, int64_t block_rows, int64_t* out,
+                         gnnrec_stream_t stream);
 int gnnrec_tiled_plan_device(const int64_t* row_ptr, const int32_t* col, const float* val,
                              int64_t n_rows, int32_t rows_per_block, int32_t panel,
                              int32_t sub_panel, int64_t max_block_nnz, uint64_t* scratch,
@@ -478,7 +483,8 @@ int gnnrec_gat_heavy_att_f32(const int32_t* col, const int64_t* seg_row, const i
  * of (seed, r, j, q) — the reference's F.dropout on the attention weights, gat.py:137 —
  * regenerated (not stored) by the backward. hfeat: the head-major [N, heads*o_dim] table
  * (ldh), s_self / s_neigh: [N, heads] (row stride ld_s); out [n_rows, heads*o_dim] (ldo).
- * No heavy-row split, no epilogue (the caller's autograd applies head mean / ELU / layer mean).
+ * No epilogue (the caller's autograd applies head mean / ELU / layer mean); the _split
+ * variants below cut long rows into segments.
  * Backward (two passes over the CSR; the pattern must be SYMMETRIC, as the normalised
  * bipartite adjacency is: row j lists the rows that aggregate j): given dout, writes
  * dh [n, heads*o_dim] (lddh), d_self and d_neigh [n, heads] (contiguous); stats is a scratch of
@@ -497,6 +503,30 @@ int gnnrec_gat_train_backward_f32(const int64_t* row_ptr, const int32_t* col, in
                                   int64_t ldo, const float* dout, int64_t lddo, float* stats,
                                   float* dh, int64_t lddh, float* d_self, float* d_neigh,
                                   gnnrec_stream_t stream);
+/* The same two calls with a heavy-row split (ABI 11; rows longer than max_row_len, e.g. the
+ * 4e5-neighbour hubs of config 5, which one lane group would walk serially): the segment plan
+ * of CsrGraph.heavy_plan (seg_row / seg_beg / seg_end [n_seg], heavy_rows [n_heavy] and
+ * heavy_seg_ptr [n_heavy + 1], every heavy row's segments contiguous), a 16-B aligned work
+ * buffer of n_seg * (heads * o_dim + 2 heads) floats. Each segment's partial sums are computed
+ * by one lane group and merged per row in segment order (deterministic). The forward writes
+ * the softmax statistics into stats (n_rows * heads * 4 floats: max, sum); the backward reads
+ * them from there (no recount pass) — it must get the stats of the forward of the same inputs.
+ * max_row_len == 0 or n_heavy == 0: no split. */
+int gnnrec_gat_train_forward_split_f32(
+    const int64_t* row_ptr, const int32_t* col, int64_t n_rows, const float* hfeat, int64_t ldh,
+    const float* s_self, const float* s_neigh, int64_t ld_s, int32_t heads, int32_t o_dim,
+    float slope, float drop_p, uint32_t seed, float* out, int64_t ldo, float* stats,
+    int64_t max_row_len, const int64_t* seg_row, const int64_t* seg_beg, const int64_t* seg_end,
+    int64_t n_seg, const int64_t* heavy_rows, const int64_t* heavy_seg_ptr, int64_t n_heavy,
+    float* work, gnnrec_stream_t stream);
+int gnnrec_gat_train_backward_split_f32(
+    const int64_t* row_ptr, const int32_t* col, int64_t n_rows, const float* hfeat, int64_t ldh,
+    const float* s_self, const float* s_neigh, int64_t ld_s, int32_t heads, int32_t o_dim,
+    float slope, float drop_p, uint32_t seed, const float* out, int64_t ldo, const float* dout,
+    int64_t lddo, float* stats, float* dh, int64_t lddh, float* d_self, float* d_neigh,
+    int64_t max_row_len, const int64_t* seg_row, const int64_t* seg_beg, const int64_t* seg_end,
+    int64_t n_seg, const int64_t* heavy_rows, const int64_t* heavy_seg_ptr, int64_t n_heavy,
+    float* work, gnnrec_stream_t stream);
 
 /* Dense projections of the GAT layer (gat.py:113-118 W_h x and the attention halves, one
  * fused weight; and the head-averaged last layer's W_h applied after the aggregation,

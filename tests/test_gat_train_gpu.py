@@ -137,3 +137,38 @@ def test_gat_trains_natively_above_the_dense_bound(cuda):
         losses.append(loss.item())
     assert losses[-1] < losses[0]
     assert torch.cuda.max_memory_allocated(cuda) - base < (nu + ni) ** 2    # no [N, N]
+
+
+@pytest.mark.parametrize("heads,o", [(4, 16), (4, 64), (1, 64)])
+def test_gat_train_heavy_split_matches_unsplit(cuda, heads, o):
+    """rows above GAT_TRAIN_HEAVY_THRESHOLD run as merged segments in the forward,
+    the backward row pass and the column pass (gnnrec_gat_train_*_split_f32). On a power-law
+    graph with rows of thousands of neighbours, forced to split at 64 / 32-edge segments, the
+    output and all three input gradients equal the unsplit kernels' within fp32 reassociation,
+    with attention dropout."""
+    rng = np.random.default_rng(21)
+    nu, ni, n_pairs = 3000, 2000, 60000
+    u = np.concatenate([np.arange(nu), rng.integers(0, nu, ni), rng.zipf(1.5, n_pairs) % nu])
+    i = np.concatenate([rng.integers(0, ni, nu), np.arange(ni), rng.zipf(1.4, n_pairs) % ni])
+    g = CsrGraph.from_interactions(u, i, nu, ni).to(cuda)
+    n = g.n_rows
+    assert g.max_degree() > 1000
+    torch.manual_seed(3)
+    h0 = torch.randn(n, heads * o, device=cuda) * 0.5
+    ss0 = torch.randn(n, heads, device=cuda) * 0.5
+    sn0 = torch.randn(n, heads, device=cuda) * 0.5
+    R = torch.randn(n, heads * o, device=cuda)
+    res = {}
+    saved = F.GAT_TRAIN_HEAVY_THRESHOLD, F.GAT_TRAIN_SEGMENT
+    try:
+        for name, (thr, seg) in {"unsplit": (0, 1024), "split": (64, 32)}.items():
+            F.GAT_TRAIN_HEAVY_THRESHOLD, F.GAT_TRAIN_SEGMENT = thr, seg
+            h, ss, sn = (t.clone().requires_grad_() for t in (h0, ss0, sn0))
+            out = F.gat_aggregate_train(g, h, ss, sn, heads, o, 0.2, 0.3, 99)
+            (out * R).sum().backward()
+            res[name] = [t.detach().cpu().numpy() for t in (out, h.grad, ss.grad, sn.grad)]
+    finally:
+        F.GAT_TRAIN_HEAVY_THRESHOLD, F.GAT_TRAIN_SEGMENT = saved
+    for what, a, b in zip(("out", "dh", "d s_self", "d s_neigh"), res["split"], res["unsplit"]):
+        assert np.isfinite(a).all(), what
+        _close(a, b, what, rel=1e-5)

@@ -216,3 +216,16 @@ def test_chunk_major_plan_on_quad_build_is_flagged(cuda):
     ref = oracle.spmm(g.row_ptr.cpu().numpy(), g.col.cpu().numpy(), g.val.cpu().numpy(),
                       x.cpu().numpy())
     assert np.array_equal(y2.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+def test_csr_row_stats_native_equals_host(cuda):
+    """gnnrec_csr_row_stats (the planner's longest row and block-edge bound, one kernel of this
+    library instead of torch reductions) against the host numpy restatement, incl. empty rows,
+    a ragged last block and block_rows <= 0."""
+    rng = np.random.default_rng(3)
+    g = CsrGraph.from_interactions(rng.integers(0, 5000, 80000), rng.zipf(1.7, 80000) % 3000,
+                                   5000, 3000)
+    gd = g.to(cuda)
+    for R in (0, 1, 7, 1117, 10**6):
+        assert gd.row_stats(R) == g.row_stats(R), R
+    assert gd.max_degree() == int(np.diff(g.row_ptr.numpy()).max())
