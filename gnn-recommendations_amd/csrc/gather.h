@@ -273,13 +273,18 @@ template <> struct SpmmCfg<32> { static constexpr int VEC = 2, CH = 16; };
 template <> struct SpmmCfg<64> { static constexpr int VEC = 1, CH = 8; };   // wave per row
 template <> struct SpmmCfg<128> { static constexpr int VEC = 2, CH = 16; };  // wave per row
 
-// Latency form (gather_row_pipe) per d: the same lane mapping, CH gathers per step.
+// Latency form (gather_row_pipe) per d: VEC features per lane (the throughput form's unless
+// GNNREC_LAT_VEC64 sets d = 64's) and CH gathers per step.
 #ifndef GNNREC_LAT_CH
-#define GNNREC_LAT_CH 8
+#define GNNREC_LAT_CH 16
+#endif
+#ifndef GNNREC_LAT_VEC64
+#define GNNREC_LAT_VEC64 4
 #endif
 template <int D> struct SpmmLatCfg {
   static constexpr bool OK = (D == 32 || D == 64 || D == 128);
-  static constexpr int GROUP = D / SpmmCfg<D>::VEC;
+  static constexpr int VEC = D == 64 ? GNNREC_LAT_VEC64 : SpmmCfg<D>::VEC;
+  static constexpr int GROUP = D / VEC;
   static constexpr int CH = GNNREC_LAT_CH < GROUP ? GNNREC_LAT_CH : GROUP;
 };
 

@@ -28,7 +28,7 @@ __global__ __launch_bounds__(kBlock) void spmm_vec_kernel(
     int epi, const float* __restrict__ self, int64_t ld_self, float* __restrict__ acc,
     int64_t ld_acc, float acc_div, int64_t skip_len, const uint8_t* __restrict__ xmask,
     const uint8_t* __restrict__ y_active) {
-  constexpr int VEC = SpmmCfg<D>::VEC;
+  constexpr int VEC = LAT ? SpmmLatCfg<D>::VEC : SpmmCfg<D>::VEC;
   constexpr int CH = SpmmCfg<D>::CH;
   constexpr int GROUP = D / VEC;
   constexpr int RPW = 64 / GROUP;
@@ -89,9 +89,16 @@ __global__ __launch_bounds__(kBlock) void spmm_generic_kernel(
 // reads neighbours j, j+1 of its feature with one conflict-free ds_read_b64 (two per 4
 // neighbours, plus one 16-B broadcast read of their 4 values), so the consumer issues ~1.75
 // instructions per neighbour around its dependent fmaf instead of a ds_read_b32 each.
-constexpr int kHeavyThreads = 512;
+// Workgroup geometry (experiment builds may halve both: 2 workgroups per CU)
+#ifndef GNNREC_HEAVY_THREADS
+#define GNNREC_HEAVY_THREADS 512
+#endif
+#ifndef GNNREC_HEAVY_BUF
+#define GNNREC_HEAVY_BUF 16384
+#endif
+constexpr int kHeavyThreads = GNNREC_HEAVY_THREADS;
 constexpr int kHeavyLoaders = kHeavyThreads - 64;       // waves 1..7
-constexpr int kHeavyBufFloats = 16384;                   // per LDS buffer (64 KB)
+constexpr int kHeavyBufFloats = GNNREC_HEAVY_BUF;        // per LDS buffer (64 KB)
 constexpr int kHeavyMinD = 16;
 constexpr int kHeavyMaxChunk = kHeavyBufFloats / kHeavyMinD;          // vals per buffer
 constexpr int kHeavyPieces = (kHeavyBufFloats / 4 + kHeavyLoaders - 1) / kHeavyLoaders;  // 10
@@ -102,6 +109,28 @@ constexpr size_t kHeavyLds = 2 * kHeavyBufFloats * sizeof(float) +
 
 // Neighbours per chunk (a multiple of 4) for a row width d: chk + 2 <= 16384 / d.
 __host__ __device__ constexpr int heavy_chunk(int d) { return ((kHeavyBufFloats / d - 2) / 4) * 4; }
+// ... for the 16-neighbour-group consumer: a multiple of 16 with chk + 4 <= 16384 / d
+__host__ __device__ constexpr int heavy_chunk_grp(int d) { return ((kHeavyBufFloats / d - 4) / 16) * 16; }
+
+// 1: the narrow-slice instances (d = 16 / 32 per workgroup, the sliced longest rows) consume in
+// 16-neighbour groups with the values broadcast by DPP (see heavy_row's consume)
+#ifndef GNNREC_HEAVY_GROUPS
+#define GNNREC_HEAVY_GROUPS 1
+#endif
+// diagnostic builds (timing only, results wrong): 1 = no consumer chain, 2 = no row gathers
+#ifndef GNNREC_HEAVY_DIAG
+#define GNNREC_HEAVY_DIAG 0
+#endif
+// 1: the group consumer's fmafs as v_fmac_f32_dpp (inline asm), 0: DPP move + v_fmac
+#ifndef GNNREC_HEAVY_DPP_FMAC
+#define GNNREC_HEAVY_DPP_FMAC 1
+#endif
+
+template <int T>
+__device__ __forceinline__ float lane_bcast16(float v) {   // DPP row_newbcast: lane T of each 16
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                               0x150 + T, 0xF, 0xF, true));
+}
 
 struct HeavyCols {        // (col, val) of one chunk, as this loader thread needs them
   int c[kHeavyPieces];
@@ -152,8 +181,12 @@ __device__ __forceinline__ void heavy_row(
   const int lt = tid - 64;                               // loader thread index
   const int64_t beg = A.row_ptr[r], end = A.row_ptr[r + 1];
   const int q4 = d >> 2;                                 // float4 per neighbour row
-  const int chk = heavy_chunk(d);                        // neighbours per chunk
-  const int S = chk + 2;                                 // LDS row stride of a feature
+  // the 16-neighbour-group consumer (narrow slices, see consume): chunks of 16k neighbours and
+  // a feature stride S = 4 x odd, so a lane's 4 neighbours are one aligned conflict-free
+  // ds_read_b128; otherwise S = chk + 2 (S/2 odd) for the ds_read_b64 pairs
+  constexpr bool kGrp = GNNREC_HEAVY_GROUPS && F == 1 && (DC == 16 || DC == 32);
+  const int chk = kGrp ? heavy_chunk_grp(d) : heavy_chunk(d);   // neighbours per chunk
+  const int S = kGrp ? chk + 4 : chk + 2;                       // LDS row stride of a feature
   const int64_t n_chunks = (end - beg + chk - 1) / chk;
 
   auto load_cols = [&](int64_t c, HeavyCols& hc) {
@@ -177,6 +210,10 @@ __device__ __forceinline__ void heavy_row(
     for (int i = 0; i < kHeavyPieces; ++i) {
       int j, part;
       heavy_piece<DC>(lt + i * kHeavyLoaders, q4, j, part);
+      if (GNNREC_HEAVY_DIAG & 2) {   // diagnostic builds only: no row gathers (wrong results)
+        st.x[i] = make_float4(__int_as_float(hc.c[i]), 0.f, 0.f, 0.f);
+        continue;
+      }
       st.x[i] = hc.c[i] >= 0
                     ? *reinterpret_cast<const float4*>(x + (int64_t)hc.c[i] * ldx + 4 * part)
                     : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -238,11 +275,69 @@ __device__ __forceinline__ void heavy_row(
     for (int f = 0; f < F; ++f) a[f] = __builtin_fmaf(st.v.w, st.x[f][1].y, a[f]);
   };
   auto consume = [&](int64_t c) {
+    if (GNNREC_HEAVY_DIAG & 1) return;   // diagnostic builds only: no chain (wrong results)
     const float* xb = buf + (c & 1) * kHeavyBufFloats;
     const float* vb = vbuf + (c & 1) * kHeavyMaxChunk;
     const int m = (int)min<int64_t>(chk, end - (beg + c * chk));
     const int steps = m >> 2;
-    if constexpr (F == 1 && DC != 0) {
+    if constexpr (kGrp) {
+      // Narrow slices (the longest rows' chains, d = 16 / 32 features per workgroup): the chain
+      // is the time, and the step form below waited on its LDS reads (2 per 4 neighbours, at
+      // most 15 outstanding: lgkmcnt) — 16-18 cycles per neighbour against the ≈ 6 of a bare
+      // dependent v_fma_f32 chain (tools/fma_latency.hip). Here a group of 16 neighbours is ONE
+      // ds_read_b32 of their values (lane l of each 16-lane row reads value j + l % 16; DPP
+      // row_newbcast hands value j + t to every lane) and 4 aligned ds_read_b128 of the lane's
+      // feature, two groups in flight. The fmafs are the row's, in its order: the same bits.
+      struct Grp {
+        float v;
+        float4 x[4];
+      };
+      auto fetch_g = [&](int j, Grp& g) {
+        g.v = vb[j + (lane & 15)];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) g.x[q] = *reinterpret_cast<const float4*>(xb + fo[0] + j + 4 * q);
+      };
+      auto apply_g = [&](const Grp& g) {
+#if GNNREC_HEAVY_DPP_FMAC
+        // one v_fmac_f32_dpp per neighbour (the compiler does not fold a DPP move into a MAC)
+#define GNNREC_F1(X, T)                                                                      \
+  asm volatile("v_fmac_f32_dpp %0, %1, %2 row_newbcast:" #T " row_mask:0xf bank_mask:0xf"  \
+               " bound_ctrl:1"                                                             \
+               : "+v"(a[0])                                                                \
+               : "v"(g.v), "v"(X));
+#define GNNREC_G4(Q, T0, T1, T2, T3) \
+  GNNREC_F1(g.x[Q].x, T0) GNNREC_F1(g.x[Q].y, T1) GNNREC_F1(g.x[Q].z, T2) GNNREC_F1(g.x[Q].w, T3)
+        GNNREC_G4(0, 0, 1, 2, 3) GNNREC_G4(1, 4, 5, 6, 7) GNNREC_G4(2, 8, 9, 10, 11)
+        GNNREC_G4(3, 12, 13, 14, 15)
+#undef GNNREC_G4
+#undef GNNREC_F1
+#else
+#define GNNREC_G4(Q, T0)                                                  \
+  a[0] = __builtin_fmaf(lane_bcast16<T0 + 0>(g.v), g.x[Q].x, a[0]);      \
+  a[0] = __builtin_fmaf(lane_bcast16<T0 + 1>(g.v), g.x[Q].y, a[0]);      \
+  a[0] = __builtin_fmaf(lane_bcast16<T0 + 2>(g.v), g.x[Q].z, a[0]);      \
+  a[0] = __builtin_fmaf(lane_bcast16<T0 + 3>(g.v), g.x[Q].w, a[0]);
+        GNNREC_G4(0, 0) GNNREC_G4(1, 4) GNNREC_G4(2, 8) GNNREC_G4(3, 12)
+#undef GNNREC_G4
+#endif
+      };
+      const int groups = m >> 4;
+      Grp g0, g1;
+      fetch_g(0, g0);
+      fetch_g(16, g1);
+      int q = 0;
+      for (; q + 2 <= groups; q += 2) {
+        apply_g(g0);
+        fetch_g(16 * (q + 2), g0);
+        __builtin_amdgcn_sched_barrier(0);
+        apply_g(g1);
+        fetch_g(16 * (q + 3), g1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (q < groups) apply_g(g0);
+      for (int j = groups * 16; j < m; ++j) a[0] = __builtin_fmaf(vb[j], xb[fo[0] + j], a[0]);
+      return;
+    } else if constexpr (F == 1 && DC != 0) {
       // d = 32 / 64: P register sets, the LDS reads of steps q+1 .. q+P-1 in flight while step
       // q's chain runs. The read-ahead is not clamped to the chunk: reads past it stay inside
       // the allocation (the next buffer, the value buffers, kHeavyPad) and are never applied,
@@ -348,8 +443,10 @@ __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
     if (b < n_sliced * SLICES) {
       const int64_t r = rows[b / SLICES];
       const int f0 = (int)(b % SLICES) * SDC;
-      heavy_row<SF, SDC>(A, r, x + f0, ldx, y + f0, ldy, SDC, epi, self + f0, ld_self,
-                         acc + f0, ld_acc, acc_div);
+      // (y / self / acc are null when the epilogue does not use them)
+      heavy_row<SF, SDC>(A, r, x + f0, ldx, y ? y + f0 : nullptr, ldy, SDC, epi,
+                         self ? self + f0 : nullptr, ld_self, acc ? acc + f0 : nullptr, ld_acc,
+                         acc_div);
       return;
     }
     b -= n_sliced * (SLICES - 1);
@@ -432,17 +529,21 @@ void launch_spmm_vec4(const Csr& A, const float* x, int64_t ldx, float* y, int64
                       const float* self, int64_t ld_self, float* acc, int64_t ld_acc,
                       float acc_div, int64_t skip, const uint8_t* xmask, const uint8_t* y_active,
                       bool lat, hipStream_t s) {
+  // rows per workgroup of each form (the latency form may map a row to fewer lanes)
   constexpr int RPB = (64 / (D / SpmmCfg<D>::VEC)) * (kBlock / 64);
-  const int64_t grid = ceil_div(A.n_rows, RPB);
+  constexpr int RPB_LAT = (64 / (D / SpmmLatCfg<D>::VEC)) * (kBlock / 64);
+  // the masked kernels have no latency form
+  const bool use_lat = lat && SpmmLatCfg<D>::OK && !xmask;
+  const int64_t grid = ceil_div(A.n_rows, use_lat ? RPB_LAT : RPB);
 #define GNNREC_VEC(M, AC, LT)                                                                      \
   hipLaunchKernelGGL((spmm_vec_kernel<D, M, AC, LT>), dim3((unsigned)grid), dim3(kBlock), 0, s, A, \
                      x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc, acc_div, skip, xmask,       \
                      y_active)
   if (xmask && y_active) GNNREC_VEC(true, true, false);
   else if (xmask) GNNREC_VEC(true, false, false);
-  else if (y_active && lat) GNNREC_VEC(false, true, SpmmLatCfg<D>::OK);
+  else if (y_active && use_lat) GNNREC_VEC(false, true, SpmmLatCfg<D>::OK);
   else if (y_active) GNNREC_VEC(false, true, false);
-  else if (lat) GNNREC_VEC(false, false, SpmmLatCfg<D>::OK);
+  else if (use_lat) GNNREC_VEC(false, false, SpmmLatCfg<D>::OK);
   else GNNREC_VEC(false, false, false);
 #undef GNNREC_VEC
 }
@@ -473,11 +574,18 @@ struct SideStream {
 std::mutex g_side_mu;
 SideStream g_side[64];
 
-int side_stream(SideStream** out) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
-    set_error("spmm: no current device for the heavy-row side stream");
+int side_stream(hipStream_t caller, SideStream** out) {
+  // the side stream lives on the caller's stream's device (the null stream: the current one)
+  hipDevice_t dev = 0;
+  int cur = 0;
+  if (hipStreamGetDevice(caller, &dev) != hipSuccess || dev < 0 || dev >= 64 ||
+      hipGetDevice(&cur) != hipSuccess) {
+    set_error("spmm: no device for the heavy-row side stream");
     return GNNREC_EHIP;
+  }
+  if (cur != dev) {
+    set_error("spmm: GNNREC_CSR_FORK needs the caller's stream on the current device");
+    return GNNREC_EINVAL;
   }
   SideStream& ss = g_side[dev];
   if (!ss.s) {
@@ -615,7 +723,7 @@ extern "C" int gnnrec_spmm_csr_heavy_f32(const int64_t* row_ptr, const int32_t* 
   // row-parallel rows fill the CUs as the shorter heavy rows retire.
   std::lock_guard<std::mutex> lock(g_side_mu);
   SideStream* ss = nullptr;
-  if (int rc = side_stream(&ss)) return rc;
+  if (int rc = side_stream(s, &ss)) return rc;
   if (hipEventRecord(ss->fork, s) != hipSuccess || hipStreamWaitEvent(ss->s, ss->fork, 0) != hipSuccess)
     return check_launch("spmm: fork");
   int rc = launch_heavy(A, heavy_rows, n_heavy, n_sliced, x, ldx, y, ldy, d, epi, self, ld_self,

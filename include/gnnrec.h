@@ -142,9 +142,11 @@ int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col, const
  *  - flags: GNNREC_CSR_FORK runs the heavy-row kernel on an internal high-priority side
  *    stream forked from and joined back into `stream` with events (capture-safe), so the
  *    row-parallel rows run beside the heavy chains instead of after them (the two write
- *    disjoint rows). GNNREC_CSR_LIGHT_LATENCY / _THROUGHPUT force the row-parallel chain's
- *    form (default: the latency form — the next step's indices loaded one step ahead — for
- *    operands of at most 65536 rows, whose rows cannot fill the chip; see csrc/gather.h).
+ *    disjoint rows; measured slower than one stream on config 2, so off by default; the
+ *    caller's stream must belong to the current device). GNNREC_CSR_LIGHT_LATENCY /
+ *    _THROUGHPUT force the row-parallel chain's form (default: the latency form — the next
+ *    step's indices loaded one step ahead — for operands of at most 65536 rows, whose rows
+ *    cannot fill the chip; see csrc/gather.h).
  * Replaces the same torch.sparse.mm calls (lightgcn.py:88, ngcf.py:70). */
 #define GNNREC_CSR_FORK 1
 #define GNNREC_CSR_LIGHT_LATENCY 2
