@@ -58,3 +58,49 @@ def test_tiled_plan_refuses_hub_rows(monkeypatch):
         g.tiled_plan(rows_per_block=100, planner="host")
     monkeypatch.setattr(graph, "TILED_PLAN_MAX_DEGREE", g.max_degree())
     assert g.tiled_plan(rows_per_block=100, planner="host")["n_chunks"] > 0
+
+
+def test_heavy_rows_longest_first_and_sliced_prefix():
+    """The SpMM's heavy-row list (CsrGraph.heavy_rows) is longest first, and
+    heavy_rows_longer(t, L) — the sliced rows gnnrec_spmm_csr_heavy_f32 takes as its first
+    n_sliced entries — is exactly the prefix of rows longer than L."""
+    g = _zipf_graph()
+    deg = np.diff(g.row_ptr.numpy())
+    for t in (8, 50, 100):
+        rows = g.heavy_rows(t).numpy()
+        assert set(rows) == set(np.nonzero(deg > t)[0])
+        d = deg[rows]
+        assert np.all(np.diff(d) <= 0)
+        for L in (t, 2 * t, 10 * t, 10**9):
+            n = g.heavy_rows_longer(t, L)
+            assert n == int((deg > max(t, L)).sum()) if L >= t else True
+            assert np.all(d[:n] > L) and np.all(d[n:] <= L)
+
+
+def test_row_stats_host():
+    """CsrGraph.row_stats on the host (the device path is gnnrec_csr_row_stats, pinned against
+    it in test_tiled_plan_gpu.py): the longest row and the planner's block edge bound."""
+    g = _zipf_graph()
+    rp = g.row_ptr.numpy()
+    assert g.row_stats()[0] == int(np.diff(rp).max()) == g.max_degree()
+    for R in (1, 7, 333, 10**7):
+        starts = np.arange(0, g.n_rows, R)
+        want = int((rp[np.minimum(starts + R, g.n_rows)] - rp[starts]).max())
+        assert g.row_stats(R) == (int(np.diff(rp).max()), want)
+
+
+def test_heavy_knobs_by_operand():
+    """functional.heavy_knobs: the round-6 sweeps' choices (small operands 128 / 1024; large ones
+    256 / 1024 at d <= 64 and 512 / 4096 above) and the module overrides."""
+    from src.ops import functional as F
+    assert F.heavy_knobs(9746, 64) == (128, 1024)
+    assert F.heavy_knobs(65536, 128) == (128, 1024)
+    assert F.heavy_knobs(4_000_000, 64) == (256, 1024)
+    assert F.heavy_knobs(4_000_000, 32) == (256, 1024)
+    assert F.heavy_knobs(4_000_000, 128) == (512, 4096)
+    saved = F.SPMM_HEAVY_THRESHOLD, F.SPMM_SLICE_LEN
+    try:
+        F.SPMM_HEAVY_THRESHOLD, F.SPMM_SLICE_LEN = 300, 0
+        assert F.heavy_knobs(9746, 64) == (300, 0)
+    finally:
+        F.SPMM_HEAVY_THRESHOLD, F.SPMM_SLICE_LEN = saved
