@@ -18,6 +18,28 @@
 
 namespace gnnrec {
 
+// Trace builds only (tools/exp_heavy_trace.py): wave-0-lane timestamps (wall_clock64, 100 MHz,
+// then clock64, core cycles) of the first kHeavyTraceBlocks heavy workgroups,
+// [2][block][wave][event]
+#ifdef GNNREC_HEAVY_TRACE
+constexpr int kHeavyTraceBlocks = 8, kHeavyTraceEvents = 64;
+__device__ unsigned long long* g_heavy_trace;
+#define GNNREC_HEAVY_STAMP(ev)                                                                  \
+  do {                                                                                          \
+    if (blockIdx.x < kHeavyTraceBlocks && (threadIdx.x & 63) == 0 && (ev) < kHeavyTraceEvents) \
+    {                                                                                           \
+      const int64_t i_ = (blockIdx.x * (kHeavyThreads / 64) + (threadIdx.x >> 6)) *            \
+                             kHeavyTraceEvents + (ev);                                          \
+      g_heavy_trace[i_] = wall_clock64();                                                       \
+      g_heavy_trace[i_ + kHeavyTraceBlocks * (kHeavyThreads / 64) * kHeavyTraceEvents] =        \
+          clock64();                                                                            \
+    }                                                                                           \
+    ++(ev);                                                                                     \
+  } while (0)
+#else
+#define GNNREC_HEAVY_STAMP(ev) ((void)0)
+#endif
+
 // MASKED: skip the neighbours whose input row is all-zero (xmask). ACTIVE: rows with
 // y_active[r] == 0 are not computed (written as +0 with the epilogue applied) — for rows
 // whose value nobody reads, or that no non-zero input row reaches.
@@ -117,9 +139,14 @@ __host__ __device__ constexpr int heavy_chunk_grp(int d) { return ((kHeavyBufFlo
 #ifndef GNNREC_HEAVY_GROUPS
 #define GNNREC_HEAVY_GROUPS 1
 #endif
-// diagnostic builds (timing only, results wrong): 1 = no consumer chain, 2 = no row gathers
+// diagnostic builds (timing only, results wrong): 1 = no consumer chain, 2 = no row gathers,
+// 4 = loaders idle (the consumer chains whatever the buffers hold)
 #ifndef GNNREC_HEAVY_DIAG
 #define GNNREC_HEAVY_DIAG 0
+#endif
+// groups of 16 neighbours the group consumer keeps in flight (LDS reads ahead of its chain)
+#ifndef GNNREC_HEAVY_GRP_AHEAD
+#define GNNREC_HEAVY_GRP_AHEAD 2
 #endif
 // 1: the group consumer's fmafs as v_fmac_f32_dpp (inline asm), 0: DPP move + v_fmac
 #ifndef GNNREC_HEAVY_DPP_FMAC
@@ -274,6 +301,9 @@ __device__ __forceinline__ void heavy_row(
 #pragma unroll
     for (int f = 0; f < F; ++f) a[f] = __builtin_fmaf(st.v.w, st.x[f][1].y, a[f]);
   };
+#ifdef GNNREC_HEAVY_TRACE
+  int ev = 0;
+#endif
   auto consume = [&](int64_t c) {
     if (GNNREC_HEAVY_DIAG & 1) return;   // diagnostic builds only: no chain (wrong results)
     const float* xb = buf + (c & 1) * kHeavyBufFloats;
@@ -321,20 +351,27 @@ __device__ __forceinline__ void heavy_row(
 #undef GNNREC_G4
 #endif
       };
+      // GA groups in flight (register sets); the read-ahead past the chunk stays inside the
+      // allocation for GA <= 3 (feature rows: chk + 4 + 16 (GA - 1) <= S + 16 (GA - 1) floats
+      // of a 16 384-float buffer; values: into kHeavyPad) and is never applied
+      constexpr int GA = GNNREC_HEAVY_GRP_AHEAD;
+      static_assert(GA >= 1 && GA <= 3, "group consumer: 1..3 groups in flight");
       const int groups = m >> 4;
-      Grp g0, g1;
-      fetch_g(0, g0);
-      fetch_g(16, g1);
+      Grp g[GA];
+#pragma unroll
+      for (int i = 0; i < GA; ++i) fetch_g(16 * i, g[i]);
       int q = 0;
-      for (; q + 2 <= groups; q += 2) {
-        apply_g(g0);
-        fetch_g(16 * (q + 2), g0);
-        __builtin_amdgcn_sched_barrier(0);
-        apply_g(g1);
-        fetch_g(16 * (q + 3), g1);
-        __builtin_amdgcn_sched_barrier(0);
+      for (; q + GA <= groups; q += GA) {
+#pragma unroll
+        for (int i = 0; i < GA; ++i) {
+          apply_g(g[i]);
+          fetch_g(16 * (q + i + GA), g[i]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
-      if (q < groups) apply_g(g0);
+#pragma unroll
+      for (int i = 0; i < GA; ++i)
+        if (q + i < groups) apply_g(g[i]);
       for (int j = groups * 16; j < m; ++j) a[0] = __builtin_fmaf(vb[j], xb[fo[0] + j], a[0]);
       return;
     } else if constexpr (F == 1 && DC != 0) {
@@ -384,7 +421,8 @@ __device__ __forceinline__ void heavy_row(
   // prologue (loaders): chunk 0 parked, chunk 1 gathering, columns of chunk 2 loading
   HeavyCols ca, cb;
   HeavyStage sa, sb;
-  if (!consumer) {
+  GNNREC_HEAVY_STAMP(ev);
+  if (!consumer && !(GNNREC_HEAVY_DIAG & 4)) {
     load_cols(0, ca);
     gather(ca, sa);
     load_cols(1, cb);
@@ -392,25 +430,30 @@ __device__ __forceinline__ void heavy_row(
     gather(cb, sb);
     load_cols(2, ca);
   }
+  GNNREC_HEAVY_STAMP(ev);
   __syncthreads();
+  GNNREC_HEAVY_STAMP(ev);
   // round c: loaders gather c+2, load the columns of c+3, park c+1; wave 0 consumes c.
   // Unrolled by two so the register sets alternate statically.
   auto round = [&](int64_t c, HeavyCols& cols_c2, HeavyCols& cols_c3, HeavyStage& st_c1,
                    HeavyStage& st_c2) {
     if (consumer) {
       consume(c);
-    } else {
+    } else if (!(GNNREC_HEAVY_DIAG & 4)) {   // diagnostic builds: 4 = idle loaders
       gather(cols_c2, st_c2);                // columns of c+2 arrived during round c-1
       load_cols(c + 3, cols_c3);
       if (c + 1 < n_chunks) park(st_c1, (int)((c + 1) & 1));
     }
+    GNNREC_HEAVY_STAMP(ev);
     __syncthreads();
+    GNNREC_HEAVY_STAMP(ev);
   };
   for (int64_t c = 0; c < n_chunks; c += 2) {
     round(c, ca, cb, sb, sa);                // c+1 in sb, c+2 -> sa, cols c+2 in ca, c+3 -> cb
     if (c + 1 < n_chunks) round(c + 1, cb, ca, sa, sb);
   }
   if (!consumer) return;
+  GNNREC_HEAVY_STAMP(ev);
 #pragma unroll
   for (int f = 0; f < F; ++f) {
     const int col_f = lane + 64 * f;
@@ -644,6 +687,12 @@ int launch_heavy(const Csr& A, const int64_t* heavy_rows, int64_t n_heavy, int64
 }
 
 }  // namespace
+
+#ifdef GNNREC_HEAVY_TRACE
+extern "C" int gnnrec_debug_heavy_trace(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_heavy_trace), &buf, sizeof(buf)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 extern "C" int gnnrec_spmm_csr_heavy_f32(const int64_t* row_ptr, const int32_t* col,
                                          const float* val, int64_t n_rows, const float* x,
