@@ -140,7 +140,8 @@ __host__ __device__ constexpr int heavy_chunk_grp(int d) { return ((kHeavyBufFlo
 #define GNNREC_HEAVY_GROUPS 1
 #endif
 // diagnostic builds (timing only, results wrong): 1 = no consumer chain, 2 = no row gathers,
-// 4 = loaders idle (the consumer chains whatever the buffers hold)
+// 4 = loaders idle (the consumer chains whatever the buffers hold), 16 = the group consumer's
+// chain without its LDS reads
 #ifndef GNNREC_HEAVY_DIAG
 #define GNNREC_HEAVY_DIAG 0
 #endif
@@ -323,6 +324,12 @@ __device__ __forceinline__ void heavy_row(
         float4 x[4];
       };
       auto fetch_g = [&](int j, Grp& g) {
+        if (GNNREC_HEAVY_DIAG & 16) {   // diagnostic builds only: no LDS reads (wrong results)
+          g.v = __int_as_float(j + lane);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) g.x[q] = make_float4(g.v, g.v, g.v, g.v);
+          return;
+        }
         g.v = vb[j + (lane & 15)];
 #pragma unroll
         for (int q = 0; q < 4; ++q) g.x[q] = *reinterpret_cast<const float4*>(xb + fo[0] + j + 4 * q);

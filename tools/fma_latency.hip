@@ -206,6 +206,68 @@ __global__ __launch_bounds__(512) void consumer_env_kernel(const float* __restri
   __syncthreads();
 }
 
+// values through v_readlane_b32 into an SGPR, then v_fmac with the SGPR operand
+__global__ void readlane_chain_kernel(const float* __restrict__ in, float* out, long long* cyc, int n) {
+  float a = in[threadIdx.x];
+  const float x = in[128 + threadIdx.x];
+  const int vv = __builtin_bit_cast(int, in[64 + threadIdx.x]);
+  const long long t0 = clock64();
+  for (int i = 0; i < n; i += 16) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+      a = __builtin_fmaf(__builtin_bit_cast(float, __builtin_amdgcn_readlane(vv, t + (i & 32))), x, a);
+  }
+  const long long t1 = clock64();
+  out[threadIdx.x] = a;
+  if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+
+// the group consumer with its values through v_readlane (one ds_read_b32 of 64 values per 64
+// neighbours) and its features as 4 aligned ds_read_b128 per 16; kernel-like LDS layout
+__global__ __launch_bounds__(64) void consumer_readlane_kernel(const float* __restrict__ in, float* out,
+                                                               long long* cyc, int reps) {
+  constexpr int CHK = 1008, S = 1012;
+  extern __shared__ float lds[];
+  float* xb = lds;
+  float* vb = lds + 2 * 16384;
+  for (int i = threadIdx.x; i < 2 * 16384 + 2 * 1024 + 64; i += 64) lds[i] = in[i & 4095] * 0.5f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int fo = min(lane, 15) * S;
+  float a = 0.f;
+  const long long t0 = clock64(), w0 = wall_clock64();
+  for (int rep = 0; rep < reps; ++rep) {
+    for (int j0 = 0; j0 + 64 <= CHK; j0 += 64) {
+      const int vv = __builtin_bit_cast(int, vb[j0 + lane]);
+      float4 x[2][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) x[0][q] = *reinterpret_cast<const float4*>(xb + fo + j0 + 4 * q);
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        if (gq < 3) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            x[(gq + 1) & 1][q] = *reinterpret_cast<const float4*>(xb + fo + j0 + 16 * (gq + 1) + 4 * q);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 xv = x[gq & 1][q];
+          a = __builtin_fmaf(__builtin_bit_cast(float, __builtin_amdgcn_readlane(vv, 16 * gq + 4 * q + 0)), xv.x, a);
+          a = __builtin_fmaf(__builtin_bit_cast(float, __builtin_amdgcn_readlane(vv, 16 * gq + 4 * q + 1)), xv.y, a);
+          a = __builtin_fmaf(__builtin_bit_cast(float, __builtin_amdgcn_readlane(vv, 16 * gq + 4 * q + 2)), xv.z, a);
+          a = __builtin_fmaf(__builtin_bit_cast(float, __builtin_amdgcn_readlane(vv, 16 * gq + 4 * q + 3)), xv.w, a);
+        }
+      }
+    }
+  }
+  const long long t1 = clock64(), w1 = wall_clock64();
+  out[threadIdx.x] = a;
+  if (threadIdx.x == 0) {
+    cyc[0] = t1 - t0;
+    cyc[1] = w1 - w0;
+  }
+}
+
 // core clock against the 100 MHz wall clock (cycles figures -> ns)
 __global__ void clock_rate_kernel(long long* cyc, int n) {
   const long long c0 = clock64(), w0 = wall_clock64();
@@ -270,6 +332,7 @@ int main() {
   run(chain_kernel<8>, "chain8", (long long)n);
   run(dpp_chain_kernel, "dpp_fmac_chain", (long long)n);
   run(sgpr_chain_kernel, "sgpr_fmac_chain", (long long)n);
+  run(readlane_chain_kernel, "readlane_fmac_chain", (long long)n);
   {
     long long cw[3];
     hipLaunchKernelGGL(clock_rate_kernel, dim3(1), dim3(64), 0, 0, cyc, 1 << 22);
@@ -305,6 +368,7 @@ int main() {
              name, (double)cw[0] / (r * 1008.0), 10.0 * (double)cw[1] / (r * 1008.0),
              hipGetErrorString(hipGetLastError()));
     };
+    env(consumer_readlane_kernel, 64, "env_readlane_1wave");
     env(consumer_env_kernel<0, 64, 0>, 64, "env_buf0_1wave");
     env(consumer_env_kernel<1, 64, 0>, 64, "env_buf1_1wave");
     env(consumer_env_kernel<0, 512, 0>, 512, "env_buf0_8waves_idle");
