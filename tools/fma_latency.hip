@@ -268,6 +268,61 @@ __global__ __launch_bounds__(64) void consumer_readlane_kernel(const float* __re
   }
 }
 
+// values as SGPR operands straight from global memory (s_load, uniform addresses) and the
+// features from LDS (kernel-like layout): 2 groups of 16 neighbours per batch, the next batch's
+// s_loads and ds_reads issued before this batch's chain; PF: also touch the values PF batches
+// ahead with one s_load_dword (warming the scalar cache)
+template <int PF>
+__global__ __launch_bounds__(64) void consumer_sgpr_kernel(const float* __restrict__ in,
+                                                           const float* __restrict__ vals,
+                                                           float* out, long long* cyc, int reps) {
+  constexpr int CHK = 1008, S = 1012, NB = 32;
+  extern __shared__ float lds[];
+  float* xb = lds;
+  for (int i = threadIdx.x; i < 2 * 16384; i += 64) lds[i] = in[i & 4095] * 0.5f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int fo = min(lane, 15) * S;
+  float a = 0.f;
+  unsigned sink = 0;
+  const long long t0 = clock64(), w0 = wall_clock64();
+  for (int rep = 0; rep < reps; ++rep) {
+    const float* vr = vals + (rep & 7) * 1024;
+    float vc[NB];
+    float4 xc[NB / 4];
+#pragma unroll
+    for (int t = 0; t < NB; ++t) vc[t] = vr[t];
+#pragma unroll
+    for (int q = 0; q < NB / 4; ++q) xc[q] = *reinterpret_cast<const float4*>(xb + fo + 4 * q);
+    for (int j0 = 0; j0 + NB <= CHK; j0 += NB) {
+      float vn[NB];
+      float4 xn[NB / 4];
+#pragma unroll
+      for (int t = 0; t < NB; ++t) vn[t] = vr[j0 + NB + t];
+#pragma unroll
+      for (int q = 0; q < NB / 4; ++q) xn[q] = *reinterpret_cast<const float4*>(xb + fo + j0 + NB + 4 * q);
+      if (PF) sink += __builtin_bit_cast(unsigned, vr[j0 + PF * NB]);
+#pragma unroll
+      for (int q = 0; q < NB / 4; ++q) {
+        a = __builtin_fmaf(vc[4 * q + 0], xc[q].x, a);
+        a = __builtin_fmaf(vc[4 * q + 1], xc[q].y, a);
+        a = __builtin_fmaf(vc[4 * q + 2], xc[q].z, a);
+        a = __builtin_fmaf(vc[4 * q + 3], xc[q].w, a);
+      }
+#pragma unroll
+      for (int t = 0; t < NB; ++t) vc[t] = vn[t];
+#pragma unroll
+      for (int q = 0; q < NB / 4; ++q) xc[q] = xn[q];
+    }
+  }
+  const long long t1 = clock64(), w1 = wall_clock64();
+  out[threadIdx.x] = a + (sink == 12345u ? 1.f : 0.f);
+  if (threadIdx.x == 0) {
+    cyc[0] = t1 - t0;
+    cyc[1] = w1 - w0;
+  }
+}
+
 // core clock against the 100 MHz wall clock (cycles figures -> ns)
 __global__ void clock_rate_kernel(long long* cyc, int n) {
   const long long c0 = clock64(), w0 = wall_clock64();
@@ -369,6 +424,27 @@ int main() {
              hipGetErrorString(hipGetLastError()));
     };
     env(consumer_readlane_kernel, 64, "env_readlane_1wave");
+    {
+      float* vals;
+      hipMalloc(&vals, 8 * 1024 * sizeof(float) + 4096);
+      hipMemcpy(vals, h, 4096 * sizeof(float), hipMemcpyHostToDevice);
+      hipMemcpy(vals + 4096, h, 4096 * sizeof(float), hipMemcpyHostToDevice);
+      auto sg = [&](auto kern, const char* name) {
+        hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        const int r = 32;
+        hipLaunchKernelGGL(kern, dim3(1), dim3(64), lds, 0, in, vals, out, cyc, r);
+        hipLaunchKernelGGL(kern, dim3(1), dim3(64), lds, 0, in, vals, out, cyc, r);
+        long long cw[2];
+        hipMemcpy(cw, cyc, sizeof(cw), hipMemcpyDeviceToHost);
+        printf("{\"case\": \"%s\", \"cycles_per_neighbour\": %.3f, \"ns_per_neighbour\": %.3f, \"err\": \"%s\"}\n",
+               name, (double)cw[0] / (r * 1008.0), 10.0 * (double)cw[1] / (r * 1008.0),
+               hipGetErrorString(hipGetLastError()));
+      };
+      sg(consumer_sgpr_kernel<0>, "sgpr_values_nopf");
+      sg(consumer_sgpr_kernel<4>, "sgpr_values_pf4");
+      sg(consumer_sgpr_kernel<8>, "sgpr_values_pf8");
+    }
     env(consumer_env_kernel<0, 64, 0>, 64, "env_buf0_1wave");
     env(consumer_env_kernel<1, 64, 0>, 64, "env_buf1_1wave");
     env(consumer_env_kernel<0, 512, 0>, 512, "env_buf0_8waves_idle");
