@@ -481,13 +481,51 @@ __device__ __forceinline__ void heavy_row(
 // longest: each slice gathers 1/SLICES of every neighbour row, so its loaders fill a chunk of
 // SLICES x the neighbours per round and the row's chain finishes in fewer rounds. Every slice
 // still applies its features' fmafs in the row's order: the same bits.
+//
+// Fused light rows (small operands, d = 32 / 64 / 128): blocks b >= n_heavy_blocks run the
+// row-parallel kernel's latency form over rows [(b - n_heavy_blocks) R, ... + R) (R rows per
+// block at GROUP lanes per row), skipping the heavy rows (longer than light_skip) exactly as
+// spmm_vec_kernel<D, false, false, true> does. They are dispatched after the heavy blocks, so
+// they fill the CUs the shorter heavy rows free while the longest chains run: one launch per
+// hop instead of two back-to-back (config 2: the light rows' ~15 us per hop ran after the
+// heavy rows' ~40 us). Same fmaf chains: the same bits.
+template <int D>
+__device__ __forceinline__ void light_rows_block(
+    const Csr& A, int64_t lb, int64_t light_skip, const float* __restrict__ x, int64_t ldx,
+    float* __restrict__ y, int64_t ldy, int epi, const float* __restrict__ self, int64_t ld_self,
+    float* __restrict__ acc, int64_t ld_acc, float acc_div) {
+  constexpr int VEC = SpmmLatCfg<D>::VEC, GROUP = D / VEC, RPW = 64 / GROUP;
+  const int lane = threadIdx.x & 63, gl = lane % GROUP;
+  const int64_t r = (lb * (kHeavyThreads / 64) + (threadIdx.x >> 6)) * RPW + lane / GROUP;
+  if (r >= A.n_rows) return;   // the whole row group leaves together
+  const int64_t beg = A.row_ptr[r], end = A.row_ptr[r + 1];
+  if (end - beg > light_skip) return;   // a heavy row: one of this launch's heavy blocks
+  const VecF<VEC> a = gather_row_pipe<VEC, GROUP, SpmmLatCfg<D>::CH>(A.col, A.val, beg, end, x, ldx, gl);
+  if (!(epi & GNNREC_EPI_NO_Y)) stv<VEC>(y + r * ldy + VEC * gl, a);
+  acc_epilogue_v<VEC>(epi, a, self + r * ld_self + VEC * gl, acc + r * ld_acc + VEC * gl, acc_div);
+}
+template <int D> constexpr int kLightRowsPerBlock =
+    (64 / (D / SpmmLatCfg<D>::VEC)) * (kHeavyThreads / 64);
+
 template <int F, int DC, int SLICES, int SF, int SDC>
 __global__ __launch_bounds__(kHeavyThreads) void spmm_heavy_kernel(
-    Csr A, const int64_t* __restrict__ rows, int64_t n_sliced, const float* __restrict__ x,
+    Csr A, const int64_t* __restrict__ rows, int64_t n_sliced, int64_t heavy_first,
+    int64_t n_light_blocks, int64_t light_skip, const float* __restrict__ x,
     int64_t ldx, float* __restrict__ y, int64_t ldy, int d_rt, int epi,
     const float* __restrict__ self, int64_t ld_self, float* __restrict__ acc, int64_t ld_acc,
     float acc_div) {
   int64_t b = blockIdx.x;
+  if constexpr (DC == 32 || DC == 64 || DC == 128) {
+    // dispatch order: heavy blocks [0, heavy_first), the light blocks, the other heavy blocks
+    if (n_light_blocks > 0 && b >= heavy_first) {
+      if (b < heavy_first + n_light_blocks) {
+        light_rows_block<DC>(A, b - heavy_first, light_skip, x, ldx, y, ldy, epi, self, ld_self,
+                             acc, ld_acc, acc_div);
+        return;
+      }
+      b -= n_light_blocks;
+    }
+  }
   if constexpr (SLICES > 1) {
     static_assert(DC > 0 && SDC * SLICES == DC, "sliced instance: SDC = DC / SLICES");
     if (b < n_sliced * SLICES) {
@@ -664,18 +702,32 @@ int heavy_slices(int d, bool small) {
   return 4;   // d = 128 (32-wide), 256 (64-wide)
 }
 
+// light_skip > 0: the launch also runs the light rows (rows of at most light_skip neighbours,
+// d = 32 / 64 / 128 only) as blocks after the heavy ones (see light_rows_block)
 int launch_heavy(const Csr& A, const int64_t* heavy_rows, int64_t n_heavy, int64_t n_sliced,
                  const float* x, int64_t ldx, float* y, int64_t ldy, int d, int epi,
                  const float* self, int64_t ld_self, float* acc, int64_t ld_acc, float acc_div,
-                 bool small, hipStream_t s) {
+                 bool small, int64_t light_skip, hipStream_t s) {
   const int slices = heavy_slices(d, small);
-  const int64_t blocks = n_heavy + n_sliced * (slices - 1);   // a block per slice
+  const int64_t heavy_blocks = n_heavy + n_sliced * (slices - 1);   // a block per slice
+  int64_t light_blocks = 0;
+  if (light_skip > 0) {
+    const int rpb = d == 32 ? kLightRowsPerBlock<32> : d == 64 ? kLightRowsPerBlock<64>
+                                                               : kLightRowsPerBlock<128>;
+    light_blocks = ceil_div(A.n_rows, (int64_t)rpb);
+  }
+  const int64_t blocks = heavy_blocks + light_blocks;
   GNNREC_REQUIRE(blocks < (int64_t)INT32_MAX, "spmm: too many heavy rows");
+  // dispatch order: the sliced (longest) rows' blocks, then the light blocks, then the other
+  // heavy rows (config 2, threshold 256: 0.124 ms per K = 3 propagation against 0.144 with
+  // every heavy block first and 0.141 with the light blocks first, profiles/r06/)
+  const int64_t heavy_first = n_sliced * slices;
   const dim3 grid((unsigned)blocks), block(kHeavyThreads);
 #define GNNREC_HEAVY(F, DC, SL, SF, SDC)                                                          \
   hipLaunchKernelGGL((spmm_heavy_kernel<F, DC, SL, SF, SDC>), grid, block, kHeavyLds, s, A,      \
-                     heavy_rows, n_sliced, x, ldx, y, ldy, d, epi, self, ld_self, acc, ld_acc,    \
-                     acc_div)
+                     heavy_rows, n_sliced, heavy_first, light_blocks, light_skip, x, ldx, y, ldy, \
+                     d, epi,                                                                      \
+                     self, ld_self, acc, ld_acc, acc_div)
   switch (d) {
     case 32: GNNREC_HEAVY(1, 32, 2, 1, 16); break;
     case 64:
@@ -729,7 +781,7 @@ extern "C" int gnnrec_spmm_csr_heavy_f32(const int64_t* row_ptr, const int32_t* 
   GNNREC_REQUIRE(heavy_threshold >= 0 && n_heavy >= 0, "spmm: negative heavy_threshold/n_heavy");
   GNNREC_REQUIRE(n_sliced >= 0 && n_sliced <= n_heavy, "spmm: n_sliced must be in [0, n_heavy]");
   GNNREC_REQUIRE((flags & ~(GNNREC_CSR_FORK | GNNREC_CSR_LIGHT_LATENCY |
-                            GNNREC_CSR_LIGHT_THROUGHPUT)) == 0 &&
+                            GNNREC_CSR_LIGHT_THROUGHPUT | GNNREC_CSR_TWO_LAUNCHES)) == 0 &&
                      (flags & (GNNREC_CSR_LIGHT_LATENCY | GNNREC_CSR_LIGHT_THROUGHPUT)) !=
                          (GNNREC_CSR_LIGHT_LATENCY | GNNREC_CSR_LIGHT_THROUGHPUT),
                  "spmm: bad flags 0x%x", flags);
@@ -769,10 +821,18 @@ extern "C" int gnnrec_spmm_csr_heavy_f32(const int64_t* row_ptr, const int32_t* 
     return check_launch("spmm");
   };
   if (!heavy) return light();
+  // small operands: the light rows as blocks of the heavy launch (one launch per hop), where
+  // the light kernel would run its latency form anyway
+  const bool fused = !(flags & (GNNREC_CSR_FORK | GNNREC_CSR_TWO_LAUNCHES)) && lat && small &&
+                     !x_nonzero && !y_active && (d == 32 || d == 64 || d == 128) &&
+                     vec4_ok(d, x, ldx, y, ldy, epi, self, ld_self, acc, ld_acc);
+  if (fused)
+    return launch_heavy(A, heavy_rows, n_heavy, n_sliced, x, ldx, y, ldy, d, epi, self, ld_self,
+                        acc, ld_acc, acc_div, small, heavy_threshold, s);
   if (!(flags & GNNREC_CSR_FORK)) {
     if (int rc = light()) return rc;
     return launch_heavy(A, heavy_rows, n_heavy, n_sliced, x, ldx, y, ldy, d, epi, self, ld_self,
-                        acc, ld_acc, acc_div, small, s);
+                        acc, ld_acc, acc_div, small, 0, s);
   }
   // Fork / join: the heavy rows (disjoint from the row-parallel kernel's rows) go first, on the
   // high-priority side stream, so their workgroups — the longest chains — start first and the
@@ -783,7 +843,7 @@ extern "C" int gnnrec_spmm_csr_heavy_f32(const int64_t* row_ptr, const int32_t* 
   if (hipEventRecord(ss->fork, s) != hipSuccess || hipStreamWaitEvent(ss->s, ss->fork, 0) != hipSuccess)
     return check_launch("spmm: fork");
   int rc = launch_heavy(A, heavy_rows, n_heavy, n_sliced, x, ldx, y, ldy, d, epi, self, ld_self,
-                        acc, ld_acc, acc_div, small, ss->s);
+                        acc, ld_acc, acc_div, small, 0, ss->s);
   const int rc_light = rc == GNNREC_OK ? light() : rc;
   // join even after a failed launch, so the caller's stream never runs ahead of the side's
   if (hipEventRecord(ss->join, ss->s) != hipSuccess || hipStreamWaitEvent(s, ss->join, 0) != hipSuccess)

@@ -29,6 +29,7 @@ EPI_ACC_X = 16
 CSR_FORK = 1
 CSR_LIGHT_LATENCY = 2
 CSR_LIGHT_THROUGHPUT = 4
+CSR_TWO_LAUNCHES = 8
 # column-ordered hop plan layout (include/gnnrec.h GNNREC_TILED_*)
 TILED_WAVES = 8
 TILED_GROUPS = 8

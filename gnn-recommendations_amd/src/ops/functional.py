@@ -51,7 +51,9 @@ def _csr_args(adj: CsrGraph):
 # by operand size; 0 = none). Round-6 sweeps, every output bit-identical
 # (profiles/r06/config2_knobs_sweep_*.jsonl, powerlaw_knobs_sweep.jsonl):
 #   small operands (<= 65 536 rows, e.g. ML-1M): threshold 128, slices above 1024 — config 2
-#     0.246 -> 0.191 ms per forward (threshold 256 unsliced: 0.215);
+#     0.246 -> 0.191 ms per forward (threshold 256 unsliced: 0.215); with the light rows fused
+#     into the heavy launch (unmasked hops, d = 32 / 64 / 128): threshold 256, slices above
+#     2048 — K = 3 propagation 0.17 -> 0.114 ms (profiles/r06/csr_fused_*.jsonl);
 #   large: threshold 256 (d <= 64) / 512 (d >= 128), slices above 1024 / 4096 — power-law
 #     2M x 2M K=3 d=64 18.98 -> 15.6 ms, d=128 36.4 -> 24.6 ms; G100M's CSR path (no row above
 #     ~200) 21.1 ms at 256 against 21.4 at 128.
@@ -64,14 +66,17 @@ SMALL_OPERAND_ROWS = 65536          # gnnrec_spmm_csr_heavy_f32's own small-oper
 CSR_FLAGS = 0
 
 
-def heavy_knobs(n_rows: int, d: int) -> Tuple[int, int]:
+def heavy_knobs(n_rows: int, d: int, masked: bool = False) -> Tuple[int, int]:
     """(heavy threshold, slice length) for a CSR hop over n_rows destination rows at width d
-    (the module's SPMM_* settings when not None)."""
+    (the module's SPMM_* settings when not None). masked: the hop has x_mask / y_active (the
+    library then keeps its light rows a launch of their own, even on small operands)."""
     small = n_rows <= SMALL_OPERAND_ROWS
+    fused = small and not masked and d in (32, 64, 128) and not (CSR_FLAGS & (
+        _lib.CSR_FORK | _lib.CSR_TWO_LAUNCHES | _lib.CSR_LIGHT_THROUGHPUT))
     ht = SPMM_HEAVY_THRESHOLD if SPMM_HEAVY_THRESHOLD is not None else (
-        128 if small else (256 if d <= 64 else 512))
+        256 if fused else 128 if small else (256 if d <= 64 else 512))
     sl = SPMM_SLICE_LEN if SPMM_SLICE_LEN is not None else (
-        1024 if (small or d <= 64) else 4096)
+        2048 if fused else 1024 if (small or d <= 64) else 4096)
     return ht, sl
 
 
@@ -241,7 +246,7 @@ def tiled_plan_for(adj: CsrGraph, x: torch.Tensor, x_mask=None, y_active=None,
 
 
 def _heavy_args(adj: CsrGraph, x: torch.Tensor, heavy_threshold: int,
-                slice_len: Optional[int] = None):
+                slice_len: Optional[int] = None, masked: bool = False):
     """(heavy_rows ptr, n_heavy, threshold, n_sliced) for the split launch, or the no-split
     tuple. n_sliced: how many of the (longest-first) heavy rows are longer than slice_len
     (None: heavy_knobs; 0: none)."""
@@ -252,7 +257,7 @@ def _heavy_args(adj: CsrGraph, x: torch.Tensor, heavy_threshold: int,
     rows = adj.heavy_rows(heavy_threshold)
     if rows is None:
         return None, 0, 0, 0
-    sl = heavy_knobs(adj.n_rows, d)[1] if slice_len is None else slice_len
+    sl = heavy_knobs(adj.n_rows, d, masked)[1] if slice_len is None else slice_len
     n_sliced = adj.heavy_rows_longer(heavy_threshold, sl) if sl > 0 else 0
     return ptr(rows), rows.numel(), int(heavy_threshold), n_sliced
 
@@ -279,7 +284,8 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
     if x.shape[0] < adj.shape[1]:
         raise ValueError(f"x has {x.shape[0]} rows, operand has {adj.shape[1]} columns")
     L = _lib.lib()
-    ht = heavy_knobs(adj.n_rows, d)[0] if heavy_threshold is None else heavy_threshold
+    masked = x_mask is not None or y_active is not None
+    ht = heavy_knobs(adj.n_rows, d, masked)[0] if heavy_threshold is None else heavy_threshold
     if y_active is not None and (y_active.dtype != torch.uint8 or y_active.device != x.device
                                  or y_active.numel() < adj.n_rows):
         raise ValueError("y_active must be a uint8 tensor on x's device with a byte per "
@@ -297,8 +303,9 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
                                       epi, ptr(self_rows),
                                       self_rows.stride(0) if self_rows is not None else d,
                                       ptr(acc), acc.stride(0) if acc is not None else d,
-                                      float(acc_div), *_heavy_args(adj, x, ht), int(CSR_FLAGS),
-                                      _lib.stream_of(adj.device)), "gnnrec_spmm_csr_heavy_f32")
+                                      float(acc_div), *_heavy_args(adj, x, ht, masked=masked),
+                                      int(CSR_FLAGS), _lib.stream_of(adj.device)),
+          "gnnrec_spmm_csr_heavy_f32")
 
 
 def spmm_tiled_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], plan: dict, *,

@@ -136,9 +136,10 @@ int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col, const
 /* The CSR hop with its heavy rows tuned (ABI 11): gnnrec_spmm_csr_masked_f32 /
  * gnnrec_lightgcn_split_f32 plus
  *  - n_sliced: the first n_sliced entries of heavy_rows (which must then be sorted longest
- *    first, as every caller in this package lists them) run as two workgroups of d/2 features
- *    each (d = 32, 64, 128, 256; ignored for other d): each gathers half of every neighbour
- *    row, so the longest chains finish in fewer LDS rounds. Same bits.
+ *    first, as every caller in this package lists them) run as feature slices, one workgroup
+ *    each (d = 32: 2 x 16 features; d = 64: 4 x 16 on operands of at most 65536 rows, else
+ *    2 x 32; d = 128: 4 x 32; d = 256: 4 x 64; ignored for other d): each gathers its slice of
+ *    every neighbour row, so the longest chains finish in fewer LDS rounds. Same bits.
  *  - flags: GNNREC_CSR_FORK runs the heavy-row kernel on an internal high-priority side
  *    stream forked from and joined back into `stream` with events (capture-safe), so the
  *    row-parallel rows run beside the heavy chains instead of after them (the two write
@@ -146,11 +147,15 @@ int gnnrec_spmm_csr_masked_f32(const int64_t* row_ptr, const int32_t* col, const
  *    caller's stream must belong to the current device). GNNREC_CSR_LIGHT_LATENCY /
  *    _THROUGHPUT force the row-parallel chain's form (default: the latency form — the next
  *    step's indices loaded one step ahead — for operands of at most 65536 rows, whose rows
- *    cannot fill the chip; see csrc/gather.h).
+ *    cannot fill the chip; see csrc/gather.h). On such operands (d = 32 / 64 / 128, no
+ *    x_nonzero / y_active, latency form) the row-parallel rows run as extra workgroups of
+ *    the heavy-row launch, dispatched after the heavy ones: one launch per hop.
+ *    GNNREC_CSR_TWO_LAUNCHES keeps them a launch of their own, before the heavy rows.
  * Replaces the same torch.sparse.mm calls (lightgcn.py:88, ngcf.py:70). */
 #define GNNREC_CSR_FORK 1
 #define GNNREC_CSR_LIGHT_LATENCY 2
 #define GNNREC_CSR_LIGHT_THROUGHPUT 4
+#define GNNREC_CSR_TWO_LAUNCHES 8
 int gnnrec_spmm_csr_heavy_f32(const int64_t* row_ptr, const int32_t* col, const float* val,
                               int64_t n_rows, const float* x, int64_t ldx,
                               const uint8_t* x_nonzero, const uint8_t* y_active, float* y,

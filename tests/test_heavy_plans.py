@@ -90,11 +90,23 @@ def test_row_stats_host():
 
 
 def test_heavy_knobs_by_operand():
-    """functional.heavy_knobs: the round-6 sweeps' choices (small operands 128 / 1024; large ones
-    256 / 1024 at d <= 64 and 512 / 4096 above) and the module overrides."""
+    """functional.heavy_knobs: the round-6 sweeps' choices (small operands 256 / 2048 when the
+    light rows run in the heavy launch, 128 / 1024 for masked hops, other widths or the
+    two-launch flags; large ones 256 / 1024 at d <= 64 and 512 / 4096 above) and the module
+    overrides."""
+    from src.ops import _lib
     from src.ops import functional as F
-    assert F.heavy_knobs(9746, 64) == (128, 1024)
-    assert F.heavy_knobs(65536, 128) == (128, 1024)
+    assert F.heavy_knobs(9746, 64) == (256, 2048)
+    assert F.heavy_knobs(65536, 128) == (256, 2048)
+    assert F.heavy_knobs(9746, 64, masked=True) == (128, 1024)
+    assert F.heavy_knobs(9746, 16) == (128, 1024)
+    saved_flags = F.CSR_FLAGS
+    try:
+        for fl in (_lib.CSR_TWO_LAUNCHES, _lib.CSR_FORK, _lib.CSR_LIGHT_THROUGHPUT):
+            F.CSR_FLAGS = fl
+            assert F.heavy_knobs(9746, 64) == (128, 1024)
+    finally:
+        F.CSR_FLAGS = saved_flags
     assert F.heavy_knobs(4_000_000, 64) == (256, 1024)
     assert F.heavy_knobs(4_000_000, 32) == (256, 1024)
     assert F.heavy_knobs(4_000_000, 128) == (512, 4096)

@@ -127,17 +127,18 @@ def test_tiled_deferred_layer_mean_bit_exact(case, rows_per_block):
 
 
 @pytest.mark.parametrize("light", ["throughput", "latency"])
-@pytest.mark.parametrize("fork", [False, True])
+@pytest.mark.parametrize("launch", ["default", "fork", "two"])
 @pytest.mark.parametrize("heavy,slice_len", [(256, 0), (256, 2048), (128, 512), (16, 16)])
-def test_csr_knobs_bit_exact(case, light, fork, heavy, slice_len):
+def test_csr_knobs_bit_exact(case, light, launch, heavy, slice_len):
     """The round-6 CSR hop knobs (gnnrec_spmm_csr_heavy_f32): the row-parallel chain's
-    latency form, the heavy rows forked onto the side stream beside it, and the longest heavy
-    rows as two half-width feature slices — every combination the reference's bits, per hop
-    (spmm_into) and through the fused K-hop launch."""
+    latency form, the light rows as blocks of the heavy launch (the default on this operand
+    with the latency form), the heavy rows forked onto the side stream or in a launch after
+    the light rows', and the longest heavy rows as feature slices — every combination the
+    reference's bits, per hop (spmm_into) and through the K-hop launch."""
     from src.ops import _lib
     f, g, x0, _, _ = case
     flags = (_lib.CSR_LIGHT_LATENCY if light == "latency" else _lib.CSR_LIGHT_THROUGHPUT) | \
-        (_lib.CSR_FORK if fork else 0)
+        {"default": 0, "fork": _lib.CSR_FORK, "two": _lib.CSR_TWO_LAUNCHES}[launch]
     saved = F.CSR_FLAGS, F.SPMM_SLICE_LEN
     F.CSR_FLAGS, F.SPMM_SLICE_LEN = flags, slice_len
     try:
@@ -171,7 +172,8 @@ def test_sliced_heavy_rows_other_widths(case, d):
     F.spmm_into(g, x, ref, heavy_threshold=0)
     saved = F.CSR_FLAGS, F.SPMM_SLICE_LEN
     try:
-        for flags, sl in ((0, 1024), (_lib.CSR_FORK, 256), (_lib.CSR_FORK, 0)):
+        for flags, sl in ((0, 1024), (0, 2048), (_lib.CSR_TWO_LAUNCHES, 2048),
+                          (_lib.CSR_FORK, 256), (_lib.CSR_FORK, 0)):
             F.CSR_FLAGS, F.SPMM_SLICE_LEN = flags, sl
             y = torch.full_like(ref, float("nan"))
             F.spmm_into(g, x, y, heavy_threshold=256)

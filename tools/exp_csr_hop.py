@@ -32,7 +32,15 @@ ap.add_argument("--one", default=None, metavar="FLAGS:SLICE:HT[,...]",
                      "(for a kernel trace)")
 ap.add_argument("--powerlaw", action="store_true",
                 help="also the power-law 2M x 2M graph (50M pairs, Zipf 0.9) at d = 64 and 128")
+ap.add_argument("--flags", type=int, default=None,
+                help="functional.CSR_FLAGS for the whole run (e.g. 8 = GNNREC_CSR_TWO_LAUNCHES)")
+ap.add_argument("--slice", type=int, default=None,
+                help="functional.SPMM_SLICE_LEN for the whole run")
 a = ap.parse_args()
+if a.flags is not None:
+    F.CSR_FLAGS = a.flags
+if a.slice is not None:
+    F.SPMM_SLICE_LEN = a.slice
 dev = torch.device("cuda", 0)
 lib = os.environ.get("GNNREC_LIB", "default")
 
@@ -78,7 +86,7 @@ with torch.no_grad():
     t, (u, i) = ms_of(lambda: m(g), 100)
     emit(case="config2_model_forward", ms=t, sha=sha(torch.cat([u, i])))
     x0 = m._initial_table().contiguous()
-    for ht in (256, 512, 1024, 4096, 0):
+    for ht in (128, 192, 256, 384, 512, 1024, 4096, 0):
         t, (out, _) = ms_of(lambda: F.lightgcn_forward(g, x0, 3, heavy_threshold=ht), 100)
         emit(case="config2_propagate", heavy_threshold=ht, ms=t, sha=sha(out),
              flags=F.CSR_FLAGS, slice_len=F.SPMM_SLICE_LEN)
