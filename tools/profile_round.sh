@@ -73,7 +73,7 @@ for step in $STEPS; do
           > $OUT/csr_hop.jsonl 2> $OUT/csr_hop.err ;;
     c2kt)
       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/c2kt -o run -- \
-          python3 tools/exp_csr_hop.py --tag $TAG --one ${C2_KNOBS:-0:1024:128} > $OUT/c2kt.jsonl 2> $OUT/c2kt.err
+          python3 tools/exp_csr_hop.py --tag $TAG --one ${C2_KNOBS:-0:2048:256} > $OUT/c2kt.jsonl 2> $OUT/c2kt.err
       cp "$(find $OUT/c2kt -name "*kernel_trace.csv" -print -quit)" $OUT/c2_kernel_trace.csv ;;
     shards)
       timeout -k 10 600 python -u tools/shard_compute.py > $OUT/shard_compute.jsonl 2> $OUT/shard_compute.err ;;
