@@ -64,6 +64,24 @@ SMALL_OPERAND_ROWS = 65536          # gnnrec_spmm_csr_heavy_f32's own small-oper
 # measured slower, the cross-stream join costs ~17 us per hop, profiles/r06/config2_trace/)
 # and the row-parallel chain's form (CSR_LIGHT_*; 0 = by operand size).
 CSR_FLAGS = 0
+# The row-parallel chain's form on large operands (the library picks the latency form by
+# itself up to SMALL_OPERAND_ROWS rows): the latency form (16 lanes x float4 per row, d = 64)
+# when the light rows average at most LIGHT_LATENCY_MAX_AVG neighbours, else the throughput
+# form (a wave per row). tools/exp_light_form.py, profiles/r06/light_form.jsonl (K = 3, d = 64,
+# ms throughput / latency): uniform 2M rows of avg degree 10: 3.50 / 2.64; 25: 5.75 / 6.05;
+# 50: 10.8 / 11.8; 100: 21.2 / 22.9; power-law 2M x 2M (light rows avg 19): 15.0 / 13.2.
+LIGHT_LATENCY_MAX_AVG = 22.0
+
+
+def light_form_flag(adj: CsrGraph, heavy_threshold: int) -> int:
+    """CSR_FLAGS plus _lib.CSR_LIGHT_LATENCY for a large operand whose light rows are short
+    (LIGHT_LATENCY_MAX_AVG), unless CSR_FLAGS already names a form."""
+    fl = int(CSR_FLAGS)
+    if fl & (_lib.CSR_LIGHT_LATENCY | _lib.CSR_LIGHT_THROUGHPUT) or adj.n_rows <= SMALL_OPERAND_ROWS:
+        return fl
+    if adj.light_avg_degree(max(int(heavy_threshold), 0)) <= LIGHT_LATENCY_MAX_AVG:
+        fl |= _lib.CSR_LIGHT_LATENCY
+    return fl
 
 
 def heavy_knobs(n_rows: int, d: int, masked: bool = False) -> Tuple[int, int]:
@@ -304,7 +322,7 @@ def spmm_into(adj: CsrGraph, x: torch.Tensor, y: Optional[torch.Tensor], *, epi:
                                       self_rows.stride(0) if self_rows is not None else d,
                                       ptr(acc), acc.stride(0) if acc is not None else d,
                                       float(acc_div), *_heavy_args(adj, x, ht, masked=masked),
-                                      int(CSR_FLAGS), _lib.stream_of(adj.device)),
+                                      light_form_flag(adj, ht), _lib.stream_of(adj.device)),
           "gnnrec_spmm_csr_heavy_f32")
 
 
@@ -562,7 +580,7 @@ def lightgcn_forward(adj: CsrGraph, x0: torch.Tensor, n_layers: int,
     ht = heavy_knobs(n, d)[0] if heavy_threshold is None else heavy_threshold
     check(L.gnnrec_lightgcn_heavy_f32(*_csr_args(adj), ptr(x0), d, int(n_layers), ptr(work0),
                                       ptr(work1), ptr(layers), ptr(out), d,
-                                      *_heavy_args(adj, x0, ht), int(CSR_FLAGS),
+                                      *_heavy_args(adj, x0, ht), light_form_flag(adj, ht),
                                       _lib.stream_of(adj.device)),
           "gnnrec_lightgcn_heavy_f32")
     return out, layers

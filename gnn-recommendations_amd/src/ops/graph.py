@@ -433,6 +433,19 @@ class CsrGraph:
                 self._plans[key] = int((deg > length).sum())
         return self._plans[key]
 
+    def light_avg_degree(self, threshold: int) -> float:
+        """Mean neighbours of the rows not in heavy_rows(threshold) (cached): picks the
+        row-parallel chain's form on large operands (functional.light_form_flag)."""
+        key = ("light_avg_degree", threshold)
+        if key not in self._plans:
+            rows = self.heavy_rows(threshold) if threshold > 0 else None
+            heavy_nnz, n_heavy = 0, 0
+            if rows is not None:
+                heavy_nnz = int((self.row_ptr[rows + 1] - self.row_ptr[rows]).sum())
+                n_heavy = rows.numel()
+            self._plans[key] = (self.nnz - heavy_nnz) / max(self.n_rows - n_heavy, 1)
+        return self._plans[key]
+
     def row_stats(self, block_rows: int = 0) -> Tuple[int, int]:
         """(longest row, most edges in a block of block_rows consecutive rows): on a device
         graph one gnnrec_csr_row_stats launch and an 16-B read (no torch kernels, whose first

@@ -116,3 +116,39 @@ def test_heavy_knobs_by_operand():
         assert F.heavy_knobs(9746, 64) == (300, 0)
     finally:
         F.SPMM_HEAVY_THRESHOLD, F.SPMM_SLICE_LEN = saved
+
+
+def test_light_form_flag_by_light_row_degree():
+    """functional.light_form_flag: on operands above SMALL_OPERAND_ROWS rows the latency form
+    of the row-parallel chain when the light rows average at most LIGHT_LATENCY_MAX_AVG
+    neighbours (the heavy rows' edges excluded), else the caller's flags unchanged; small
+    operands and an explicit form in CSR_FLAGS are left alone."""
+    from src.ops import _lib
+    from src.ops import functional as F
+    rng = np.random.default_rng(5)
+    nu, ni = 60_000, 20_000
+    sparse = CsrGraph.from_interactions(rng.integers(0, nu, 200_000), rng.integers(0, ni, 200_000),
+                                        nu, ni)
+    assert sparse.n_rows > F.SMALL_OPERAND_ROWS
+    assert sparse.light_avg_degree(0) == pytest.approx(sparse.nnz / sparse.n_rows)
+    rp = sparse.row_ptr.numpy()
+    deg = np.diff(rp)
+    t = int(np.sort(deg)[-10]) - 1   # a handful of heavy rows
+    light = deg[deg <= t]
+    assert sparse.light_avg_degree(t) == pytest.approx(light.sum() / light.size)
+    assert F.light_form_flag(sparse, t) == _lib.CSR_LIGHT_LATENCY
+    dense = CsrGraph.from_interactions(rng.integers(0, nu, 1_200_000),
+                                       rng.integers(0, 1_000, 1_200_000), nu, 1_000)
+    assert dense.light_avg_degree(0) > F.LIGHT_LATENCY_MAX_AVG
+    assert F.light_form_flag(dense, 0) == 0
+    saved = F.CSR_FLAGS
+    try:
+        F.CSR_FLAGS = _lib.CSR_LIGHT_THROUGHPUT
+        assert F.light_form_flag(sparse, t) == _lib.CSR_LIGHT_THROUGHPUT
+        F.CSR_FLAGS = _lib.CSR_FORK
+        assert F.light_form_flag(sparse, t) == _lib.CSR_FORK | _lib.CSR_LIGHT_LATENCY
+    finally:
+        F.CSR_FLAGS = saved
+    small = CsrGraph.from_interactions(rng.integers(0, 500, 5_000), rng.integers(0, 500, 5_000),
+                                       500, 500)
+    assert F.light_form_flag(small, 0) == F.CSR_FLAGS
