@@ -54,9 +54,11 @@ def _csr_args(adj: CsrGraph):
 #     0.246 -> 0.191 ms per forward (threshold 256 unsliced: 0.215); with the light rows fused
 #     into the heavy launch (unmasked hops, d = 32 / 64 / 128): threshold 256, slices above
 #     2048 — K = 3 propagation 0.17 -> 0.114 ms (profiles/r06/csr_fused_*.jsonl);
-#   large: threshold 256 (d <= 64) / 512 (d >= 128), slices above 1024 / 4096 — power-law
-#     2M x 2M K=3 d=64 18.98 -> 15.6 ms, d=128 36.4 -> 24.6 ms; G100M's CSR path (no row above
-#     ~200) 21.1 ms at 256 against 21.4 at 128.
+#   large: threshold 256 (d <= 64) / 512 (d >= 128), slices above 4096 — power-law 2M x 2M
+#     K=3 d=64 18.98 -> 15.6 ms (slices above 1024, throughput-form light rows), 12.9 ms with
+#     the latency-form light rows (light_form_flag) and slices above 4096 (13.2 at 1024,
+#     profiles/r06/powerlaw_knobs_sweep_latency.jsonl); d=128 36.4 -> 24.0 ms; G100M's CSR path
+#     (no row above ~200) 21.1 ms at 256 against 21.4 at 128.
 SPMM_HEAVY_THRESHOLD = None
 SPMM_SLICE_LEN = None
 SMALL_OPERAND_ROWS = 65536          # gnnrec_spmm_csr_heavy_f32's own small-operand bound
@@ -94,7 +96,7 @@ def heavy_knobs(n_rows: int, d: int, masked: bool = False) -> Tuple[int, int]:
     ht = SPMM_HEAVY_THRESHOLD if SPMM_HEAVY_THRESHOLD is not None else (
         256 if fused else 128 if small else (256 if d <= 64 else 512))
     sl = SPMM_SLICE_LEN if SPMM_SLICE_LEN is not None else (
-        2048 if fused else 1024 if (small or d <= 64) else 4096)
+        2048 if fused else 1024 if small else 4096)
     return ht, sl
 
 

@@ -92,7 +92,7 @@ def test_row_stats_host():
 def test_heavy_knobs_by_operand():
     """functional.heavy_knobs: the round-6 sweeps' choices (small operands 256 / 2048 when the
     light rows run in the heavy launch, 128 / 1024 for masked hops, other widths or the
-    two-launch flags; large ones 256 / 1024 at d <= 64 and 512 / 4096 above) and the module
+    two-launch flags; large ones 256 / 4096 at d <= 64 and 512 / 4096 above) and the module
     overrides."""
     from src.ops import _lib
     from src.ops import functional as F
@@ -107,8 +107,8 @@ def test_heavy_knobs_by_operand():
             assert F.heavy_knobs(9746, 64) == (128, 1024)
     finally:
         F.CSR_FLAGS = saved_flags
-    assert F.heavy_knobs(4_000_000, 64) == (256, 1024)
-    assert F.heavy_knobs(4_000_000, 32) == (256, 1024)
+    assert F.heavy_knobs(4_000_000, 64) == (256, 4096)
+    assert F.heavy_knobs(4_000_000, 32) == (256, 4096)
     assert F.heavy_knobs(4_000_000, 128) == (512, 4096)
     saved = F.SPMM_HEAVY_THRESHOLD, F.SPMM_SLICE_LEN
     try:
