@@ -30,6 +30,9 @@ ARCH = "gfx950"
 CFLAGS = [
     "-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17", "-ffp-contract=off",
     "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wall", "-Wno-unused-function",
+    # compressed code-object bundles (the HIP runtime inflates them at load): the library
+    # goes from 9.4 to ~3.5 MB, which every GPU-box push carries
+    "--offload-compress",
 ]
 
 
