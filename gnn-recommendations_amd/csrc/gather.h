@@ -281,11 +281,18 @@ template <> struct SpmmCfg<128> { static constexpr int VEC = 2, CH = 16; };  // 
 #ifndef GNNREC_LAT_VEC64
 #define GNNREC_LAT_VEC64 4
 #endif
+// d = 128 takes 8 gathers per step (a wave per row, 2 features per lane): the power-law
+// 2M x 2M K = 3 propagation 24.0 -> 22.6 ms against 16 (the throughput form's count, which
+// made the two forms the same), config 2 unchanged (profiles/r06/light_chunk_ab.jsonl)
+#ifndef GNNREC_LAT_CH128
+#define GNNREC_LAT_CH128 8
+#endif
 template <int D> struct SpmmLatCfg {
   static constexpr bool OK = (D == 32 || D == 64 || D == 128);
   static constexpr int VEC = D == 64 ? GNNREC_LAT_VEC64 : SpmmCfg<D>::VEC;
   static constexpr int GROUP = D / VEC;
-  static constexpr int CH = GNNREC_LAT_CH < GROUP ? GNNREC_LAT_CH : GROUP;
+  static constexpr int CH_WANT = D == 128 ? GNNREC_LAT_CH128 : GNNREC_LAT_CH;
+  static constexpr int CH = CH_WANT < GROUP ? CH_WANT : GROUP;
 };
 
 // ---- GAS (block-diagonal orthogonal transform + column shuffle) -----------------------
