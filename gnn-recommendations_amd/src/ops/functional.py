@@ -724,8 +724,24 @@ def dense_layer(adj: CsrGraph, x: torch.Tensor, M: torch.Tensor, c_out: float,
     return y if store_y else None
 
 
-GAT_HEAVY_THRESHOLD = 2048   # rows with more neighbours go to the split (segment) path
-GAT_SEGMENT = 1024
+# GAT heavy-row split: rows with more than the threshold's neighbours run as segments of at
+# most `segment` edges (partials merged per row). By operand (gat_knobs): large operands
+# (G1B / 5M x 5M, request-bound) 2048 / 1024; small ones (<= SMALL_OPERAND_ROWS rows, e.g. the
+# reference's ML-1M configs) are latency-bound on their longest per-row chains: 64 / 32 —
+# the ML-1M-shaped GAT forward 1.09 -> 0.28-0.29 ms, outputs within 2.1e-9 of the unsplit
+# kernels' (tools/exp_gat_small.py, profiles/r06/gat_small_knobs.jsonl). An int here forces it.
+GAT_HEAVY_THRESHOLD: Optional[int] = None
+GAT_SEGMENT: Optional[int] = None
+GAT_LARGE_KNOBS = (2048, 1024)
+GAT_SMALL_KNOBS = (64, 32)
+
+
+def gat_knobs(n_rows: int) -> Tuple[int, int]:
+    """(heavy threshold, segment length) of the GAT forward split for an operand of n_rows
+    destination rows (GAT_HEAVY_THRESHOLD / GAT_SEGMENT when set)."""
+    base = GAT_SMALL_KNOBS if n_rows <= SMALL_OPERAND_ROWS else GAT_LARGE_KNOBS
+    return (GAT_HEAVY_THRESHOLD if GAT_HEAVY_THRESHOLD is not None else base[0],
+            GAT_SEGMENT if GAT_SEGMENT is not None else base[1])
 
 
 def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh: torch.Tensor,
@@ -738,9 +754,10 @@ def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh:
     with rows longer than `heavy_threshold` split into segments (gnnrec_gat_heavy_f32).
     shared_rows: `h` is ONE [N, o_dim] table every head aggregates (head_stride 0), e.g. the
     layer input x when W_h is applied after the aggregation. heavy_threshold None:
-    GAT_HEAVY_THRESHOLD at call time; 0: no split."""
+    gat_knobs at call time; 0: no split."""
+    knob_threshold, segment = gat_knobs(adj.n_rows)
     if heavy_threshold is None:
-        heavy_threshold = GAT_HEAVY_THRESHOLD
+        heavy_threshold = knob_threshold
     h = _rowmajor(h)
     # score tables are read in place with their row strides (e.g. columns of the projection
     # output); only a column-strided view is compacted
@@ -753,7 +770,7 @@ def gat_aggregate(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor, s_neigh:
     width = o_dim if mean_heads else heads * o_dim
     if out is None and not (epi & EPI_NO_Y):
         out = torch.empty((adj.n_rows, width), dtype=torch.float32, device=h.device)
-    plan = adj.heavy_plan(heavy_threshold, GAT_SEGMENT) if heavy_threshold > 0 else None
+    plan = adj.heavy_plan(heavy_threshold, segment) if heavy_threshold > 0 else None
     common = (ptr(h), h.stride(0), head_stride, ptr(s_self), ptr(s_neigh), s_self.stride(0),
               s_neigh.stride(0), int(heads),
               int(o_dim), float(slope), int(mean_heads), int(apply_elu), ptr(out),
@@ -807,8 +824,9 @@ def gat_aggregate_att(adj: CsrGraph, h: torch.Tensor, hself: torch.Tensor, att: 
     the self and neighbour attention vectors (shared_rows: the row vectors W_h^T a_h acting on
     the shared o_dim-wide row); hself: the destination rows' own rows of h's layout (row r of
     adj -> hself[r]). No score tables are read: a neighbour costs its feature row only."""
+    knob_threshold, segment = gat_knobs(adj.n_rows)
     if heavy_threshold is None:
-        heavy_threshold = GAT_HEAVY_THRESHOLD
+        heavy_threshold = knob_threshold
     if not gat_att_supported(o_dim):
         raise ValueError(f"gat_aggregate_att: o_dim = {o_dim} unsupported")
     h, hself = _rowmajor(h), _rowmajor(hself)
@@ -826,12 +844,12 @@ def gat_aggregate_att(adj: CsrGraph, h: torch.Tensor, hself: torch.Tensor, att: 
     plan = None
     if heavy_threshold > 0:
         if GAT_SEGMENT_ORDER == "panel":
-            plan = adj.heavy_plan_panels(heavy_threshold, GAT_SEGMENT, GAT_PANEL,
+            plan = adj.heavy_plan_panels(heavy_threshold, segment, GAT_PANEL,
                                          GAT_PANEL_MIN_EDGES)
         elif GAT_SEGMENT_ORDER == "column":
-            plan = adj.heavy_plan_by_column(heavy_threshold, GAT_SEGMENT)
+            plan = adj.heavy_plan_by_column(heavy_threshold, segment)
         else:
-            plan = adj.heavy_plan(heavy_threshold, GAT_SEGMENT)
+            plan = adj.heavy_plan(heavy_threshold, segment)
     common = (ptr(h), h.stride(0), head_stride, ptr(hself), hself.stride(0), ptr(att),
               int(heads), int(o_dim), float(slope), int(mean_heads), int(apply_elu), ptr(out),
               out.stride(0) if out is not None else width, int(epi), ptr(self_rows),
@@ -870,21 +888,36 @@ def gat_train_supported(adj: CsrGraph, heads: int, o_dim: int) -> bool:
 # are cut into segments of at most GAT_TRAIN_SEGMENT edges (CsrGraph.heavy_plan), their partial
 # sums merged per row. 0 disables it (every row one lane group: a 4e5-neighbour hub then takes
 # the whole step, profiles/r06/gat_train_*).
-GAT_TRAIN_HEAVY_THRESHOLD = 2048
-GAT_TRAIN_SEGMENT = 1024
+# By operand (gat_train_knobs): 2048 / 1024 on large operands; 128 / 64 up to
+# SMALL_OPERAND_ROWS rows, where the per-row chains set the time — the ML-1M-shaped GAT training
+# step (forward + backward, attention dropout) 10.8 -> 3.1 ms, loss and gradients equal to
+# fp32 reassociation (tools/exp_gat_train.py --ml1m, profiles/r06/gat_train_ml1m_knobs.jsonl).
+# An int here forces it.
+GAT_TRAIN_HEAVY_THRESHOLD: Optional[int] = None
+GAT_TRAIN_SEGMENT: Optional[int] = None
+GAT_TRAIN_LARGE_KNOBS = (2048, 1024)
+GAT_TRAIN_SMALL_KNOBS = (128, 64)
+
+
+def gat_train_knobs(n_rows: int) -> Tuple[int, int]:
+    """(heavy threshold, segment length) of the GAT training split for n_rows destination rows
+    (GAT_TRAIN_HEAVY_THRESHOLD / GAT_TRAIN_SEGMENT when set)."""
+    base = GAT_TRAIN_SMALL_KNOBS if n_rows <= SMALL_OPERAND_ROWS else GAT_TRAIN_LARGE_KNOBS
+    return (GAT_TRAIN_HEAVY_THRESHOLD if GAT_TRAIN_HEAVY_THRESHOLD is not None else base[0],
+            GAT_TRAIN_SEGMENT if GAT_TRAIN_SEGMENT is not None else base[1])
 
 
 def _gat_train_split_args(adj: CsrGraph, F: int, heads: int, device):
     """(max_row_len, seg_row, seg_beg, seg_end, n_seg, heavy_rows, heavy_seg_ptr, n_heavy,
     work) for the split launches, or the no-split tuple; work is returned separately to keep
     it alive."""
-    plan = (adj.heavy_plan(GAT_TRAIN_HEAVY_THRESHOLD, GAT_TRAIN_SEGMENT)
-            if GAT_TRAIN_HEAVY_THRESHOLD > 0 else None)
+    threshold, segment = gat_train_knobs(adj.n_rows)
+    plan = adj.heavy_plan(threshold, segment) if threshold > 0 else None
     if plan is None:
         return (0, None, None, None, 0, None, None, 0, None), None
     n_seg = plan["seg_row"].numel()
     work = torch.empty(n_seg * (F + 2 * heads) + 4, dtype=torch.float32, device=device)
-    return (int(GAT_TRAIN_HEAVY_THRESHOLD), ptr(plan["seg_row"]), ptr(plan["seg_beg"]),
+    return (int(threshold), ptr(plan["seg_row"]), ptr(plan["seg_beg"]),
             ptr(plan["seg_end"]), n_seg, ptr(plan["heavy_rows"]), ptr(plan["heavy_seg_ptr"]),
             plan["heavy_rows"].numel(), ptr(work)), work
 
@@ -893,7 +926,7 @@ class _GatTrainAggregate(torch.autograd.Function):
     """out[:, q*o:(q+1)*o] = dropout(softmax_j(LeakyReLU(s_self[r,q] + s_neigh[j,q]))) @ h_q —
     one GATLayer's per-head aggregation (gat.py:113-141) with its backward in two native passes;
     h, s_self and s_neigh are the differentiable inputs (the projections stay in autograd).
-    Rows above GAT_TRAIN_HEAVY_THRESHOLD run as merged segments in all three passes; the forward
+    Rows above gat_train_knobs' threshold run as merged segments in all three passes; the forward
     keeps the softmax statistics for the backward."""
 
     @staticmethod

@@ -67,13 +67,13 @@ def test_config3_g100m_ngcf_gas_every_layer_vs_oracle(cuda):
 def slice5(cuda):
     g = bench_configs.powerlaw_graph(2_000_000, 2_000_000, 50_000_000, 0.9, 0, 16)
     deg = np.diff(g.row_ptr.numpy())
-    assert deg.min() >= 1 and deg.max() > F.GAT_HEAVY_THRESHOLD
+    assert deg.min() >= 1 and deg.max() > F.gat_knobs(g.n_rows)[0]
     return g, g.to(cuda), bench_configs.config5_model((2_000_000, 2_000_000), cuda)
 
 
 def test_config5_slice_gat_heads_vs_oracle(cuda, slice5):
     g, gd, m = slice5
-    assert gd.heavy_plan(F.GAT_HEAVY_THRESHOLD, F.GAT_SEGMENT) is not None
+    assert gd.heavy_plan(*F.gat_knobs(gd.n_rows)) is not None
     rp, col = g.row_ptr.numpy(), g.col.numpy()
     with torch.no_grad():
         x = m._initial_table()

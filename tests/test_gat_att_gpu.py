@@ -58,7 +58,7 @@ def test_att_head_major_vs_oracle(cuda, heads, o, heavy):
     att = torch.randn(2, heads, o, device=cuda) * 0.5
     z = F.gat_aggregate_att(gd, feat, feat, att, heads, o, 0.2, heavy_threshold=heavy)
     if heavy:
-        assert gd.heavy_plan(heavy, F.GAT_SEGMENT) is not None
+        assert gd.heavy_plan(heavy, F.gat_knobs(gd.n_rows)[1]) is not None
     np.testing.assert_allclose(z.cpu().numpy(), _oracle(g, feat, att, heads, o, False),
                                rtol=1e-4, atol=1e-6)
 

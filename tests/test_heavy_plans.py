@@ -152,3 +152,22 @@ def test_light_form_flag_by_light_row_degree():
     small = CsrGraph.from_interactions(rng.integers(0, 500, 5_000), rng.integers(0, 500, 5_000),
                                        500, 500)
     assert F.light_form_flag(small, 0) == F.CSR_FLAGS
+
+
+def test_gat_split_knobs_by_operand():
+    """functional.gat_knobs / gat_train_knobs: the GAT heavy-row split on small operands
+    (<= SMALL_OPERAND_ROWS rows: 64 / 32 forward, 128 / 64 training) and large ones (2048 /
+    1024), and the module overrides."""
+    from src.ops import functional as F
+    assert F.gat_knobs(9746) == (64, 32) and F.gat_knobs(20_000_000) == (2048, 1024)
+    assert F.gat_train_knobs(9746) == (128, 64) and F.gat_train_knobs(4_000_000) == (2048, 1024)
+    saved = (F.GAT_HEAVY_THRESHOLD, F.GAT_SEGMENT, F.GAT_TRAIN_HEAVY_THRESHOLD,
+             F.GAT_TRAIN_SEGMENT)
+    try:
+        F.GAT_HEAVY_THRESHOLD, F.GAT_SEGMENT = 0, 7
+        assert F.gat_knobs(9746) == (0, 7) and F.gat_knobs(20_000_000) == (0, 7)
+        F.GAT_TRAIN_HEAVY_THRESHOLD = 300
+        assert F.gat_train_knobs(9746) == (300, 64)
+    finally:
+        (F.GAT_HEAVY_THRESHOLD, F.GAT_SEGMENT, F.GAT_TRAIN_HEAVY_THRESHOLD,
+         F.GAT_TRAIN_SEGMENT) = saved

@@ -208,7 +208,7 @@ def test_gat_heavy_row_split_matches_unsplit(cuda, threshold):
         got = F.gat_aggregate(g, h, ss, sn, heads, o, 0.2, mean, True,
                               heavy_threshold=threshold or 10 ** 9)
         if threshold:
-            assert g.heavy_plan(threshold, F.GAT_SEGMENT) is not None
+            assert g.heavy_plan(threshold, F.gat_knobs(g.n_rows)[1]) is not None
         torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
     # and with a segment length smaller than the rows
     old = F.GAT_SEGMENT

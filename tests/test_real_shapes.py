@@ -38,7 +38,7 @@ def test_gat_heavy_fixture_shape():
     from src.ops import functional as F
     m, f, g = gat_heavy()
     deg = np.diff(g.row_ptr.numpy())
-    assert int((deg > F.GAT_HEAVY_THRESHOLD).sum()) >= 2 and deg.min() >= 1
+    assert int((deg > F.GAT_LARGE_KNOBS[0]).sum()) >= 2 and deg.min() >= 1
     with torch.no_grad():
         u, i = m(g.to_torch_sparse_coo())
     np.testing.assert_allclose(u.numpy(), f["user_out"], rtol=1e-5, atol=1e-6)

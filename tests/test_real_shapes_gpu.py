@@ -78,7 +78,7 @@ def test_gat_heavy_rows_match_reference(cuda, monkeypatch, threshold):
     m, f, g = gat_heavy()
     g = g.to(cuda)
     if threshold:
-        assert g.heavy_plan(threshold, F.GAT_SEGMENT) is not None
+        assert g.heavy_plan(threshold, F.gat_knobs(g.n_rows)[1]) is not None
     m = m.to(cuda)
     with torch.no_grad():
         u, i = m(g)
