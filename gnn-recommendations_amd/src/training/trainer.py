@@ -75,6 +75,17 @@ def batch_rows(n_users: int, n_items: int, users, pos_items, neg_items) -> torch
     return need
 
 
+def _row_subset_pays(adj) -> bool:
+    """The row-subset forward skips most rows of the last hops on a large operand; on a small
+    one (at most functional.SMALL_OPERAND_ROWS rows, e.g. ML-1M) a full hop is one ~40 us
+    launch and marking the rows costs more: the ML-1M-shaped LightGCN step 1.31-1.32 ms with
+    the subset, 1.13-1.15 ms without, alternating runs (tools/exp_train_ml1m.py,
+    profiles/r06/train_ml1m.jsonl). Same loss and gradient bits either way."""
+    from ..ops import functional as F
+    n = getattr(adj, "n_rows", None)
+    return n is None or n > F.SMALL_OPERAND_ROWS
+
+
 def train_step(model: nn.Module, adj, users, pos_items, neg_items, optimizer,
                loss_fn: Optional[nn.Module] = None, max_grad_norm: float = 1.0,
                row_subset: bool = True) -> torch.Tensor:
@@ -82,9 +93,10 @@ def train_step(model: nn.Module, adj, users, pos_items, neg_items, optimizer,
     Returns the loss as a 0-d device tensor (no host sync). The loss reads only the batch's
     rows of the propagated table, so with `row_subset` a model with `forward_rows` computes
     just those (and what they depend on): the same loss and gradient bits as the full
-    propagation the reference runs (trainer.py:251-254)."""
+    propagation the reference runs (trainer.py:251-254); on small operands the full
+    propagation is cheaper and is used (_row_subset_pays)."""
     loss_fn = loss_fn or BPRLoss()
-    if row_subset and hasattr(model, "forward_rows"):
+    if row_subset and hasattr(model, "forward_rows") and _row_subset_pays(adj):
         need = batch_rows(model.n_users, model.n_items, users, pos_items, neg_items)
         user_emb, item_emb = model.forward_rows(adj, need)
     elif hasattr(model, "get_all_embeddings"):

@@ -98,3 +98,15 @@ def test_bpr_scores_shapes():
     ue, ie = torch.randn(4, 8), torch.randn(6, 8)
     p, n = bpr_scores(ue, ie, torch.tensor([0, 1]), torch.tensor([2, 3]), torch.tensor([[4], [5]]))
     assert p.shape == (2,) and n.shape == (2, 1)
+
+
+def test_row_subset_only_on_large_operands():
+    """train_step's row-subset forward is used above functional.SMALL_OPERAND_ROWS rows only
+    (on small operands the full propagation is cheaper; the bits are the same either way)."""
+    from types import SimpleNamespace
+
+    from src.ops import functional as F
+    from src.training import trainer
+    assert not trainer._row_subset_pays(SimpleNamespace(n_rows=9746))
+    assert trainer._row_subset_pays(SimpleNamespace(n_rows=F.SMALL_OPERAND_ROWS + 1))
+    assert trainer._row_subset_pays(object())   # an operand without a row count (torch sparse)

@@ -21,9 +21,12 @@ def test_three_adam_steps_native_match_reference(cuda, opt):
     np.testing.assert_allclose(m.item_embedding.weight.detach().cpu().numpy(), f["item_w"], atol=2e-5)
 
 
-def test_row_subset_step_same_bits_as_full_propagation(cuda):
+def test_row_subset_step_same_bits_as_full_propagation(cuda, monkeypatch):
     """The training forward computes only the batch's rows (and their neighbourhoods): the
-    loss and the updated weights are bit-identical to the full propagation's."""
+    loss and the updated weights are bit-identical to the full propagation's. (train_step
+    skips the subset on operands this small, trainer._row_subset_pays; forced on here.)"""
+    from src.training import trainer
+    monkeypatch.setattr(trainer, "_row_subset_pays", lambda adj: True)
     g, _, _ = _golden_graph()
     gd = g.to(cuda)
     _, m1, l1 = _run_steps(gd, cuda, row_subset=True)
