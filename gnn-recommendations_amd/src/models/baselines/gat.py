@@ -269,7 +269,8 @@ class GATLayer(nn.Module):
         The dropout mask's seed is drawn from torch's generator (torch.manual_seed makes runs
         repeatable)."""
         H, o = self.n_heads, self.out_dim
-        h = torch.cat([w(x) for w in self.W], dim=1)                       # [N, H*o]
+        # (row-chunked weight gradients, ops.functional.linear_rows)
+        h = torch.cat([ops.functional.linear_rows(x, w) for w in self.W], dim=1)   # [N, H*o]
         hs = h.view(-1, H, o)
         a_s = torch.stack([a[:, 0] for a in self.a_self])                  # [H, o]
         a_n = torch.stack([a[:, 0] for a in self.a_neigh])

@@ -44,7 +44,11 @@ class NGCFLayer(nn.Module):
                                   self.W2.bias, self.activation.negative_slope,
                                   gas_blocks=blocks, gas_perm=perm, fused=self.single_kernel)
         n = ops.sparse_mm(a, x)
-        out = self.W1(n) + self.W2(x * n)
+        if isinstance(a, CsrGraph):   # device path: row-chunked weight gradients (training)
+            lin = ops.functional.linear_rows
+            out = lin(n, self.W1) + lin(x * n, self.W2)
+        else:
+            out = self.W1(n) + self.W2(x * n)
         out = self.dropout(self.activation(out))
         return gas(out) if gas is not None else out
 

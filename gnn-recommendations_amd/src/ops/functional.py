@@ -982,6 +982,64 @@ def gat_aggregate_train(adj: CsrGraph, h: torch.Tensor, s_self: torch.Tensor,
                                     o_dim, slope, drop_p, seed & 0xFFFFFFFF)
 
 
+# ---- Linear layers whose weight gradient reduces over every row (training) -----------------
+# nn.Linear's weight gradient dW = dY^T X is a [out, in] product with an N-long reduction: one
+# library GEMM gives it one or two output tiles that each walk all N rows (64 x 64 over 2M rows
+# 2.93 ms). Cut into row chunks as one batched GEMM plus a sum over the chunks it is 0.23 ms,
+# and closer to the float64 value (tools/exp_linear_dw.py, profiles/r06/linear_dw.jsonl:
+# 9 746 rows 0.073 -> 0.054 ms, 200K 0.40 -> 0.058 ms). Forward and input gradient are
+# nn.Linear's own ops. Below SMALL_OPERAND_ROWS rows the autograd Function's own overhead
+# outweighs the GEMM it saves (ML-1M-shaped NGCF step 2.1 -> 3.2 ms with it), so those keep
+# nn.Linear; config 5's 2M x 2M GAT training step 222.8 -> 176.9 ms
+# (profiles/r06/gat_train_slice_linear_rows.jsonl, same loss and gradient sums).
+LINEAR_SPLIT_K_MIN_ROWS = 65536
+
+
+def _dw_split_k(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """dy^T x ([out, in]) as chunked partial products summed over the chunks."""
+    n = dy.shape[0]
+    chunk = max(256, (n // 512) // 64 * 64)
+    c = n // chunk
+    w = torch.bmm(dy[:c * chunk].view(c, chunk, -1).transpose(1, 2),
+                  x[:c * chunk].view(c, chunk, -1)).sum(0)
+    if c * chunk < n:
+        w = w + dy[c * chunk:].t() @ x[c * chunk:]
+    return w
+
+
+class _LinearRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return torch.nn.functional.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = (dy2 @ weight).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            dw = (_dw_split_k(dy2, x2) if dy2.shape[0] >= LINEAR_SPLIT_K_MIN_ROWS
+                  else dy2.t() @ x2)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy2.sum(0)
+        return dx, dw, db
+
+
+def linear_rows(x: torch.Tensor, layer: torch.nn.Linear) -> torch.Tensor:
+    """layer(x) with the weight gradient reduced over row chunks (_dw_split_k) on a ROCm
+    device when x has at least LINEAR_SPLIT_K_MIN_ROWS rows and autograd needs it; the
+    forward is nn.Linear's. Otherwise layer(x) itself."""
+    if not (x.is_cuda and torch.is_grad_enabled() and layer.weight.requires_grad
+            and x.reshape(-1, x.shape[-1]).shape[0] >= LINEAR_SPLIT_K_MIN_ROWS):
+        return layer(x)
+    return _LinearRows.apply(x, layer.weight, layer.bias)
+
+
 def rows_gemm_supported(k: int, p: int) -> bool:
     """(k, p) shapes gnnrec_rows_gemm_f32 has an instance for (csrc/dense_epi.hip)."""
     return k in (64, 128, 256) and p % 4 == 0 and 0 < p <= (80 if k == 64 else 64)

@@ -110,3 +110,26 @@ def test_row_subset_only_on_large_operands():
     assert not trainer._row_subset_pays(SimpleNamespace(n_rows=9746))
     assert trainer._row_subset_pays(SimpleNamespace(n_rows=F.SMALL_OPERAND_ROWS + 1))
     assert trainer._row_subset_pays(object())   # an operand without a row count (torch sparse)
+
+
+@pytest.mark.parametrize("n,bias", [(5000, True), (70_000, False), (300, True)])
+def test_linear_rows_gradients_match_nn_linear(n, bias):
+    """functional._LinearRows (the row-chunked weight gradient behind linear_rows): the same
+    forward bits as nn.Linear and gradients within fp32 reassociation, with a row count that
+    is not a multiple of the chunk."""
+    from src.ops import functional as F
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(64, 48, bias=bias)
+    x = torch.randn(n, 64, requires_grad=True)
+    g = torch.randn(n, 48)
+    y_ref = lin(x)
+    (y_ref * g).sum().backward()
+    ref = [x.grad.clone(), lin.weight.grad.clone()] + ([lin.bias.grad.clone()] if bias else [])
+    x.grad = None
+    lin.zero_grad()
+    y = F._LinearRows.apply(x, lin.weight, lin.bias)
+    assert torch.equal(y, y_ref)
+    (y * g).sum().backward()
+    got = [x.grad, lin.weight.grad] + ([lin.bias.grad] if bias else [])
+    for a, b in zip(got, ref):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4 * float(b.abs().max()))

@@ -26,6 +26,8 @@ ap.add_argument("--shape", type=int, nargs=3, default=[2_000_000, 2_000_000, 50_
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--dropout", type=float, default=0.1)
 ap.add_argument("--ml1m", action="store_true", help="config 2's ML-1M-shaped operand instead")
+ap.add_argument("--split-k-ab", action="store_true",
+                help="also time the steps with the library weight-gradient GEMM (no row chunks)")
 ap.add_argument("--train-knobs", nargs="*", default=[],
                 help="GAT_TRAIN_HEAVY_THRESHOLD:GAT_TRAIN_SEGMENT settings to time in turn")
 a = ap.parse_args()
@@ -54,7 +56,11 @@ def step():
 
 from src.ops import functional as F  # noqa: E402
 
-for knob in a.train_knobs or [None]:
+runs = [(k, None) for k in (a.train_knobs or [None])]
+if a.split_k_ab:
+    runs = [(k, mn) for k in (a.train_knobs or [None]) for mn in (10 ** 12, None)]
+for knob, split_min in runs:
+    F.LINEAR_SPLIT_K_MIN_ROWS = split_min if split_min is not None else 4096
     if knob is not None:
         F.GAT_TRAIN_HEAVY_THRESHOLD, F.GAT_TRAIN_SEGMENT = (int(v) for v in knob.split(":"))
     torch.manual_seed(5)
@@ -72,6 +78,7 @@ for knob in a.train_knobs or [None]:
     print(json.dumps({"case": "gat_train_step", "shape": a.shape, "nnz": g.nnz,
                       "max_degree": int(deg.max()), "dropout": a.dropout,
                       "train_knobs": list(F.gat_train_knobs(g.n_rows)),
+                      "weight_grad": "library" if split_min else "row_chunks",
                       "ms_median": ts[len(ts) // 2], "ms_samples": ts, "loss": float(loss.detach()),
                       "grad_abs_sum": float(grads.abs().sum()),
                       "loss_finite": bool(torch.isfinite(loss).item())}), flush=True)
