@@ -59,8 +59,9 @@ from src.ops import functional as F  # noqa: E402
 runs = [(k, None) for k in (a.train_knobs or [None])]
 if a.split_k_ab:
     runs = [(k, mn) for k in (a.train_knobs or [None]) for mn in (10 ** 12, None)]
+split_default = F.LINEAR_SPLIT_K_MIN_ROWS
 for knob, split_min in runs:
-    F.LINEAR_SPLIT_K_MIN_ROWS = split_min if split_min is not None else 4096
+    F.LINEAR_SPLIT_K_MIN_ROWS = split_min if split_min is not None else split_default
     if knob is not None:
         F.GAT_TRAIN_HEAVY_THRESHOLD, F.GAT_TRAIN_SEGMENT = (int(v) for v in knob.split(":"))
     torch.manual_seed(5)
