@@ -183,10 +183,12 @@ def test_sliced_heavy_rows_other_widths(case, d):
 
 
 def test_sliced_heavy_rows_large_operand(cuda):
-    """Above 65 536 rows the d = 64 heavy rows slice into two 32-feature (whole-line) pieces
-    and the row-parallel kernel takes its throughput form: a 100K-row power-law operand with
-    rows of several thousand neighbours, every knob combination bit-identical to the plain
-    row-parallel chain (heavy=0), at d = 64 and 128."""
+    """Above 65 536 rows the d = 64 heavy rows slice into two 32-feature (whole-line) pieces,
+    and the row-parallel kernel's form follows the light rows' degree (functional
+    light_form_flag: this operand's light rows are short, so the latency form): a 100K-row
+    power-law operand with rows of several thousand neighbours, every knob combination — both
+    light-row forms forced, the fork — bit-identical to the plain row-parallel chain
+    (heavy=0), at d = 64 and 128."""
     from src.ops import _lib
     rng = np.random.default_rng(11)
     nu, ni, n = 60_000, 40_000, 1_500_000
@@ -194,6 +196,7 @@ def test_sliced_heavy_rows_large_operand(cuda):
     users = rng.integers(0, nu, n)
     g = CsrGraph.from_interactions(users, items, nu, ni).to(cuda)
     assert g.n_rows > 65_536 and g.max_degree() > 4096
+    assert F.light_form_flag(g, 128) & _lib.CSR_LIGHT_LATENCY
     saved = F.CSR_FLAGS, F.SPMM_SLICE_LEN
     try:
         for d in (64, 128):
@@ -202,6 +205,7 @@ def test_sliced_heavy_rows_large_operand(cuda):
             ref = torch.empty(g.n_rows, d, device=cuda)
             F.spmm_into(g, x, ref, heavy_threshold=0)
             for flags, sl, ht in ((0, 1024, 128), (0, 0, 256), (_lib.CSR_LIGHT_LATENCY, 512, 256),
+                                  (_lib.CSR_LIGHT_THROUGHPUT, 4096, 256),
                                   (_lib.CSR_FORK, 1024, 128)):
                 F.CSR_FLAGS, F.SPMM_SLICE_LEN = flags, sl
                 y = torch.full_like(ref, float("nan"))
