@@ -202,3 +202,26 @@ def test_sharded_step_deferred_mean_same_bits(cuda, monkeypatch):
     for losses, emb in res[1:]:
         assert losses == res[0][0]
         assert torch.equal(emb, res[0][1])
+
+
+def test_linear_rows_on_device_matches_nn_linear(cuda):
+    """functional.linear_rows on a ROCm device above LINEAR_SPLIT_K_MIN_ROWS rows (the
+    row-chunked weight gradient, NGCF / GAT training): nn.Linear's forward bits and its
+    gradients within fp32 reassociation."""
+    from src.ops import functional as F
+    torch.manual_seed(0)
+    n = F.LINEAR_SPLIT_K_MIN_ROWS + 12_345
+    lin = torch.nn.Linear(64, 64).to(cuda)
+    x = torch.randn(n, 64, device=cuda, requires_grad=True)
+    g = torch.randn(n, 64, device=cuda)
+    y_ref = lin(x)
+    (y_ref * g).sum().backward()
+    ref = [x.grad.clone(), lin.weight.grad.clone(), lin.bias.grad.clone()]
+    x.grad = None
+    lin.zero_grad()
+    y = F.linear_rows(x, lin)
+    assert y.grad_fn is not None and "LinearRows" in type(y.grad_fn).__name__
+    assert torch.equal(y, y_ref)
+    (y * g).sum().backward()
+    for a, b in zip([x.grad, lin.weight.grad, lin.bias.grad], ref):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4 * float(b.abs().max()))
